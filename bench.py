@@ -1,0 +1,219 @@
+"""Headline benchmark: frames/sec + Gaussians-splatted/sec of the
+project -> bin -> sort -> blend -> BGR8 frame path at 1920x1080 on a synthetic
+1M-Gaussian SH-3 scene (BASELINE.json configs[2]; configs[3] for N > 1:
+framebuffer tile rows split into N bands, one RCCL all-gather per frame).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  A "step" is one full frame.  The timed region
+covers K frames enqueued back to back (inputs resident in HBM), bracketed by a
+barrier + device synchronise; the value is K / max-over-ranks elapsed.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--tile", type=int, default=16)
+    ap.add_argument("--scale-div", type=float, default=1.0)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--sh-degree", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    return ap.parse_args()
+
+
+def alg_bytes(kernel: str, st: dict, n: int, px: int) -> float:
+    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md)."""
+    T, P = st["n_tiles"], st["n_pairs"]
+    return {
+        "project": n * (56 + 52),
+        "scan": T * 12,
+        "emit": n * 12 + P * 12,
+        "sort": P * 24,
+        "blend": T * 8 + P * (4 + 36) + px * (16 + 3),
+    }[kernel]
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("bench.py --gpus N>1 must be launched with torchrun / torch.distributed.run")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from gaussian_splat_ipu_amd import camera, scene
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    W, H, TW = a.width, a.height, a.tile
+    ply = scene.synthetic(scene.SynthSpec(n=a.n, seed=a.seed, sh_degree=a.sh_degree))
+    g, bb = scene.prepare_scene(ply)
+    del ply
+    view, proj = camera.headless(bb, W, H)
+    fb = TiledFramebuffer(W, H, TW, TW)
+    s = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=True)
+    s.set_view_wire(view)
+    s.set_projection_wire(proj)
+    s.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
+    stream = torch.cuda.current_stream()
+    s.set_stream(stream.cuda_stream)
+
+    band_bytes = fb.rows_per_band_padded(world) * W * 3
+    band = torch.empty(band_bytes, dtype=torch.uint8, device="cuda")
+    frame = torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") if world > 1 else None
+
+    def one_frame():
+        s.execute_async()
+        if world > 1:
+            s.copy_bgr8_device(band.data_ptr(), band_bytes)
+            dist.all_gather_into_tensor(frame, band)
+
+    # warm-up (the first blocking render sizes the pair buffer)
+    s.execute()
+    for _ in range(a.warmup):
+        one_frame()
+    s.sync()
+    torch.cuda.synchronize()
+    s.reset_kernel_times()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one_frame()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    s.sync()  # raises on pair overflow
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = s.stats()
+    kt = s.kernel_times()
+    fps = a.steps / elapsed
+    ms_per_step = 1e3 * elapsed / a.steps
+
+    # per-kernel roofline of this rank's band (rank 0 reports)
+    px = st["band_rows"] * W
+    kern = {}
+    for name, (avg_ms, cnt) in kt.items():
+        b = alg_bytes(name, st, a.n, px)
+        kern[name] = {
+            "avg_ms": round(avg_ms, 5),
+            "launches": int(cnt),
+            "alg_bytes": int(b),
+            "alg_GBps": round(b / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None,
+        }
+    dom = max(kern, key=lambda k: kern[k]["avg_ms"])
+    pmc = None
+    if os.path.exists(a.pmc_json):
+        try:
+            pm = json.load(open(a.pmc_json))
+            if pm.get("config") == f"{a.n}@{W}x{H}/t{TW}/w{world}" and dom in pm.get("kernels", {}):
+                pmc = pm["kernels"][dom].get("hbm_bytes_per_launch")
+        except Exception:
+            pmc = None
+    dk = kern[dom]
+    achieved = dk["alg_GBps"]
+    roofline = {
+        "bound": "hbm",
+        "kernel": dom,
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "traffic": pmc,
+        "alg_bytes_per_launch": dk["alg_bytes"],
+        "avg_launch_ms": dk["avg_ms"],
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O
+
+        threads = min(16, os.cpu_count() or 1)
+        f = O.make_frame(view, proj, W, H, TW, TW, camera.FOV_DEFAULT, a.scale_div)
+        O.render(g, f, nthreads=threads, want_rgba=False)  # warm (page-in)
+        tc0 = time.perf_counter()
+        for _ in range(a.cpu_frames):
+            O.render(g, f, nthreads=threads, want_rgba=False)
+        tc = (time.perf_counter() - tc0) / a.cpu_frames
+        cpu = {
+            "value": round(1.0 / tc, 4),
+            "unit": "frames/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"{a.cpu_frames} full frames of the same {a.n}-Gaussian {W}x{H} workload through the "
+            f"CPU oracle Gaussian rasteriser (OpenMP, {threads} threads)",
+            "gaussians_per_sec": round(a.n / tc, 1),
+        }
+
+    if rank == 0:
+        out = {
+            "metric": "frames/sec + Gaussians-splatted/sec at 1080p, 1M-Gaussian scene, 1/2/4/8 MI355X",
+            "value": round(fps, 3),
+            "unit": "frames/s",
+            "gaussians_per_sec": round(fps * a.n, 1),
+            "pairs_per_sec": round(fps * st["n_pairs"] * world, 1) if world == 1 else None,
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded xoshiro256**, INRIA 3DGS layout, SH degree 3; parity semantics use DC only)",
+            "config": {
+                "workload": f"synthetic {a.n} Gaussians, {W}x{H}, {TW}x{TW} tiles, headless camera, fxy[1]={a.scale_div}",
+                "gaussians": a.n,
+                "resolution": [W, H],
+                "tile": [TW, TW],
+                "parallelism": f"row-band x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+            },
+            "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "max_list", "n_tiles", "n_big_tiles")},
+            "kernels": kern,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    s.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,586 @@
+// gs_kernels.hip -- the frame path as hand-written HIP for gfx950 (MI355X).
+//
+//   project  one thread per Gaussian: MVP transform, clip-space EWA covariance,
+//            eigenvalue radius, guard band + z cull, conic, tile rectangle,
+//            per-tile list lengths (global atomics)
+//            reference: codelets.cpp:437-499, ipu_geometry.hpp:247-383
+//   scan     one workgroup: exclusive scan of the per-tile lengths
+//   emit     one thread per Gaussian: scatter (depth key << 32 | index) into
+//            its tiles' segments (the converged lattice of codelets.cpp:194-293,
+//            507-602 in one frame)
+//   sort     one workgroup per tile: bitonic sort of the tile's keys in LDS;
+//            lists longer than kSortLdsCap go to a block-wide LSD radix sort
+//            with wave64 ballot multisplit ranking
+//            reference: codelets.cpp:295-356 (per-tile quicksort by clip z)
+//   blend    one wave per 64-pixel chunk of a tile: front-to-back alpha
+//            compositing with the Gaussian records read by wave-uniform
+//            (scalar) loads; RGBA f32 + BGR8 stores fused
+//            reference: codelets.cpp:358-421, ipu_rasteriser.cpp:131-144
+//
+// Arithmetic: fp32 everywhere, compiled with -ffp-contract=off and the default
+// correctly rounded divide / sqrt, so every expression below performs exactly
+// the IEEE operations written (and matches the CPU oracle bit for bit).
+#include "gs_kernels.hpp"
+
+namespace gsk {
+namespace {
+
+// --------------------------------------------------------------- math
+// Shared expf specification (oracle/gs_oracle.cpp: or_expf): Cody-Waite
+// reduction + degree-6 polynomial; fmaf is one fused op on both sides.
+__device__ __forceinline__ float gs_expf(float x) {
+  // branch-free: clamp into the finite range, evaluate, then select the
+  // NaN / overflow / underflow results (same selects in the oracle)
+  float xc = (x != x) ? 0.0f : x;
+  xc = (xc < -104.0f) ? -104.0f : xc;
+  xc = (xc > 89.0f) ? 89.0f : xc;
+  const float k = __builtin_rintf(xc * 1.44269502162933349609f);
+  float r = __builtin_fmaf(k, -0.693145751953125f, xc);
+  r = __builtin_fmaf(k, -1.428606765330187045e-06f, r);
+  float p = 1.9875691500e-4f;
+  p = __builtin_fmaf(p, r, 1.3981999507e-3f);
+  p = __builtin_fmaf(p, r, 8.3334519073e-3f);
+  p = __builtin_fmaf(p, r, 4.1665795894e-2f);
+  p = __builtin_fmaf(p, r, 1.6666665459e-1f);
+  p = __builtin_fmaf(p, r, 5.0000001201e-1f);
+  const float r2 = r * r;
+  p = __builtin_fmaf(p, r2, r);
+  p = p + 1.0f;
+  int ki = (int)k;
+  const bool lo = ki < -125;
+  p = lo ? p * 5.42101086242752217004e-20f : p;  // 2^-64
+  ki = lo ? ki + 64 : ki;
+  const bool hi = ki > 127;
+  p = hi ? p * 2.0f : p;
+  ki = hi ? ki - 1 : ki;
+  float res = p * __uint_as_float((uint32_t)(ki + 127) << 23);
+  res = (x < -103.972084045410f) ? 0.0f : res;
+  res = (x > 88.72283935546875f) ? __builtin_huge_valf() : res;
+  return (x != x) ? x : res;
+}
+
+// blend variant: the argument is known <= 0 and not NaN-producing paths are
+// kept identical (same ops, same order) -- only the overflow branch is dead.
+__device__ __forceinline__ float gs_expf_nonpos(float x) { return gs_expf(x); }
+
+__device__ __forceinline__ float smax(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float smin(float a, float b) { return a < b ? a : b; }
+
+struct M3 {
+  float m[3][3];  // glm column-major: m[c][r]
+};
+
+// glm mat3 * mat3: (A[0][r]*B[c][0] + A[1][r]*B[c][1]) + A[2][r]*B[c][2]
+__device__ __forceinline__ M3 m3_mul(const M3& A, const M3& B) {
+  M3 R;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float s = A.m[0][r] * B.m[c][0];
+      s = s + A.m[1][r] * B.m[c][1];
+      s = s + A.m[2][r] * B.m[c][2];
+      R.m[c][r] = s;
+    }
+  return R;
+}
+
+__device__ __forceinline__ M3 m3_t(const M3& A) {
+  M3 R;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) R.m[c][r] = A.m[r][c];
+  return R;
+}
+
+// glm mat4 * vec4 row r: (m0*x + m1*y) + (m2*z + m3*w)
+__device__ __forceinline__ float mv_row(const float* m, int r, float x, float y, float z, float w) {
+  const float a = m[0 * 4 + r] * x + m[1 * 4 + r] * y;
+  const float b = m[2 * 4 + r] * z + m[3 * 4 + r] * w;
+  return a + b;
+}
+
+// Gaussian3D::ComputeCov3D (ipu_geometry.hpp:315-323) with scale already
+// divided by fxy[1] (codelets.cpp:463).
+__device__ __forceinline__ M3 cov3d(float4 q4, float sx, float sy, float sz) {
+  const float qw = q4.x, qx = q4.y, qy = q4.z, qz = q4.w;  // glm::quat(w, x, y, z)
+  const float dot = (qw * qw + qx * qx) + (qy * qy + qz * qz);
+  const float len = __builtin_sqrtf(dot);
+  float w, x, y, z;
+  if (len <= 0.0f) {
+    w = 1.0f; x = 0.0f; y = 0.0f; z = 0.0f;
+  } else {
+    const float inv = 1.0f / len;
+    w = qw * inv; x = qx * inv; y = qy * inv; z = qz * inv;
+  }
+  const float qxx = x * x, qyy = y * y, qzz = z * z;
+  const float qxz = x * z, qxy = x * y, qyz = y * z;
+  const float qwx = w * x, qwy = w * y, qwz = w * z;
+  M3 R;
+  R.m[0][0] = 1.0f - 2.0f * (qyy + qzz);
+  R.m[0][1] = 2.0f * (qxy + qwz);
+  R.m[0][2] = 2.0f * (qxz - qwy);
+  R.m[1][0] = 2.0f * (qxy - qwz);
+  R.m[1][1] = 1.0f - 2.0f * (qxx + qzz);
+  R.m[1][2] = 2.0f * (qyz + qwx);
+  R.m[2][0] = 2.0f * (qxz + qwy);
+  R.m[2][1] = 2.0f * (qyz - qwx);
+  R.m[2][2] = 1.0f - 2.0f * (qxx + qyy);
+  M3 S;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) S.m[c][r] = 0.0f;
+  S.m[0][0] = gs_expf(sx);
+  S.m[1][1] = gs_expf(sy);
+  S.m[2][2] = gs_expf(sz);
+  return m3_mul(m3_mul(m3_mul(R, S), m3_t(S)), m3_t(R));
+}
+
+__device__ __forceinline__ uint32_t depth_key_of(float z) {
+  // order-preserving: ascending float z <-> ascending key (z < 0 here)
+  const uint32_t b = __float_as_uint(z);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+constexpr uint2 kEmptyRect = {1u, 1u};  // tx0 = 1 > tx1 = 0
+
+// ------------------------------------------------------------------ project
+__global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= fp.n) return;
+  const float4 mean = b.mean[i];
+  const float4 col = b.colour[i];
+  const float4 rot = b.rot[i];
+  const float4 sg = b.scale_gid[i];
+  float4* rec = b.rec + 3 * (size_t)i;
+  uint2 rect = kEmptyRect;
+  uint32_t dkey = 0xFFFFFFFFu;
+  if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
+    const float* m = fp.mvp;
+    // clip = mvp * mean (codelets.cpp:460)
+    const float cx = mv_row(m, 0, mean.x, mean.y, mean.z, mean.w);
+    const float cy = mv_row(m, 1, mean.x, mean.y, mean.z, mean.w);
+    const float cz = mv_row(m, 2, mean.x, mean.y, mean.z, mean.w);
+    const float cw = mv_row(m, 3, mean.x, mean.y, mean.z, mean.w);
+    // Viewport::clipSpaceToViewport (viewport.hpp:21-35)
+    const float s = 0.5f / cw;
+    float vx = cx * s, vy = cy * s;
+    vx = vx + 0.5f;
+    vy = vy + 0.5f;
+    vx = vx * fp.W;
+    vy = vy * fp.H;
+    vx = vx + 0.0f;
+    vy = vy + 0.0f;
+    // ComputeCov2D (ipu_geometry.hpp:333-383): t = mv * (mean.xyz, 1)
+    float tx = mv_row(m, 0, mean.x, mean.y, mean.z, 1.0f);
+    float ty = mv_row(m, 1, mean.x, mean.y, mean.z, 1.0f);
+    const float tz = mv_row(m, 2, mean.x, mean.y, mean.z, 1.0f);
+    const float limx = 1.3f * fp.tanfov;
+    const float limy = 1.3f * fp.tanfov;
+    const float txtz = tx / tz;
+    const float tytz = ty / tz;
+    tx = smin(limx, smax(-limx, txtz)) * tz;
+    ty = smin(limy, smax(-limy, tytz)) * tz;
+    M3 J;
+    J.m[0][0] = fp.focal_x / tz;
+    J.m[0][1] = 0.0f;
+    J.m[0][2] = -(fp.focal_x * tx) / (tz * tz);
+    J.m[1][0] = 0.0f;
+    J.m[1][1] = fp.focal_y / tz;
+    J.m[1][2] = -(fp.focal_y * ty) / (tz * tz);
+    J.m[2][0] = 0.0f;
+    J.m[2][1] = 0.0f;
+    J.m[2][2] = 0.0f;
+    M3 W;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) W.m[c][r] = m[c * 4 + r];
+    const M3 T = m3_mul(W, J);
+    const M3 C3 = cov3d(rot, sg.x / fp.scale_div, sg.y / fp.scale_div, sg.z / fp.scale_div);
+    M3 cov = m3_mul(m3_mul(m3_t(T), m3_t(C3)), T);
+    const float a = cov.m[0][0] + 0.3f;
+    const float bb = cov.m[0][1];
+    const float c = cov.m[1][1] + 0.3f;
+    // ComputeEigenvalues / GetBoundingBox (ipu_geometry.hpp:247-276)
+    const float det = a * c - bb * bb;
+    const float mid = 0.5f * (a + c);
+    const float l1 = mid + __builtin_sqrtf(smax(0.1f, mid * mid - det));
+    const float l2 = mid - __builtin_sqrtf(smax(0.1f, mid * mid - det));
+    const float radius = __builtin_ceilf(3.0f * __builtin_sqrtf(smax(l1, l2)));
+    const float minx = vx - radius, miny = vy - radius;
+    const float maxx = vx + radius, maxy = vy + radius;
+    const float ddx = maxx - minx, ddy = maxy - miny;
+    const bool within = __builtin_sqrtf(ddx * ddx + ddy * ddy) < fp.guard_thr;
+    // ComputeConicOpacity (ipu_geometry.hpp:278-286)
+    float k0 = 0.0f, k1 = 0.0f, k2 = 0.0f, k3 = 0.0f;
+    const float cdet = a * c - bb * bb;
+    if (!(cdet == 0.0f)) {
+      const float inv = 1.0f / cdet;
+      k0 = c * inv;
+      k1 = -bb * inv;
+      k2 = a * inv;
+      k3 = col.w;
+    }
+    rec[0] = make_float4(vx, vy, k0, k1);
+    rec[1] = make_float4(k2, k3, col.x, col.y);
+    rec[2] = make_float4(col.z, radius, cz, 0.0f);
+    if (within && cz < 0.0f) {  // codelets.cpp:493
+      atomicAdd(&b.counters[2], 1u);
+      dkey = depth_key_of(cz);
+      // converged lattice rectangle
+      float fx0 = __builtin_floorf(__builtin_floorf(minx) / fp.tw);
+      float fx1 = __builtin_floorf(__builtin_ceilf(maxx) / fp.tw);
+      float fy0 = __builtin_floorf(__builtin_floorf(miny) / fp.th);
+      float fy1 = __builtin_floorf(__builtin_ceilf(maxy) / fp.th);
+      const float gx1 = (float)(fp.tiles_x - 1);
+      const float gy0 = (float)fp.band_ty0, gy1 = (float)(fp.band_ty1 - 1);
+      if (fx0 < 0.0f) fx0 = 0.0f;
+      if (fx1 > gx1) fx1 = gx1;
+      if (fy0 < gy0) fy0 = gy0;
+      if (fy1 > gy1) fy1 = gy1;
+      if (fx0 <= fx1 && fy0 <= fy1) {
+        const uint32_t x0 = (uint32_t)(int)fx0, x1 = (uint32_t)(int)fx1;
+        const uint32_t y0 = (uint32_t)((int)fy0 - fp.band_ty0);
+        const uint32_t y1 = (uint32_t)((int)fy1 - fp.band_ty0);
+        rect = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
+        for (uint32_t y = y0; y <= y1; ++y)
+          for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&b.tile_count[y * fp.tiles_x + x], 1u);
+      }
+    }
+  } else {
+    rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    rec[1] = make_float4(0.0f, 0.0f, col.x, col.y);
+    rec[2] = make_float4(col.z, 0.0f, 0.0f, 0.0f);
+  }
+  b.rect[i] = rect;
+  b.depth_key[i] = dkey;
+}
+
+// --------------------------------------------------------------------- scan
+// One workgroup of 1024 threads: tile_start = exclusive scan(tile_count).
+__global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long wsum[16];
+  __shared__ uint32_t wmax[16];
+  const int T = fp.n_tiles;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (T + 1023) / 1024;
+  const int beg = min(T, tid * per), end = min(T, beg + per);
+  unsigned long long sum = 0;
+  uint32_t mx = 0;
+  for (int i = beg; i < end; ++i) {
+    const uint32_t v = b.tile_count[i];
+    sum += v;
+    mx = max(mx, v);
+  }
+  // wave inclusive scan
+  unsigned long long inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+  if (lane == 63) wsum[wave] = inc;
+  if (lane == 0) wmax[wave] = mx;
+  __syncthreads();
+  unsigned long long base = 0;
+  for (int w = 0; w < wave; ++w) base += wsum[w];
+  unsigned long long run = base + inc - sum;  // exclusive prefix of this thread
+  for (int i = beg; i < end; ++i) {
+    b.tile_start[i] = (uint32_t)run;
+    b.tile_cursor[i] = (uint32_t)run;
+    run += b.tile_count[i];
+  }
+  if (tid == 1023) {
+    unsigned long long total = 0;
+    uint32_t m = 0;
+    for (int w = 0; w < 16; ++w) {
+      total += wsum[w];
+      m = max(m, wmax[w]);
+    }
+    b.tile_start[T] = (uint32_t)(total < 0xFFFFFFFFull ? total : 0xFFFFFFFFull);
+    b.counters[3] = total > fp.pair_cap ? 1u : 0u;
+    b.counters[4] = m;
+    b.counters[5] = (uint32_t)total;
+    b.counters[6] = (uint32_t)(total >> 32);
+  }
+}
+
+// --------------------------------------------------------------------- emit
+__global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= fp.n) return;
+  const uint2 r = b.rect[i];
+  const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+  if (x0 > x1) return;
+  const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | (uint32_t)i;
+  for (uint32_t y = y0; y <= y1; ++y)
+    for (uint32_t x = x0; x <= x1; ++x) {
+      const uint32_t pos = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], 1u);
+      if (pos < fp.pair_cap) b.pairs[pos] = key;
+    }
+}
+
+// --------------------------------------------------------------------- sort
+__device__ __forceinline__ void tile_segment(const FrameParams& fp, const Buffers& b, int t,
+                                             uint32_t& s, uint32_t& L) {
+  uint32_t st = b.tile_start[t], en = b.tile_start[t + 1];
+  const unsigned long long cap = fp.pair_cap;
+  if (en > cap) en = (uint32_t)cap;
+  if (st > en) st = en;
+  s = st;
+  L = en - st;
+}
+
+// Small and medium lists: bitonic network over the padded power-of-two list
+// in LDS (32 KB), 256 threads.  Keys are unique (the index is in the low
+// word), so the order is total and deterministic.
+__global__ __launch_bounds__(256) void gs_sort_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long keys[kSortLdsCap];
+  const int t = blockIdx.x;
+  const int tid = threadIdx.x;
+  uint32_t s, L;
+  tile_segment(fp, b, t, s, L);
+  if (L == 0) return;
+  if (L > (uint32_t)kSortLdsCap) {
+    if (tid == 0) b.big_tiles[atomicAdd(&b.counters[0], 1u)] = (uint32_t)t;
+    return;
+  }
+  if (L == 1) {
+    if (tid == 0) b.list[s] = (uint32_t)b.pairs[s];
+    return;
+  }
+  uint32_t n2 = 2;
+  while (n2 < L) n2 <<= 1;
+  for (uint32_t i = tid; i < n2; i += 256) keys[i] = i < L ? b.pairs[s + i] : ~0ull;
+  __syncthreads();
+  for (uint32_t k = 2; k <= n2; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = tid; i < (n2 >> 1); i += 256) {
+        const uint32_t lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+        const uint32_t hi = lo + j;
+        const bool asc = (lo & k) == 0;
+        const unsigned long long x = keys[lo], y = keys[hi];
+        if ((x > y) == asc) {
+          keys[lo] = y;
+          keys[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = tid; i < L; i += 256) b.list[s + i] = (uint32_t)keys[i];
+}
+
+// Large lists: a block-wide stable LSD radix sort (8 passes x 8 bits) over the
+// tile's segment in global memory, pairs <-> pairs_alt.  Ranking inside each
+// 1024-key chunk: wave64 ballot multisplit (8 ballots give each lane the mask
+// of lanes holding the same digit), then a per-digit prefix over the 16 waves.
+// Workgroups pull big tiles from a counter until none is left.
+__global__ __launch_bounds__(1024) void gs_sort_big_kernel(FrameParams fp, Buffers b) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t wcnt[16][256];
+  __shared__ uint32_t s_item;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  const uint32_t n_big = b.counters[0];
+  for (;;) {
+    if (tid == 0) s_item = atomicAdd(&b.counters[1], 1u);
+    __syncthreads();
+    const uint32_t item = s_item;
+    __syncthreads();
+    if (item >= n_big) break;
+    const int t = (int)b.big_tiles[item];
+    uint32_t s, L;
+    tile_segment(fp, b, t, s, L);
+    unsigned long long* src = b.pairs + s;
+    unsigned long long* dst = b.pairs_alt + s;
+    for (int pass = 0; pass < 8; ++pass) {
+      const int shift = pass * 8;
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < L; i += 1024) atomicAdd(&hist[(uint32_t)(src[i] >> shift) & 255u], 1u);
+      __syncthreads();
+      const bool trivial = hist[(uint32_t)(src[0] >> shift) & 255u] == L;
+      if (trivial) {
+        __syncthreads();
+        continue;  // every key has the same digit: order unchanged
+      }
+      if (wave == 0) {  // exclusive scan of 256 bins, 4 per lane
+        uint32_t v[4], tot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k] = hist[lane * 4 + k];
+          tot += v[k];
+        }
+        uint32_t inc = tot;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t o = __shfl_up(inc, d, 64);
+          if (lane >= d) inc += o;
+        }
+        uint32_t run = inc - tot;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          base[lane * 4 + k] = run;
+          run += v[k];
+        }
+      }
+      __syncthreads();
+      for (uint32_t c0 = 0; c0 < L; c0 += 1024) {
+        const uint32_t i = c0 + tid;
+        const bool valid = i < L;
+        const unsigned long long key = valid ? src[i] : 0ull;
+        const uint32_t d = (uint32_t)(key >> shift) & 255u;
+        unsigned long long m = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+          const bool set = (d >> bit) & 1u;
+          const unsigned long long bb = __ballot(set);
+          m &= set ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & lt_mask);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wcnt[wave][lane * 4 + k] = 0;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t chunk_tot = 0;
+        if (tid < 256) {
+          uint32_t run = 0;
+#pragma unroll
+          for (int w = 0; w < 16; ++w) {
+            const uint32_t c = wcnt[w][tid];
+            wcnt[w][tid] = run;
+            run += c;
+          }
+          chunk_tot = run;
+        }
+        __syncthreads();
+        if (valid) dst[base[d] + wcnt[wave][d] + rank] = key;
+        __syncthreads();
+        if (tid < 256) base[tid] += chunk_tot;
+        __syncthreads();
+      }
+      unsigned long long* tmp = src;
+      src = dst;
+      dst = tmp;
+    }
+    for (uint32_t i = tid; i < L; i += 1024) b.list[s + i] = (uint32_t)src[i];
+    __syncthreads();
+  }
+}
+
+// -------------------------------------------------------------------- blend
+__device__ __forceinline__ uint8_t to_u8(float v) {
+  // cv::min(v * 255, 255) -> convertTo(CV_8U): round half to even, saturate
+  float x = v * 255.0f;
+  x = (255.0f < x) ? 255.0f : x;
+  if (x != x) return 0;
+  const float r = __builtin_rintf(x);
+  if (r < 0.0f) return 0;
+  if (r > 255.0f) return 255;
+  return (uint8_t)r;
+}
+
+// One wave = 64 consecutive pixels (tile-local index x + y*tw) of one tile;
+// the wave walks the tile's depth-sorted list with wave-uniform (SMEM) loads
+// of the index and the 48-B record and stops when all its pixels saturate.
+__global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wid = blockIdx.x * 4 + wave;
+  const int tile = wid / fp.chunks_per_tile;
+  const int chunk = wid - tile * fp.chunks_per_tile;
+  if (tile >= fp.n_tiles) return;
+  const int lane = threadIdx.x & 63;
+  const int lp = chunk * 64 + lane;
+  const int lx = lp % fp.tile_w, ly = lp / fp.tile_w;
+  const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
+  const int px = tx * fp.tile_w + lx;
+  const int py = (fp.band_ty0 + tyb) * fp.tile_h + ly;
+  const bool valid = lp < fp.tile_w * fp.tile_h && px < fp.width && py < fp.height;
+  const float pfx = (float)px, pfy = (float)py;
+
+  uint32_t s, L;
+  tile_segment(fp, b, tile, s, L);
+  const uint32_t* __restrict__ list = b.list + s;
+  const float* __restrict__ recf = reinterpret_cast<const float*>(b.rec);
+
+  float T = 1.0f;
+  float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
+  bool done = !valid;
+  for (uint32_t k = 0; k < L; ++k) {
+    if (__ballot(!done) == 0ull) break;
+    const uint32_t g = __builtin_amdgcn_readfirstlane(list[k]);
+    if (g >= (uint32_t)fp.n) continue;  // defensive: never read past the records
+    const float* r = recf + 12 * (size_t)g;
+    const float mx = r[0], my = r[1], k0 = r[2], k1 = r[3];
+    const float k2 = r[4], k3 = r[5], cr = r[6], cg = r[7];
+    const float cb = r[8];
+    if (k3 == 0.0f) continue;  // con_o.w == 0 (codelets.cpp:389)
+    if (!done) {
+      const float dx = mx - pfx;
+      const float dy = my - pfy;
+      const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
+      if (!(power > 0.0f)) {
+        const float v = k3 * gs_expf_nonpos(power);
+        const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
+        if (!(alpha < 1.0f / 255.0f)) {
+          const float test_T = T * (1.0f - alpha);
+          if (test_T < 0.0001f) {
+            done = true;  // break (codelets.cpp:406-408)
+          } else {
+            C0 = C0 + (cr * alpha) * T;  // colour += gCont * alpha * T
+            C1 = C1 + (cg * alpha) * T;
+            C2 = C2 + (cb * alpha) * T;
+            C3 = C3 + (k3 * alpha) * T;
+            T = test_T;
+          }
+        }
+      }
+    }
+  }
+  if (!valid) return;
+  const int row = py - fp.band_py0;
+  const float o0 = 0.0f + C0, o1 = 0.0f + C1, o2 = 0.0f + C2, o3 = 0.0f + C3;
+  if (fp.write_rgba) b.rgba[(size_t)row * fp.width + px] = make_float4(o0, o1, o2, o3);
+  uint8_t* dst = b.bgr + (size_t)row * fp.bgr_pitch + 3 * (size_t)px;
+  dst[0] = to_u8(o2);  // RGBA2BGR
+  dst[1] = to_u8(o1);
+  dst[2] = to_u8(o0);
+}
+
+}  // namespace
+
+void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (fp.n == 0) return;
+  gs_project_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+}
+
+void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  gs_scan_kernel<<<1, 1024, 0, s>>>(fp, b);
+}
+
+void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (fp.n == 0) return;
+  gs_emit_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+}
+
+void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (fp.n_tiles == 0) return;
+  gs_sort_kernel<<<fp.n_tiles, 256, 0, s>>>(fp, b);
+  gs_sort_big_kernel<<<64, 1024, 0, s>>>(fp, b);
+}
+
+void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
+  if (waves == 0) return;
+  gs_blend_kernel<<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(fp, b);
+}
+
+}  // namespace gsk

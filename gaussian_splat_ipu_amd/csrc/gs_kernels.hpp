@@ -1,0 +1,70 @@
+// gs_kernels.hpp -- launch interface of the HIP kernels of the frame path
+// (project -> bin -> sort -> blend).  Internal to libgsplat.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gsk {
+
+// Per-frame constants, passed by value as kernel arguments.
+struct FrameParams {
+  float mvp[16];      // proj * view, glm column-major (codelets.cpp:443)
+  float tanfov;       // (float)tan(0.5 * fxy[0])   (codelets.cpp:444)
+  float focal_x;      // W / (2 tanf(fxy[0]/2))    (codelets.cpp:447)
+  float focal_y;
+  float guard_thr;    // tb.diagonal().length() * clipSize (codelets.cpp:470)
+  float scale_div;    // fxy[1]                    (codelets.cpp:463)
+  float W, H;         // viewport (codelets.cpp:621)
+  float tw, th;       // tile size as float (tile_config.hpp:57-71)
+  int width, height;
+  int tile_w, tile_h;
+  int tiles_x;        // ceil(W / tw)
+  int band_ty0;       // first tile row of this band (absolute)
+  int band_ty1;       // one past the last tile row of this band
+  int band_py0;       // first pixel row of this band
+  int band_rows;      // pixel rows of this band (<= (ty1-ty0)*th)
+  int n;              // Gaussians
+  int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
+  int chunks_per_tile;  // ceil(tw*th / 64): one wave per 64-pixel chunk
+  unsigned long long pair_cap;
+  int write_rgba;
+  int bgr_pitch;      // bytes per row of the BGR8 output
+};
+
+// Device workspace of one renderer.
+struct Buffers {
+  // scene (SoA of the 64-B Gaussian3D record, ipu_geometry.hpp:305-311)
+  const float4* mean;       // x y z w
+  const float4* colour;     // r g b opacity
+  const float4* rot;        // quaternion (w x y z)
+  const float4* scale_gid;  // sx sy sz gid
+  // per-Gaussian projection outputs
+  float4* rec;              // 3 x float4: mx my cx cy | cz cw r g | b radius clipz 0
+  uint32_t* depth_key;      // order-preserving key of clip z
+  uint2* rect;              // (tx0 | tx1 << 16, ty0 | ty1 << 16), band-relative rows
+  // binning
+  uint32_t* tile_count;     // [n_tiles]      (memset 0 each frame)
+  uint32_t* tile_start;     // [n_tiles + 1]
+  uint32_t* tile_cursor;    // [n_tiles]
+  unsigned long long* pairs;      // [pair_cap]  (depth_key << 32 | index)
+  unsigned long long* pairs_alt;  // [pair_cap]  scratch of the large-list sort
+  uint32_t* list;           // [pair_cap]  depth-sorted Gaussian indices
+  uint32_t* big_tiles;      // [n_tiles]
+  uint32_t* counters;       // [8]: 0 n_big, 1 big_next, 2 n_rendered, 3 overflow,
+                            //      4 max_list, 5 n_pairs (low), 6 n_pairs (high)
+  // outputs
+  float4* rgba;             // band_rows x width, row-major
+  uint8_t* bgr;             // band rows (padded) x width x 3
+};
+
+constexpr int GS_STAGE_EVENTS = 6;  // profile events: before project .. after blend
+constexpr int kSortLdsCap = 4096;  // largest tile list sorted in LDS by one workgroup
+
+void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s);
+void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s);
+void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s);
+void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s);
+void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s);
+
+}  // namespace gsk

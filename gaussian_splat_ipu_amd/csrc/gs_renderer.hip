@@ -1,0 +1,656 @@
+// gs_renderer.hip -- host side of the C ABI (include/gsplat.h): the MI355X
+// replacement of splat::IpuSplatter (src/splat/ipu_rasteriser.cpp).
+//
+// Owns one device's copy of the scene (SoA, uploaded once like the reference's
+// "write_verts" program, ipu_rasteriser.cpp:401-418), the per-frame workspace
+// and the outputs, and enqueues the five stages of the frame on one HIP
+// stream.  No exceptions cross the ABI; failures return a gs_status and set the
+// thread-local message of gs_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gsplat.h"
+#include "gs_kernels.hpp"
+#include "host/gs_host.hpp"
+
+using gsh::set_error;
+
+namespace {
+
+constexpr int kProfileRing = 64;
+
+struct ProfileSlot {
+  hipEvent_t ev[gsk::GS_STAGE_EVENTS];
+  bool pending = false;
+};
+
+}  // namespace
+
+struct gs_renderer {
+  gs_config cfg{};
+  int device = 0;
+  size_t n = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+
+  // frame inputs (row-major as on the reference's wire)
+  float view_rm[16];
+  float proj_rm[16];
+  float fov = 0.6981317f;  // glm::radians(40.f) (splat.cpp:170)
+  float scale_div = 0.1f;  // lambda1 / 10 with lambda1 = 1 (InterfaceServer.hpp:238)
+
+  // geometry
+  int tiles_x = 0, tiles_y = 0, band_ty0 = 0, band_ty1 = 0, band_py0 = 0, band_rows = 0;
+  int band_rows_padded = 0, n_tiles = 0;
+  uint64_t pair_cap = 0;
+
+  // device memory
+  void* d_scene = nullptr;      // 4 x float4 x n
+  void* d_gauss = nullptr;      // rec (48 B) + depth key (4 B) + rect (8 B) per Gaussian
+  void* d_zero = nullptr;       // counters[16] + tile_count[n_tiles] (memset every frame)
+  void* d_tiles = nullptr;      // tile_start[n_tiles+1], tile_cursor, big_tiles
+  void* d_pairs = nullptr;      // pairs, pairs_alt, list
+  void* d_out = nullptr;        // rgba f32 + bgr8
+  size_t zero_bytes = 0;
+  size_t bgr_bytes = 0;
+  gsk::Buffers buf{};
+
+  // host mirrors
+  uint32_t* h_counters = nullptr;  // pinned mirror of d_zero: counters[16] + tile_count[T]
+  std::vector<uint32_t> hist_snapshot;
+  std::mutex hist_mu;
+  bool frame_pending = false;
+  bool have_frame = false;
+  gs_frame_stats stats{};
+
+  // profiling
+  bool profile = false;
+  ProfileSlot ring[kProfileRing];
+  int ring_head = 0;
+  double k_ms[GS_K_COUNT] = {0};
+  uint64_t k_launches[GS_K_COUNT] = {0};
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return GS_EOOM;
+  return GS_EDEVICE;
+}
+
+#define GS_HIP(call)                                  \
+  do {                                                \
+    hipError_t e_ = (call);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #call); \
+  } while (0)
+
+int select_device(gs_renderer* r) {
+  GS_HIP(hipSetDevice(r->device));
+  return GS_OK;
+}
+
+void free_pairs(gs_renderer* r) {
+  if (r->d_pairs) (void)hipFree(r->d_pairs);
+  r->d_pairs = nullptr;
+}
+
+int alloc_pairs(gs_renderer* r, uint64_t cap) {
+  free_pairs(r);
+  const size_t bytes = (size_t)cap * (8 + 8 + 4);
+  GS_HIP(hipMalloc(&r->d_pairs, bytes));
+  r->pair_cap = cap;
+  char* p = (char*)r->d_pairs;
+  r->buf.pairs = (unsigned long long*)p;
+  r->buf.pairs_alt = (unsigned long long*)(p + (size_t)cap * 8);
+  r->buf.list = (uint32_t*)(p + (size_t)cap * 16);
+  return GS_OK;
+}
+
+void release(gs_renderer* r) {
+  if (!r) return;
+  (void)hipSetDevice(r->device);
+  if (r->stream) (void)hipStreamSynchronize(r->stream);
+  for (void* p : {r->d_scene, r->d_gauss, r->d_zero, r->d_tiles, r->d_out})
+    if (p) (void)hipFree(p);
+  free_pairs(r);
+  if (r->h_counters) (void)hipHostFree(r->h_counters);
+  for (auto& s : r->ring)
+    for (auto& e : s.ev)
+      if (e) (void)hipEventDestroy(e);
+  if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
+}
+
+gsk::FrameParams make_params(const gs_renderer* r) {
+  gsk::FrameParams fp{};
+  // mvp = projmatrix * viewmatrix, both from the row-major wire format
+  // (codelets.cpp:625-628, 443): glm::transpose(glm::make_mat4(p)).
+  float view[16], proj[16];
+  gsh::mat4_transpose(r->view_rm, view);
+  gsh::mat4_transpose(r->proj_rm, proj);
+  gsh::mat4_mul(proj, view, fp.mvp);
+  // codelets.cpp:444-448
+  fp.tanfov = (float)std::tan(0.5 * (double)r->fov);
+  const float tf = std::tan(r->fov / 2.0f);
+  fp.focal_x = (float)r->cfg.width / (2.0f * tf);
+  fp.focal_y = (float)r->cfg.height / (2.0f * tf);
+  const uint32_t gw = r->cfg.guard_tile_width ? r->cfg.guard_tile_width : r->cfg.tile_width;
+  const uint32_t gh = r->cfg.guard_tile_height ? r->cfg.guard_tile_height : r->cfg.tile_height;
+  const float gx = (float)gw, gy = (float)gh;
+  fp.guard_thr = std::sqrt(gx * gx + gy * gy) * r->cfg.guard_band;  // codelets.cpp:470
+  fp.scale_div = r->scale_div;
+  fp.W = (float)r->cfg.width;
+  fp.H = (float)r->cfg.height;
+  fp.tw = (float)r->cfg.tile_width;
+  fp.th = (float)r->cfg.tile_height;
+  fp.width = (int)r->cfg.width;
+  fp.height = (int)r->cfg.height;
+  fp.tile_w = (int)r->cfg.tile_width;
+  fp.tile_h = (int)r->cfg.tile_height;
+  fp.tiles_x = r->tiles_x;
+  fp.band_ty0 = r->band_ty0;
+  fp.band_ty1 = r->band_ty1;
+  fp.band_py0 = r->band_py0;
+  fp.band_rows = r->band_rows;
+  fp.n = (int)r->n;
+  fp.n_tiles = r->n_tiles;
+  fp.chunks_per_tile = (int)((r->cfg.tile_width * r->cfg.tile_height + 63) / 64);
+  fp.pair_cap = r->pair_cap;
+  fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
+  fp.bgr_pitch = (int)r->cfg.width * 3;
+  return fp;
+}
+
+int profile_harvest(gs_renderer* r, ProfileSlot& s) {
+  if (!s.pending) return GS_OK;
+  GS_HIP(hipEventSynchronize(s.ev[gsk::GS_STAGE_EVENTS - 1]));
+  for (int k = 0; k < GS_K_COUNT; ++k) {
+    float ms = 0.0f;
+    GS_HIP(hipEventElapsedTime(&ms, s.ev[k], s.ev[k + 1]));
+    r->k_ms[k] += ms;
+    r->k_launches[k] += 1;
+  }
+  s.pending = false;
+  return GS_OK;
+}
+
+int enqueue_frame(gs_renderer* r) {
+  // several frames may be in flight on the stream; the host mirrors always
+  // hold the last one's counters after gs_sync
+  const gsk::FrameParams fp = make_params(r);
+  hipStream_t s = r->stream;
+  ProfileSlot* slot = nullptr;
+  if (r->profile) {
+    slot = &r->ring[r->ring_head];
+    r->ring_head = (r->ring_head + 1) % kProfileRing;
+    int rc = profile_harvest(r, *slot);
+    if (rc != GS_OK) return rc;
+  }
+  GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, s));
+  if (slot) GS_HIP(hipEventRecord(slot->ev[0], s));
+  gsk::launch_project(fp, r->buf, s);
+  if (slot) GS_HIP(hipEventRecord(slot->ev[1], s));
+  gsk::launch_scan(fp, r->buf, s);
+  if (slot) GS_HIP(hipEventRecord(slot->ev[2], s));
+  gsk::launch_emit(fp, r->buf, s);
+  if (slot) GS_HIP(hipEventRecord(slot->ev[3], s));
+  gsk::launch_sort(fp, r->buf, s);
+  if (slot) GS_HIP(hipEventRecord(slot->ev[4], s));
+  gsk::launch_blend(fp, r->buf, s);
+  if (slot) {
+    GS_HIP(hipEventRecord(slot->ev[5], s));
+    slot->pending = true;
+  }
+  GS_HIP(hipGetLastError());
+  // counters and per-tile list lengths are adjacent: one small D2H copy
+  GS_HIP(hipMemcpyAsync(r->h_counters, r->d_zero, (16 + (size_t)r->n_tiles) * 4,
+                        hipMemcpyDeviceToHost, s));
+  r->frame_pending = true;
+  return GS_OK;
+}
+
+int finish_frame(gs_renderer* r) {
+  if (!r->frame_pending) return GS_OK;
+  GS_HIP(hipStreamSynchronize(r->stream));
+  r->frame_pending = false;
+  const uint32_t* c = r->h_counters;
+  const uint64_t P = (uint64_t)c[5] | ((uint64_t)c[6] << 32);
+  r->stats.n_gaussians = r->n;
+  r->stats.n_rendered = c[2];
+  r->stats.n_pairs = P;
+  r->stats.max_list = c[4];
+  r->stats.pair_capacity = r->pair_cap;
+  r->stats.n_big_tiles = c[0];
+  if (c[3]) {
+    set_error("pair list overflow: " + std::to_string(P) + " pairs > capacity " +
+              std::to_string(r->pair_cap));
+    return GS_EOVERFLOW;
+  }
+  {
+    std::lock_guard<std::mutex> lk(r->hist_mu);
+    r->hist_snapshot.assign(r->h_counters + 16, r->h_counters + 16 + r->n_tiles);
+  }
+  r->have_frame = true;
+  return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_abi_version(void) { return GSPLAT_ABI_VERSION; }
+
+const char* gs_last_error(void) { return gsh::last_error(); }
+
+int gs_device_count(int* count) {
+  if (!count) return GS_EINVAL;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *count = c;
+  return GS_OK;
+}
+
+int gs_config_init(gs_config* cfg) {
+  if (!cfg) return GS_EINVAL;
+  std::memset(cfg, 0, sizeof(*cfg));
+  // tile_config.hpp:5-15: 1280x720, 40x36 tiles of 32x20; codelets.cpp:622
+  cfg->width = 1280;
+  cfg->height = 720;
+  cfg->tile_width = 32;
+  cfg->tile_height = 20;
+  cfg->guard_band = 15.0f;
+  cfg->device = -1;
+  cfg->band_index = 0;
+  cfg->band_count = 1;
+  return GS_OK;
+}
+
+int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_renderer** out) {
+  if (!out || !cfg || (n > 0 && !g)) {
+    set_error("gs_create: null argument");
+    return GS_EINVAL;
+  }
+  *out = nullptr;
+  if (cfg->width == 0 || cfg->height == 0 || cfg->tile_width == 0 || cfg->tile_height == 0 ||
+      cfg->width > 65535 * 16 || cfg->tile_width * cfg->tile_height > (1u << 20) ||
+      cfg->band_count == 0 || cfg->band_index >= cfg->band_count || n >= 0x7FFFFFFFull) {
+    set_error("gs_create: invalid configuration");
+    return GS_EINVAL;
+  }
+  gs_renderer* r = new gs_renderer();
+  r->cfg = *cfg;
+  r->n = n;
+  r->profile = (cfg->flags & GS_FLAG_PROFILE) != 0;
+  int dev = cfg->device;
+  if (dev < 0) {
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) {
+      delete r;
+      return hip_fail(e, "hipGetDevice");
+    }
+  }
+  r->device = dev;
+  auto fail = [&](int rc) {
+    release(r);
+    delete r;
+    return rc;
+  };
+  if (hipSetDevice(dev) != hipSuccess) return fail(hip_fail(hipSetDevice(dev), "hipSetDevice"));
+  // identity camera until set
+  for (int i = 0; i < 16; ++i) r->view_rm[i] = r->proj_rm[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+
+  // tile grid (ceil: partial tiles are masked) and the row band
+  r->tiles_x = (int)((cfg->width + cfg->tile_width - 1) / cfg->tile_width);
+  r->tiles_y = (int)((cfg->height + cfg->tile_height - 1) / cfg->tile_height);
+  if (r->tiles_x > 65535 || r->tiles_y > 65535) {
+    set_error("gs_create: tile grid too large");
+    return fail(GS_EINVAL);
+  }
+  const int rpb = (r->tiles_y + (int)cfg->band_count - 1) / (int)cfg->band_count;
+  r->band_ty0 = std::min(r->tiles_y, (int)cfg->band_index * rpb);
+  r->band_ty1 = std::min(r->tiles_y, r->band_ty0 + rpb);
+  r->band_py0 = r->band_ty0 * (int)cfg->tile_height;
+  r->band_rows = std::max(0, std::min((int)cfg->height, r->band_ty1 * (int)cfg->tile_height) - r->band_py0);
+  r->band_rows_padded = rpb * (int)cfg->tile_height;
+  r->n_tiles = r->tiles_x * (r->band_ty1 - r->band_ty0);
+  r->stats.n_tiles = (uint32_t)r->n_tiles;
+  r->stats.tiles_x = (uint32_t)r->tiles_x;
+  r->stats.tiles_y = (uint32_t)(r->band_ty1 - r->band_ty0);
+  r->stats.band_y0 = (uint32_t)r->band_py0;
+  r->stats.band_rows = (uint32_t)r->band_rows;
+
+  hipError_t e;
+  if ((e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail(hip_fail(e, "hipStreamCreate"));
+  r->stream = r->own_stream;
+
+  // scene: SoA of the 64-B records
+  const size_t nn = std::max<size_t>(n, 1);
+  if ((e = hipMalloc(&r->d_scene, nn * 64)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(scene)"));
+  {
+    std::vector<float> soa(nn * 16, 0.0f);
+    for (size_t i = 0; i < n; ++i) {
+      const float* s = reinterpret_cast<const float*>(&g[i]);
+      for (int k = 0; k < 4; ++k) {
+        soa[(0 * nn + i) * 4 + k] = s[0 + k];
+        soa[(1 * nn + i) * 4 + k] = s[4 + k];
+        soa[(2 * nn + i) * 4 + k] = s[8 + k];
+        soa[(3 * nn + i) * 4 + k] = s[12 + k];
+      }
+    }
+    if ((e = hipMemcpy(r->d_scene, soa.data(), nn * 64, hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(hip_fail(e, "hipMemcpy(scene)"));
+  }
+  const float4* sc = (const float4*)r->d_scene;
+  r->buf.mean = sc;
+  r->buf.colour = sc + nn;
+  r->buf.rot = sc + 2 * nn;
+  r->buf.scale_gid = sc + 3 * nn;
+
+  if ((e = hipMalloc(&r->d_gauss, nn * (48 + 4 + 8))) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(per-Gaussian)"));
+  r->buf.rec = (float4*)r->d_gauss;
+  r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 48);
+  r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 56);
+
+  const size_t T = (size_t)std::max(r->n_tiles, 1);
+  r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
+  if ((e = hipMalloc(&r->d_zero, r->zero_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(zero)"));
+  r->buf.counters = (uint32_t*)r->d_zero;
+  r->buf.tile_count = (uint32_t*)r->d_zero + 16;
+  if ((e = hipMalloc(&r->d_tiles, (T + 1 + T + T) * 4)) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(tiles)"));
+  r->buf.tile_start = (uint32_t*)r->d_tiles;
+  r->buf.tile_cursor = r->buf.tile_start + T + 1;
+  r->buf.big_tiles = r->buf.tile_cursor + T;
+  if ((e = hipMemset(r->d_tiles, 0, (T + 1 + T + T) * 4)) != hipSuccess)
+    return fail(hip_fail(e, "hipMemset(tiles)"));
+
+  uint64_t cap = cfg->pair_capacity;
+  if (cap == 0) cap = std::max<uint64_t>(1u << 20, 8ull * n);
+  cap = std::min<uint64_t>(cap, 0xFFFFFFF0ull);
+  int rc = alloc_pairs(r, cap);
+  if (rc != GS_OK) return fail(rc);
+
+  const size_t px = (size_t)cfg->width * std::max(r->band_rows_padded, 1);
+  r->bgr_bytes = px * 3;
+  if ((e = hipMalloc(&r->d_out, px * 16 + (r->bgr_bytes + 15) / 16 * 16)) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(framebuffer)"));
+  r->buf.rgba = (float4*)r->d_out;
+  r->buf.bgr = (uint8_t*)r->d_out + px * 16;
+  if ((e = hipMemset(r->d_out, 0, px * 16 + r->bgr_bytes)) != hipSuccess)
+    return fail(hip_fail(e, "hipMemset(framebuffer)"));
+
+  if ((e = hipHostMalloc((void**)&r->h_counters, r->zero_bytes, hipHostMallocDefault)) != hipSuccess)
+    return fail(hip_fail(e, "hipHostMalloc"));
+  std::memset(r->h_counters, 0, r->zero_bytes);
+  r->hist_snapshot.assign((size_t)r->n_tiles, 0u);
+  if (r->profile) {
+    for (auto& s : r->ring)
+      for (auto& ev : s.ev)
+        if ((e = hipEventCreate(&ev)) != hipSuccess) return fail(hip_fail(e, "hipEventCreate"));
+  }
+  *out = r;
+  return GS_OK;
+}
+
+void gs_destroy(gs_renderer* r) {
+  if (!r) return;
+  release(r);
+  delete r;
+}
+
+int gs_set_view(gs_renderer* r, const float rowmajor[16]) {
+  if (!r || !rowmajor) return GS_EINVAL;
+  std::memcpy(r->view_rm, rowmajor, sizeof(r->view_rm));
+  return GS_OK;
+}
+
+int gs_set_projection(gs_renderer* r, const float rowmajor[16]) {
+  if (!r || !rowmajor) return GS_EINVAL;
+  std::memcpy(r->proj_rm, rowmajor, sizeof(r->proj_rm));
+  return GS_OK;
+}
+
+int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor) {
+  if (!r) return GS_EINVAL;
+  r->fov = fov_rad;
+  r->scale_div = scale_divisor;
+  return GS_OK;
+}
+
+int gs_set_stream(gs_renderer* r, void* hip_stream) {
+  if (!r) return GS_EINVAL;
+  if (r->frame_pending) {
+    set_error("gs_set_stream: a frame is in flight");
+    return GS_EINVAL;
+  }
+  r->stream = hip_stream ? (hipStream_t)hip_stream : r->own_stream;
+  return GS_OK;
+}
+
+int gs_render_async(gs_renderer* r) {
+  if (!r) return GS_EINVAL;
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  return enqueue_frame(r);
+}
+
+int gs_sync(gs_renderer* r) {
+  if (!r) return GS_EINVAL;
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  return finish_frame(r);
+}
+
+int gs_render(gs_renderer* r) {
+  if (!r) return GS_EINVAL;
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    rc = enqueue_frame(r);
+    if (rc != GS_OK) return rc;
+    rc = finish_frame(r);
+    if (rc != GS_EOVERFLOW) return rc;
+    // grow the pair capacity (the reference silently drops on overflow)
+    const uint64_t need = r->stats.n_pairs + r->stats.n_pairs / 4 + 1024;
+    const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(need, 2 * r->pair_cap), 0xFFFFFFF0ull);
+    if (need > 0xFFFFFFF0ull) {
+      set_error("gs_render: pair count exceeds 2^32");
+      return GS_EOVERFLOW;
+    }
+    if (hipStreamSynchronize(r->stream) != hipSuccess) return GS_EDEVICE;
+    rc = alloc_pairs(r, cap);
+    if (rc != GS_OK) return rc;
+  }
+  set_error("gs_render: capacity growth did not converge");
+  return GS_EOVERFLOW;
+}
+
+int gs_read_bgr8(gs_renderer* r, uint8_t* dst, size_t bytes) {
+  if (!r || !dst) return GS_EINVAL;
+  const size_t need = (size_t)r->band_rows * r->cfg.width * 3;
+  if (bytes < need) {
+    set_error("gs_read_bgr8: destination too small");
+    return GS_EINVAL;
+  }
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if ((rc = finish_frame(r)) != GS_OK) return rc;
+  GS_HIP(hipMemcpy(dst, r->buf.bgr, need, hipMemcpyDeviceToHost));
+  return GS_OK;
+}
+
+int gs_read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
+  if (!r || !dst) return GS_EINVAL;
+  if (r->cfg.flags & GS_FLAG_NO_RGBA32F) {
+    set_error("gs_read_rgba32f: renderer created with GS_FLAG_NO_RGBA32F");
+    return GS_EINVAL;
+  }
+  const size_t W = r->cfg.width;
+  const size_t rows = (size_t)r->band_rows;
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if ((rc = finish_frame(r)) != GS_OK) return rc;
+  if (layout == GS_LAYOUT_ROW_MAJOR) {
+    if (n_floats < rows * W * 4) {
+      set_error("gs_read_rgba32f: destination too small");
+      return GS_EINVAL;
+    }
+    GS_HIP(hipMemcpy(dst, r->buf.rgba, rows * W * 16, hipMemcpyDeviceToHost));
+    return GS_OK;
+  }
+  if (layout != GS_LAYOUT_REF_TILE_MAJOR) return GS_EINVAL;
+  // the IPU layout (ipu_rasteriser.cpp:164-214 + codelets.cpp:174-176)
+  const size_t tw = r->cfg.tile_width, th = r->cfg.tile_height;
+  const size_t need = (size_t)r->n_tiles * tw * th * 4;
+  if (n_floats < need) {
+    set_error("gs_read_rgba32f: destination too small");
+    return GS_EINVAL;
+  }
+  std::vector<float> rm(rows * W * 4);
+  GS_HIP(hipMemcpy(rm.data(), r->buf.rgba, rm.size() * 4, hipMemcpyDeviceToHost));
+  std::memset(dst, 0, need * 4);
+  for (int t = 0; t < r->n_tiles; ++t) {
+    const size_t tx = t % r->tiles_x, ty = t / r->tiles_x;
+    for (size_t ly = 0; ly < th; ++ly) {
+      const size_t y = ty * th + ly;
+      if (y >= rows) break;
+      for (size_t lx = 0; lx < tw; ++lx) {
+        const size_t x = tx * tw + lx;
+        if (x >= W) break;
+        std::memcpy(dst + ((size_t)t * tw * th + lx + ly * tw) * 4, &rm[(y * W + x) * 4], 16);
+      }
+    }
+  }
+  return GS_OK;
+}
+
+int gs_read_tile_histogram(gs_renderer* r, uint32_t* dst, size_t n) {
+  if (!r || !dst) return GS_EINVAL;
+  std::lock_guard<std::mutex> lk(r->hist_mu);
+  if (n < r->hist_snapshot.size()) {
+    set_error("gs_read_tile_histogram: destination too small");
+    return GS_EINVAL;
+  }
+  std::copy(r->hist_snapshot.begin(), r->hist_snapshot.end(), dst);
+  return GS_OK;
+}
+
+int gs_get_stats(gs_renderer* r, gs_frame_stats* st) {
+  if (!r || !st) return GS_EINVAL;
+  *st = r->stats;
+  st->pair_capacity = r->pair_cap;
+  return GS_OK;
+}
+
+int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list,
+                 size_t n_list) {
+  if (!r || !tile_start || (!list && n_list)) return GS_EINVAL;
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if ((rc = finish_frame(r)) != GS_OK) return rc;
+  const size_t T = (size_t)r->n_tiles;
+  if (n_start < T + 1 || n_list < r->stats.n_pairs) {
+    set_error("gs_read_bins: destination too small");
+    return GS_EINVAL;
+  }
+  std::vector<uint32_t> ts(T + 1);
+  GS_HIP(hipMemcpy(ts.data(), r->buf.tile_start, (T + 1) * 4, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i <= T; ++i) tile_start[i] = ts[i];
+  if (r->stats.n_pairs)
+    GS_HIP(hipMemcpy(list, r->buf.list, r->stats.n_pairs * 4, hipMemcpyDeviceToHost));
+  return GS_OK;
+}
+
+int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
+  if (!r || !dst) return GS_EINVAL;
+  if (n_floats < r->n * 12) {
+    set_error("gs_read_projected: destination too small");
+    return GS_EINVAL;
+  }
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if ((rc = finish_frame(r)) != GS_OK) return rc;
+  std::vector<float> rec(r->n * 12);
+  std::vector<uint32_t> rect(r->n * 2);
+  if (r->n) {
+    GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 48, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(rect.data(), r->buf.rect, r->n * 8, hipMemcpyDeviceToHost));
+  }
+  for (size_t i = 0; i < r->n; ++i) {
+    const float* q = &rec[i * 12];
+    float* o = dst + i * 12;
+    o[0] = q[0];  // mean2d
+    o[1] = q[1];
+    o[2] = q[2];  // conic
+    o[3] = q[3];
+    o[4] = q[4];
+    o[5] = q[5];
+    o[6] = q[10];  // clip z
+    o[7] = q[9];   // radius
+    const uint32_t rx = rect[i * 2], ry = rect[i * 2 + 1];
+    o[8] = (float)(rx & 0xFFFF);
+    o[9] = (float)(ry & 0xFFFF);
+    o[10] = (float)(rx >> 16);
+    o[11] = (float)(ry >> 16);
+  }
+  return GS_OK;
+}
+
+int gs_bgr8_device(gs_renderer* r, void** dev_ptr, size_t* bytes) {
+  if (!r || !dev_ptr || !bytes) return GS_EINVAL;
+  *dev_ptr = r->buf.bgr;
+  *bytes = r->bgr_bytes;
+  return GS_OK;
+}
+
+int gs_copy_bgr8_device(gs_renderer* r, void* dst_dev, size_t bytes) {
+  if (!r || !dst_dev || bytes < r->bgr_bytes) return GS_EINVAL;
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  GS_HIP(hipMemcpyAsync(dst_dev, r->buf.bgr, r->bgr_bytes, hipMemcpyDeviceToDevice, r->stream));
+  return GS_OK;
+}
+
+int gs_kernel_times(gs_renderer* r, double* avg_ms, uint64_t* launches, int n) {
+  if (!r || !avg_ms) return GS_EINVAL;
+  if (!r->profile) {
+    set_error("gs_kernel_times: renderer created without GS_FLAG_PROFILE");
+    return GS_EINVAL;
+  }
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  for (auto& s : r->ring)
+    if ((rc = profile_harvest(r, s)) != GS_OK) return rc;
+  for (int k = 0; k < n && k < GS_K_COUNT; ++k) {
+    avg_ms[k] = r->k_launches[k] ? r->k_ms[k] / (double)r->k_launches[k] : 0.0;
+    if (launches) launches[k] = r->k_launches[k];
+  }
+  return GS_OK;
+}
+
+int gs_reset_kernel_times(gs_renderer* r) {
+  if (!r) return GS_EINVAL;
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  for (auto& s : r->ring)
+    if ((rc = profile_harvest(r, s)) != GS_OK) return rc;
+  for (int k = 0; k < GS_K_COUNT; ++k) {
+    r->k_ms[k] = 0.0;
+    r->k_launches[k] = 0;
+  }
+  return GS_OK;
+}
+
+}  // extern "C"

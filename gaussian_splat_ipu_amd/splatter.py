@@ -1,0 +1,222 @@
+"""GpuSplatter: the MI355X drop-in for ``splat::IpuSplatter``
+(include/splat/ipu_rasteriser.hpp:20-55, src/splat/ipu_rasteriser.cpp).
+
+Same surface, same argument meaning::
+
+    IpuSplatter(const Gaussians&, TiledFramebuffer&, bool noAMP)   -> GpuSplatter(gaussians, fb)
+    updateModelView(glm::mat4) / updateProjection(glm::mat4)      -> update_model_view / update_projection
+    updateFocalLengths(fov, lambda1 / 10)                          -> update_focal_lengths
+    GraphManager::execute(splatter)                                -> execute()
+    getFrameBuffer(cv::Mat&)  (8-bit BGR, H x W)                   -> get_frame_buffer()
+    getIPUHistogram(std::vector<u32>&)                             -> get_histogram()
+
+Every call goes through the C ABI of libgsplat.so; there is no CPU path.
+Errors raise GsError (the reference throws std::runtime_error).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import camera
+from ._lib import (
+    GS_FLAG_NO_RGBA32F,
+    GS_FLAG_PROFILE,
+    GS_K_COUNT,
+    GS_LAYOUT_REF_TILE_MAJOR,
+    GS_LAYOUT_ROW_MAJOR,
+    KERNEL_NAMES,
+    Config,
+    FrameStats,
+    Gaussian3D,
+    check,
+    fptr,
+    lib,
+)
+from .scene import GAUSSIAN_DTYPE, from_float16
+from .tiles import TiledFramebuffer
+
+
+def device_count() -> int:
+    c = C.c_int(0)
+    rc = lib().gs_device_count(C.byref(c))
+    return c.value if rc == 0 else 0
+
+
+class GpuSplatter:
+    def __init__(
+        self,
+        gaussians,
+        fb: TiledFramebuffer,
+        *,
+        guard_band: float = 15.0,
+        guard_tile=None,
+        device: int = -1,
+        band_index: int = 0,
+        band_count: int = 1,
+        pair_capacity: int = 0,
+        write_rgba: bool = True,
+        profile: bool = False,
+    ):
+        g = gaussians
+        if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
+            g = from_float16(g)
+        g = np.ascontiguousarray(g)
+        self.n = int(g.shape[0])
+        self.fb = fb
+        cfg = Config()
+        check(lib().gs_config_init(C.byref(cfg)))
+        cfg.width, cfg.height = fb.width, fb.height
+        cfg.tile_width, cfg.tile_height = fb.tile_width, fb.tile_height
+        if guard_tile is not None:
+            cfg.guard_tile_width, cfg.guard_tile_height = guard_tile
+        cfg.guard_band = guard_band
+        cfg.device = device
+        cfg.band_index, cfg.band_count = band_index, band_count
+        cfg.pair_capacity = pair_capacity
+        cfg.flags = (0 if write_rgba else GS_FLAG_NO_RGBA32F) | (GS_FLAG_PROFILE if profile else 0)
+        self.cfg = cfg
+        h = C.c_void_p()
+        gp = g.ctypes.data_as(C.POINTER(Gaussian3D)) if self.n else None
+        check(lib().gs_create(gp, self.n, C.byref(cfg), C.byref(h)), "gs_create")
+        self._h = h
+        st = self.stats()
+        self.n_tiles = st["n_tiles"]
+        self.band_y0 = st["band_y0"]
+        self.band_rows = st["band_rows"]
+        # reference defaults: fov = radians(40), fxy[1] = lambda1 / 10 = 0.1
+        self.update_focal_lengths(camera.FOV_DEFAULT, 0.1)
+
+    # ------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().gs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ------------------------------------------------------------ inputs
+    def update_model_view(self, mv) -> None:
+        """IpuSplatter::updateModelView (ipu_rasteriser.cpp:86-93): takes a
+        glm-layout (column-major) 4x4 and streams its transpose."""
+        self.set_view_wire(camera.to_wire(mv))
+
+    def update_projection(self, mp) -> None:
+        self.set_projection_wire(camera.to_wire(mp))
+
+    def set_view_wire(self, rowmajor) -> None:
+        a = np.ascontiguousarray(rowmajor, dtype=np.float32).reshape(16)
+        check(lib().gs_set_view(self._h, fptr(a)))
+
+    def set_projection_wire(self, rowmajor) -> None:
+        a = np.ascontiguousarray(rowmajor, dtype=np.float32).reshape(16)
+        check(lib().gs_set_projection(self._h, fptr(a)))
+
+    def update_focal_lengths(self, fov: float, scale_divisor: float) -> None:
+        """IpuSplatter::updateFocalLengths (ipu_rasteriser.cpp:108-110)."""
+        check(lib().gs_set_focal(self._h, fov, scale_divisor))
+        self.fov, self.scale_divisor = fov, scale_divisor
+
+    def set_stream(self, stream_ptr: int | None) -> None:
+        check(lib().gs_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    # ------------------------------------------------------------ execute
+    def execute(self) -> None:
+        """GraphManager::execute -> IpuSplatter::execute (blocking)."""
+        check(lib().gs_render(self._h), "gs_render")
+
+    def execute_async(self) -> None:
+        check(lib().gs_render_async(self._h), "gs_render_async")
+
+    def sync(self) -> None:
+        check(lib().gs_sync(self._h), "gs_sync")
+
+    # ------------------------------------------------------------ outputs
+    def get_frame_buffer(self) -> np.ndarray:
+        """IpuSplatter::getFrameBuffer: rows x W x 3 uint8 BGR, row-major."""
+        out = np.empty((self.band_rows, self.fb.width, 3), np.uint8)
+        check(lib().gs_read_bgr8(self._h, out.ctypes.data_as(C.POINTER(C.c_uint8)), out.nbytes), "gs_read_bgr8")
+        return out
+
+    def get_rgba(self, layout: str = "row_major") -> np.ndarray:
+        if layout == "row_major":
+            out = np.empty((self.band_rows, self.fb.width, 4), np.float32)
+            lay = GS_LAYOUT_ROW_MAJOR
+        else:
+            out = np.empty(self.n_tiles * self.fb.tile_width * self.fb.tile_height * 4, np.float32)
+            lay = GS_LAYOUT_REF_TILE_MAJOR
+        check(lib().gs_read_rgba32f(self._h, fptr(out), out.size, lay), "gs_read_rgba32f")
+        return out
+
+    def get_histogram(self) -> np.ndarray:
+        """IpuSplatter::getIPUHistogram: per-tile render-list length."""
+        out = np.empty(self.n_tiles, np.uint32)
+        check(lib().gs_read_tile_histogram(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
+        return out
+
+    def stats(self) -> dict:
+        st = FrameStats()
+        check(lib().gs_get_stats(self._h, C.byref(st)))
+        return st.as_dict()
+
+    def get_bins(self):
+        """(tile_start[T+1] uint64, list[P] uint32): depth-sorted per-tile lists."""
+        st = self.stats()
+        ts = np.empty(st["n_tiles"] + 1, np.uint64)
+        lst = np.empty(max(st["n_pairs"], 1), np.uint32)
+        check(
+            lib().gs_read_bins(
+                self._h,
+                ts.ctypes.data_as(C.POINTER(C.c_uint64)),
+                ts.size,
+                lst.ctypes.data_as(C.POINTER(C.c_uint32)),
+                lst.size,
+            )
+        )
+        return ts, lst[: st["n_pairs"]]
+
+    def get_projected(self) -> np.ndarray:
+        """(N, 12) float32: mean2d[2], conic[4], clip z, radius, rect tx0 ty0 tx1 ty1."""
+        out = np.empty((self.n, 12), np.float32)
+        check(lib().gs_read_projected(self._h, fptr(out), out.size))
+        return out
+
+    def bgr8_device(self):
+        p = C.c_void_p()
+        nbytes = C.c_size_t()
+        check(lib().gs_bgr8_device(self._h, C.byref(p), C.byref(nbytes)))
+        return p.value, nbytes.value
+
+    def copy_bgr8_device(self, dst_ptr: int, nbytes: int) -> None:
+        check(lib().gs_copy_bgr8_device(self._h, C.c_void_p(dst_ptr), nbytes))
+
+    def kernel_times(self) -> dict:
+        avg = (C.c_double * GS_K_COUNT)()
+        cnt = (C.c_uint64 * GS_K_COUNT)()
+        check(lib().gs_kernel_times(self._h, avg, cnt, GS_K_COUNT))
+        return {KERNEL_NAMES[k]: (avg[k], cnt[k]) for k in range(GS_K_COUNT)}
+
+    def reset_kernel_times(self) -> None:
+        check(lib().gs_reset_kernel_times(self._h))
+
+    # reference-spelled aliases (ipu_rasteriser.hpp:20-55)
+    updateModelView = update_model_view
+    updateProjection = update_projection
+    updateFocalLengths = update_focal_lengths
+    getFrameBuffer = get_frame_buffer
+    getIPUHistogram = get_histogram

@@ -1,0 +1,225 @@
+/*
+ * gsplat.h -- C ABI of the MI355X Gaussian-splat tile rasteriser (libgsplat.so).
+ *
+ * This is the drop-in boundary for the reference's operator
+ * `splat::IpuSplatter` (include/splat/ipu_rasteriser.hpp:20-55 in
+ * Nmjfry/gaussian_splat_ipu).  Every entry point below names the reference
+ * interface it replaces.  Plain C types only: no C++, HIP or torch types cross
+ * this ABI, no exceptions cross it; every call returns a gs_status and the
+ * reason for a failure is available from gs_last_error() (thread-local).
+ *
+ * Threading (reference: one render thread drives updateModelView, execute and
+ * getFrameBuffer,
+ * the UI thread reads the histogram, splat.cpp:208-225,257-265): calls on one
+ * handle must be serialised by the caller, except gs_read_tile_histogram, which
+ * reads a mutex-protected host snapshot and is safe from any thread.
+ */
+#ifndef GSPLAT_H
+#define GSPLAT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSPLAT_ABI_VERSION 1
+
+typedef enum gs_status {
+  GS_OK = 0,
+  GS_EINVAL = 1,     /* bad argument (std::logic_error in the reference) */
+  GS_EDEVICE = 2,    /* HIP runtime / device failure (no GPU, launch error) */
+  GS_EOOM = 3,       /* device or pinned-host allocation failed */
+  GS_EOVERFLOW = 4,  /* (tile, Gaussian) pair list exceeded capacity; the
+                        reference drops Gaussians silently (codelets.cpp:544) */
+  GS_EIO = 5         /* file could not be read / parsed */
+} gs_status;
+
+/* One world-space Gaussian, 64 bytes: splat::Gaussian3D
+ * (include/splat/ipu_geometry.hpp:305-311) as flattened by the IpuSplatter
+ * constructor (src/splat/ipu_rasteriser.cpp:49-68). */
+typedef struct gs_gaussian3d {
+  float mean[4];    /* x, y, z, w (w = 1)                         */
+  float colour[4];  /* r, g, b, raw opacity logit (no sigmoid)    */
+  float rot[4];     /* quaternion, rot[0] is the real part        */
+  float scale[3];   /* raw log-scales                             */
+  float gid;        /* i + 1; gid <= 0 marks an empty slot        */
+} gs_gaussian3d;
+
+/* Renderer configuration: the TiledFramebuffer (tile_config.hpp:19-41) and
+ * the hard-coded constants of the codelet (codelets.cpp:620-622). */
+typedef struct gs_config {
+  uint32_t width, height;             /* IMWIDTH, IMHEIGHT                  */
+  uint32_t tile_width, tile_height;   /* IPU_TILEWIDTH, IPU_TILEHEIGHT      */
+  uint32_t guard_tile_width;          /* tile size used by the guard band;  */
+  uint32_t guard_tile_height;         /*   0 = same as the render tile      */
+  float guard_band;                   /* clipSize (15)                      */
+  int32_t device;                     /* HIP device ordinal, -1 = current   */
+  uint32_t band_index, band_count;    /* row-band shard: tile rows split into
+                                         band_count contiguous bands         */
+  uint64_t pair_capacity;             /* initial (tile,Gaussian) capacity, 0 = auto */
+  uint32_t flags;                     /* GS_FLAG_*                          */
+} gs_config;
+
+#define GS_FLAG_NO_RGBA32F 1u  /* skip the RGBA f32 framebuffer store (BGR8 only) */
+#define GS_FLAG_PROFILE 2u     /* record HIP events around every kernel     */
+
+typedef enum gs_layout {
+  GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */
+  GS_LAYOUT_REF_TILE_MAJOR = 1  /* the IPU framebuffer layout: one tile's
+                                   tw*th*4 floats after another, pixel (x,y)
+                                   at (x + y*tw)*4 (codelets.cpp:174-176)   */
+} gs_layout;
+
+typedef struct gs_frame_stats {
+  uint64_t n_gaussians;   /* N                                  */
+  uint64_t n_rendered;    /* V: pass guard band and z < 0       */
+  uint64_t n_pairs;       /* P: sum over tiles of list lengths  */
+  uint64_t max_list;      /* max tile list length               */
+  uint64_t pair_capacity;
+  uint32_t n_tiles;       /* tiles in this renderer's band      */
+  uint32_t tiles_x, tiles_y;
+  uint32_t band_y0, band_rows;  /* pixel rows of this band          */
+  uint32_t n_big_tiles;   /* tiles sorted by the large-list path */
+} gs_frame_stats;
+
+/* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */
+enum {
+  GS_K_PROJECT = 0,
+  GS_K_SCAN = 1,
+  GS_K_EMIT = 2,
+  GS_K_SORT = 3,
+  GS_K_BLEND = 4,
+  GS_K_COUNT = 5
+};
+
+typedef struct gs_renderer gs_renderer;
+
+/* ------------------------------------------------------------ lifetime */
+int gs_abi_version(void);
+const char* gs_last_error(void);
+int gs_device_count(int* count);
+/* Defaults: 1280x720, 32x20 tiles, guard band 15 (the reference build). */
+int gs_config_init(gs_config* cfg);
+
+/* Replaces IpuSplatter::IpuSplatter(const Gaussians&, TiledFramebuffer&, bool)
+ * (ipu_rasteriser.cpp:49-83) + GraphManager::compileOrLoad/prepareEngine
+ * (splat.cpp:166-168,199).  Copies the records to the device once (the
+ * reference's "write_verts" program, ipu_rasteriser.cpp:401-418); the caller
+ * keeps ownership of `g`. */
+int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_renderer** out);
+/* Replaces IpuSplatter::~IpuSplatter. */
+void gs_destroy(gs_renderer* r);
+
+/* ------------------------------------------------------------ per-frame inputs */
+/* Replaces IpuSplatter::updateModelView (ipu_rasteriser.cpp:86-93): the
+ * argument is the row-major float[16] the reference streams to the device
+ * (glm::transpose(mv) flattened). */
+int gs_set_view(gs_renderer* r, const float rowmajor[16]);
+/* Replaces IpuSplatter::updateProjection (ipu_rasteriser.cpp:95-102). */
+int gs_set_projection(gs_renderer* r, const float rowmajor[16]);
+/* Replaces IpuSplatter::updateFocalLengths(fx, fy) (ipu_rasteriser.cpp:108-110):
+ * fxy = (fov radians, scale divisor lambda1/10). */
+int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor);
+/* HIP stream (hipStream_t as void*) the frame is enqueued on; NULL = the
+ * renderer's own stream. */
+int gs_set_stream(gs_renderer* r, void* hip_stream);
+
+/* ------------------------------------------------------------ execute */
+/* Replaces GraphManager::execute -> IpuSplatter::execute (ipu_rasteriser.cpp:
+ * 408-420): synchronous.  Grows the pair capacity and re-renders on overflow. */
+int gs_render(gs_renderer* r);
+/* Enqueue one frame on the stream and return; gs_sync waits and reports
+ * GS_EOVERFLOW if the capacity was exceeded (then call gs_render). */
+int gs_render_async(gs_renderer* r);
+int gs_sync(gs_renderer* r);
+
+/* ------------------------------------------------------------ outputs */
+/* Replaces IpuSplatter::getFrameBuffer (ipu_rasteriser.cpp:131-144): 8-bit
+ * BGR, row-major, band_rows x width x 3 (the full H x W x 3 for one band). */
+int gs_read_bgr8(gs_renderer* r, uint8_t* dst, size_t bytes);
+/* The f32 RGBA framebuffer the reference streams out (frame_buffer,
+ * ipu_rasteriser.cpp:398) in either layout. */
+int gs_read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout);
+/* Replaces IpuSplatter::getIPUHistogram (ipu_rasteriser.cpp:104-106): per
+ * tile render-list length of the last completed frame (thread-safe). */
+int gs_read_tile_histogram(gs_renderer* r, uint32_t* dst, size_t n);
+int gs_get_stats(gs_renderer* r, gs_frame_stats* st);
+/* Parity/debug: tile_start (n_tiles+1 entries) and the depth-sorted per-tile
+ * Gaussian index lists (n_pairs entries, 0-based Gaussian indices). */
+int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list,
+                 size_t n_list);
+/* Parity/debug: per-Gaussian projection: mean2d[2], conic[4] (w = opacity or 0),
+ * clip z, radius, rect[4] (tx0,ty0,tx1,ty1; empty if tx0 > tx1) as floats:
+ * 12 floats per Gaussian. */
+int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats);
+/* Device pointer of this band's BGR8 output (band_rows_padded x width x 3)
+ * and its padded byte size, for an in-place RCCL all-gather. */
+int gs_bgr8_device(gs_renderer* r, void** dev_ptr, size_t* bytes);
+/* Enqueue a device-to-device copy of the band's BGR8 (padded) into dst. */
+int gs_copy_bgr8_device(gs_renderer* r, void* dst_dev, size_t bytes);
+/* Average device milliseconds per launch of each kernel (GS_K_*) over the
+ * frames since the last reset (requires GS_FLAG_PROFILE). */
+int gs_kernel_times(gs_renderer* r, double* avg_ms, uint64_t* launches, int n);
+int gs_reset_kernel_times(gs_renderer* r);
+
+/* ------------------------------------------------------------ host-side data path */
+/* PLY / XYZ ingest (src/splat/file_io.cpp:11-77): all 14 3DGS properties are
+ * required for .ply (fillPlyProperties); f_rest_* are kept when present. */
+typedef struct gs_ply gs_ply;
+int gs_ply_load(const char* path, gs_ply** out);
+int gs_ply_save(const gs_ply* p, const char* path);
+void gs_ply_free(gs_ply* p);
+int64_t gs_ply_count(const gs_ply* p);
+int gs_ply_has(const gs_ply* p, const char* name);
+int gs_ply_get(const gs_ply* p, const char* name, float* dst, size_t n);
+
+/* Seeded synthetic scene (SURVEY §8 d): xoshiro256** PRNG. */
+typedef struct gs_synth_params {
+  uint64_t n;
+  uint64_t seed;
+  int32_t sh_degree;          /* 0 or 3 (45 f_rest)                      */
+  float bb_min[3], bb_max[3]; /* uniform positions inside this box       */
+  float log_scale_mu, log_scale_sigma;
+  float opacity_lo, opacity_hi;
+  const float* cluster_xyz;   /* optional: positions resampled from these */
+  uint64_t n_cluster;         /*   points with N(0, cluster_sigma) jitter */
+  float cluster_sigma;
+} gs_synth_params;
+int gs_synth_params_init(gs_synth_params* sp);
+int gs_ply_synthetic(const gs_synth_params* sp, gs_ply** out);
+
+/* Scene preparation of the render server (splat.cpp:83-163): centre the
+ * bounding box, negate z, colour = max(SH_C0 * f_dc + 0.5, 0), raw opacity,
+ * raw log-scale, raw rotation, gid = i + 1.  bb_out = min[3], max[3] of the
+ * centred points (may be NULL). */
+int gs_scene_prepare(const gs_ply* p, gs_gaussian3d* out, size_t n, float* bb_out);
+
+/* ------------------------------------------------------------ camera (glm, column-major) */
+int gs_mat4_mul(const float* a, const float* b, float* out);
+int gs_mat4_mul_vec4(const float* m, const float* v, float* out);
+int gs_mat4_transpose(const float* m, float* out);
+int gs_cam_look_at(const float* eye, const float* center, const float* up, float* out);
+int gs_cam_frustum(float l, float r, float b, float t, float n, float f, float* out);
+/* splat::fitFrustumToBoundingBox (src/splat/geometry.cpp:9-24) */
+int gs_cam_fit_frustum(const float* bb_min, const float* bb_max, float fov, float aspect,
+                       float* out);
+/* splat::lookAtBoundingBox (src/splat/camera.cpp:10-15) */
+int gs_cam_look_at_bbox(const float* bb_min, const float* bb_max, const float* up, float scale,
+                        float* out);
+int gs_cam_rotate(const float* m, float angle_rad, const float* axis, float* out);
+int gs_cam_translate(const float* m, const float* v, float* out);
+/* The hard-coded first-frame view `mvpStart` (splat.cpp:235-241). */
+int gs_cam_mvp_start(float* out);
+/* The headless camera of the render server (splat.cpp:186-199,235-244):
+ * view = mvpStart, projection = fitFrustumToBoundingBox(bb in camera space,
+ * fov, width/height).  Outputs are ROW-MAJOR (ready for gs_set_view/projection). */
+int gs_cam_headless(const float* bb6, uint32_t width, uint32_t height, float fov,
+                    float* view_rm, float* proj_rm);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSPLAT_H */

@@ -1,0 +1,239 @@
+"""GPU parity: the HIP frame path (through the C ABI) against the CPU oracle.
+
+Bar: projection records, tile binning (per-tile depth-sorted
+Gaussian indices) and the tile histogram are compared bit-exactly; the RGBA f32
+framebuffer is asserted bit-identical as well (tolerance 0 -- the kernels and
+the oracle implement the same IEEE op sequence, -ffp-contract=off, the same
+specified expf), and the BGR8 frame exactly.
+"""
+import numpy as np
+import pytest
+
+from conftest import PC12
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_same_bits(a, b, what=""):
+    """Bit-exact float comparison, except that all NaNs compare equal (the NaN
+    sign/payload an operation produces differs between x86 -- default NaN
+    0xFFC00000 -- and gfx950 -- 0x7FC00000 -- and is not a value)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+    if not same.all():
+        bad = np.argwhere(~same)
+        raise AssertionError(
+            f"{what}: {len(bad)} of {a.size} values differ; first {bad[:4].tolist()}: "
+            f"{a[tuple(bad[0])]} vs {b[tuple(bad[0])]}"
+        )
+
+
+def _frame_pair(g, view, proj, W, H, TW, TH, scale_div, fov=None, guard_tile=None, band=None, band_count=1,
+                band_index=0, pair_capacity=0):
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+    from oracle import oracle as O
+
+    fov = camera.FOV_DEFAULT if fov is None else fov
+    fb = TiledFramebuffer(W, H, TW, TH)
+    s = GpuSplatter(g, fb, device=0, guard_tile=guard_tile, band_index=band_index, band_count=band_count,
+                    pair_capacity=pair_capacity)
+    s.set_view_wire(view)
+    s.set_projection_wire(proj)
+    s.update_focal_lengths(fov, scale_div)
+    s.execute()
+    if band_count > 1:
+        ty0, ty1, _, _ = fb.band_rows(band_count)[band_index]
+        band = (ty0, ty1) if ty1 > ty0 else None
+    f = O.make_frame(view, proj, W, H, TW, TH, fov, scale_div, guard_tile=guard_tile, band=band)
+    return s, f
+
+
+def _assert_parity(s, f, g, check_proj=True):
+    from oracle import oracle as O
+
+    ref = O.render(g, f)
+    st = s.stats()
+    assert st["n_rendered"] == ref["stats"]["n_rendered"]
+    assert st["n_pairs"] == ref["stats"]["n_pairs"]
+    assert st["max_list"] == ref["stats"]["max_list"]
+    if check_proj and g.shape[0]:
+        p = O.project(g, f)
+        gp = s.get_projected()
+        live = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16)[:, 15] > 0
+        assert_same_bits(gp[live, 0:2], p["mean2d"][live], "mean2d")
+        assert_same_bits(gp[live, 2:6], p["conic"][live], "conic")
+        assert_same_bits(gp[live, 6], p["clip_z"][live], "clip z")
+        assert_same_bits(gp[live, 7], p["radius"][live], "radius")
+        r = p["rect"]
+        ok = (p["rendered"] != 0) & (r[:, 0] <= r[:, 2])
+        grect = gp[:, 8:12].astype(np.int64)
+        gok = grect[:, 0] <= grect[:, 2]
+        np.testing.assert_array_equal(gok, ok)
+        np.testing.assert_array_equal(grect[ok], r[ok])
+    ts, lst = s.get_bins()
+    rts, rlst = O.bin_lists(O.project(g, f), f)
+    np.testing.assert_array_equal(ts.astype(np.int64), rts)
+    np.testing.assert_array_equal(lst, rlst)
+    np.testing.assert_array_equal(s.get_histogram(), ref["hist"])
+    assert_same_bits(s.get_rgba(), ref["rgba"], "RGBA f32 framebuffer")
+    np.testing.assert_array_equal(s.get_frame_buffer(), ref["bgr"])
+    return ref
+
+
+@pytest.fixture(scope="module")
+def pc12(built):
+    from gaussian_splat_ipu_amd import scene
+
+    g, bb = scene.prepare_scene(scene.load_ply(PC12))
+    return g, bb
+
+
+@pytest.mark.parametrize("scale_div", [0.1, 1.0])
+def test_pc12_reference_geometry_720p(pc12, scale_div):
+    """config 2 at the reference's own build geometry: 1280x720, 32x20 tiles."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = pc12
+    view, proj = camera.headless(bb, 1280, 720)
+    s, f = _frame_pair(g, view, proj, 1280, 720, 32, 20, scale_div)
+    ref = _assert_parity(s, f, g)
+    assert ref["stats"]["n_pairs"] > 50000
+
+
+@pytest.mark.parametrize("tw,th", [(16, 16), (48, 30), (32, 20)])
+def test_pc12_1080p(pc12, tw, th):
+    """config 2: point_cloud_12 at 1920x1080 (16x16 production tiles, 48x30 =
+    the reference macros at 1080p, 32x20); 1080/16 leaves a partial tile row."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = pc12
+    view, proj = camera.headless(bb, 1920, 1080)
+    s, f = _frame_pair(g, view, proj, 1920, 1080, tw, th, 1.0)
+    _assert_parity(s, f, g)
+
+
+def test_synthetic_1080p_16x16(built):
+    from gaussian_splat_ipu_amd import camera, scene
+
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=200_000, seed=1, sh_degree=3)))
+    view, proj = camera.headless(bb, 1920, 1080)
+    s, f = _frame_pair(g, view, proj, 1920, 1080, 16, 16, 1.0)
+    _assert_parity(s, f, g)
+
+
+def test_large_tile_lists_take_the_radix_path(built):
+    """A clustered scene (config 5's construction) puts > 4096 Gaussians on
+    some tiles: those go through the block-wide LSD radix sort."""
+    from gaussian_splat_ipu_amd import camera, scene
+
+    src = scene.load_ply(PC12)
+    cl = np.stack([src["x"], src["y"], src["z"]], 1)[:200]
+    ply = scene.synthetic(scene.SynthSpec(n=150_000, seed=8, sh_degree=0, cluster_xyz=cl, cluster_sigma=0.02))
+    g, bb = scene.prepare_scene(ply)
+    view, proj = camera.headless(bb, 1280, 720)
+    s, f = _frame_pair(g, view, proj, 1280, 720, 16, 16, 1.0)
+    _assert_parity(s, f, g)
+    assert s.stats()["n_big_tiles"] > 0
+
+
+@pytest.mark.parametrize("band_count", [2, 3, 8])
+def test_row_bands_union_equals_full_frame(pc12, band_count):
+    """The multi-GPU decomposition: each band renders its tile rows; every band
+    matches the oracle restricted to that band, and stacking the bands gives the
+    single-renderer frame."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = pc12
+    W, H, TW, TH = 1920, 1080, 16, 16
+    view, proj = camera.headless(bb, W, H)
+    full, _ = _frame_pair(g, view, proj, W, H, TW, TH, 1.0)
+    whole = full.get_rgba()
+    parts = []
+    for b in range(band_count):
+        s, f = _frame_pair(g, view, proj, W, H, TW, TH, 1.0, band_count=band_count, band_index=b)
+        if s.band_rows == 0:
+            continue
+        _assert_parity(s, f, g, check_proj=False)
+        parts.append(s.get_rgba())
+    assert_same_bits(np.concatenate(parts, 0), whole, "stacked bands")
+
+
+def test_edge_cases(built):
+    """Empty scene, empty slots (gid <= 0), Gaussians behind the camera,
+    degenerate covariance (det == 0), huge Gaussians beyond the guard band,
+    non-finite inputs and off-screen means."""
+    from gaussian_splat_ipu_amd import camera, scene
+
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=5000, seed=3, sh_degree=0)))
+    a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
+    a[0:50, 15] = 0.0  # empty slots
+    a[50:100, 15] = -3.0
+    a[100:150, 0:3] = [0.0, 0.0, 40.0]  # behind the camera (world z +40 maps behind)
+    a[150:200, 12:15] = 30.0  # huge (guard band drops them)
+    a[200:250, 8:12] = 0.0  # zero quaternion -> normalize() returns identity
+    a[250:300, 12:15] = -200.0  # scale -> exp underflow (det == 0 path)
+    a[300:310, 0] = np.nan
+    a[310:320, 0] = np.inf
+    a[320:370, 0] = 30.0  # far off-screen
+    a[370:400, 4:7] = -1.0  # negative colour
+    view, proj = camera.headless(bb, 800, 600)
+    for tw, th in [(16, 16), (32, 20)]:
+        s, f = _frame_pair(a, view, proj, 800, 600, tw, th, 1.0)
+        _assert_parity(s, f, a)
+    # empty scene
+    s, f = _frame_pair(a[:0], view, proj, 800, 600, 16, 16, 1.0)
+    assert s.stats()["n_pairs"] == 0
+    assert not s.get_frame_buffer().any()
+
+
+def test_overflow_grows_capacity(pc12):
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = pc12
+    view, proj = camera.headless(bb, 1280, 720)
+    s, f = _frame_pair(g, view, proj, 1280, 720, 16, 16, 1.0, pair_capacity=1000)
+    assert s.stats()["pair_capacity"] >= s.stats()["n_pairs"] > 1000
+    _assert_parity(s, f, g, check_proj=False)
+
+
+def test_repeatable_and_async(pc12):
+    """Same inputs twice -> identical frames (no atomics-order dependence);
+    execute_async + sync gives the same frame."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = pc12
+    view, proj = camera.headless(bb, 1920, 1080)
+    s, _ = _frame_pair(g, view, proj, 1920, 1080, 16, 16, 1.0)
+    a = s.get_rgba().copy()
+    ts1, l1 = s.get_bins()
+    s.execute_async()
+    s.sync()
+    assert_same_bits(s.get_rgba(), a, "async frame")
+    ts2, l2 = s.get_bins()
+    np.testing.assert_array_equal(l1, l2)
+
+
+def test_orbit_frames(pc12):
+    """config 5's orbit camera on a few frames (view changes per frame)."""
+    from gaussian_splat_ipu_amd import camera
+    from oracle import oracle as O
+
+    g, bb = pc12
+    _, proj = camera.headless(bb, 1280, 720)
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    s = GpuSplatter(g, TiledFramebuffer(1280, 720, 16, 16), device=0)
+    s.set_projection_wire(proj)
+    s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+    for k in (0, 17, 45, 90):
+        view = camera.orbit_view(k)
+        s.set_view_wire(view)
+        s.execute()
+        f = O.make_frame(view, proj, 1280, 720, 16, 16, camera.FOV_DEFAULT, 1.0)
+        ref = O.render(g, f)
+        assert_same_bits(s.get_rgba(), ref["rgba"], f"orbit frame {k}")
