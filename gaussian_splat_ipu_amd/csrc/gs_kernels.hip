@@ -145,16 +145,67 @@ __device__ __forceinline__ uint32_t depth_key_of(float z) {
 }
 
 constexpr uint2 kEmptyRect = {1u, 1u};  // tx0 = 1 > tx1 = 0
+constexpr uint32_t kEmptyBox = 0x80007FFFu;  // lo = +32767 > hi = -32768
+constexpr uint32_t kFullBox = 0x7FFF8000u;   // lo = -32768, hi = +32767
+
+__device__ __forceinline__ uint32_t pack_i16x2(double lo, double hi) {
+  lo = fmax(-32768.0, fmin(32767.0, lo));
+  hi = fmax(-32768.0, fmin(32767.0, hi));
+  return ((uint32_t)(int)lo & 0xFFFFu) | ((uint32_t)(int)hi << 16);
+}
+
+// Conservative alpha footprint of one 2D Gaussian, used by the blend to skip
+// work that cannot change a pixel ("blend culling"):
+//   pcut: a lane with power < pcut has op * expf(power) < 1/255, i.e. the
+//         reference would `continue` (codelets.cpp:401-403);
+//   box:  integer pixel box (x0,x1 | y0,y1) outside of which every pixel has
+//         power < pcut (the ellipse { d^T Q d <= -2 pcut } of the conic Q,
+//         widened by 0.1% + 1 px, computed in fp64).
+// Both only ever remove evaluations whose outcome is "skip", so the blended
+// result is bit-identical to evaluating every list entry.
+__device__ __forceinline__ void alpha_footprint(float mx, float my, float k0, float k1, float k2,
+                                                float op, const FrameParams& fp, float& pcut,
+                                                uint32_t& box_x, uint32_t& box_y) {
+  pcut = -__builtin_huge_valf();  // no per-lane cut
+  box_x = kFullBox;
+  box_y = kFullBox;
+  const bool nice = __builtin_fabsf(k0) < 1e30f && __builtin_fabsf(k1) < 1e30f &&
+                    __builtin_fabsf(k2) < 1e30f && __builtin_fabsf(mx) < 1e30f &&
+                    __builtin_fabsf(my) < 1e30f && fp.width <= 32767 && fp.height <= 32767;
+  if (!nice || op != op) return;  // NaN opacity: alpha = min(0.99, NaN) = 0.99, never skipped
+  if (op < 1.0f / 255.0f) {       // alpha <= op < 1/255 for every pixel: always skipped
+    pcut = __builtin_huge_valf();
+    box_x = kEmptyBox;
+    box_y = kEmptyBox;
+    return;
+  }
+  const double pc = -log(255.0 * (double)op) - 0.05;  // power below this: alpha < 0.96 / 255
+  float pf = (float)pc;
+  // round toward -inf (pc <= -0.05 < 0: one ulp more negative is bits + 1)
+  if ((double)pf > pc) pf = __uint_as_float(__float_as_uint(pf) + 1u);
+  pcut = pf;
+  const double a = k0, b = k1, c = k2;
+  const double det = a * c - b * b;
+  // Well-conditioned conics only (1 - rho^2 > 1e-3): then the fp32 rounding of
+  // the reference's power expression is < 7e-4 relative, far inside the 0.05
+  // margin of pcut ("blend culling").
+  if (a > 0.0 && c > 0.0 && det > 1e-3 * a * c) {
+    const double R = -2.0 * pc;
+    const double ex = sqrt(R * c / det) * 1.001 + 1.0;
+    const double ey = sqrt(R * a / det) * 1.001 + 1.0;
+    box_x = pack_i16x2(floor((double)mx - ex), ceil((double)mx + ex));
+    box_y = pack_i16x2(floor((double)my - ey), ceil((double)my + ey));
+  }
+}
 
 // ------------------------------------------------------------------ project
-__global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= fp.n) return;
+__device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i) {
+  bool rendered = false;
   const float4 mean = b.mean[i];
   const float4 col = b.colour[i];
   const float4 rot = b.rot[i];
   const float4 sg = b.scale_gid[i];
-  float4* rec = b.rec + 3 * (size_t)i;
+  float4* rec = b.rec + 4 * (size_t)i;  // 64-B record
   uint2 rect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
@@ -224,11 +275,15 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
       k2 = a * inv;
       k3 = col.w;
     }
+    float pcut;
+    uint32_t b01, b23;
+    alpha_footprint(vx, vy, k0, k1, k2, k3, fp, pcut, b01, b23);
     rec[0] = make_float4(vx, vy, k0, k1);
     rec[1] = make_float4(k2, k3, col.x, col.y);
-    rec[2] = make_float4(col.z, radius, cz, 0.0f);
+    rec[2] = make_float4(col.z, pcut, __uint_as_float(b01), __uint_as_float(b23));
+    rec[3] = make_float4(radius, cz, 0.0f, 0.0f);
     if (within && cz < 0.0f) {  // codelets.cpp:493
-      atomicAdd(&b.counters[2], 1u);
+      rendered = true;
       dkey = depth_key_of(cz);
       // converged lattice rectangle
       float fx0 = __builtin_floorf(__builtin_floorf(minx) / fp.tw);
@@ -246,17 +301,30 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
         const uint32_t y0 = (uint32_t)((int)fy0 - fp.band_ty0);
         const uint32_t y1 = (uint32_t)((int)fy1 - fp.band_ty0);
         rect = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
-        for (uint32_t y = y0; y <= y1; ++y)
-          for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&b.tile_count[y * fp.tiles_x + x], 1u);
+        if (fp.bin_global)  // fallback binning: per-tile lengths by global atomics
+          for (uint32_t y = y0; y <= y1; ++y)
+            for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&b.tile_count[y * fp.tiles_x + x], 1u);
       }
     }
   } else {
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     rec[1] = make_float4(0.0f, 0.0f, col.x, col.y);
-    rec[2] = make_float4(col.z, 0.0f, 0.0f, 0.0f);
+    rec[2] = make_float4(col.z, __builtin_huge_valf(), __uint_as_float(kEmptyBox),
+                         __uint_as_float(kEmptyBox));
+    rec[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
   b.rect[i] = rect;
   b.depth_key[i] = dkey;
+  return rendered;
+}
+
+__global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  bool rendered = false;
+  if (i < fp.n) rendered = project_one(fp, b, i);
+  // V per workgroup (summed by the scan kernel): no single-address atomics
+  const int v = __syncthreads_count(rendered);
+  if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
 }
 
 // --------------------------------------------------------------------- scan
@@ -264,6 +332,7 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
 __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b) {
   __shared__ unsigned long long wsum[16];
   __shared__ uint32_t wmax[16];
+  __shared__ uint32_t wvis[16];
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int per = (T + 1023) / 1024;
@@ -295,7 +364,18 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
     b.tile_cursor[i] = (uint32_t)run;
     run += b.tile_count[i];
   }
+  // V = sum of the project workgroups' counts
+  uint32_t vsum = 0;
+  const int nb = (fp.n + 255) / 256;
+  for (int i = tid; i < nb; i += 1024) vsum += b.block_rendered[i];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
+  if (lane == 0) wvis[wave] = vsum;
+  __syncthreads();
   if (tid == 1023) {
+    uint32_t vis = 0;
+    for (int w = 0; w < 16; ++w) vis += wvis[w];
+    b.counters[2] = vis;
     unsigned long long total = 0;
     uint32_t m = 0;
     for (int w = 0; w < 16; ++w) {
@@ -310,7 +390,96 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
   }
 }
 
+// ------------------------------------------------------------ chunked binning
+// The Gaussians are cut into chunks of fp.chunk_size; one 1024-thread
+// workgroup per chunk keeps a private histogram over all band tiles in LDS,
+// two 16-bit counters per word (a chunk adds at most chunk_size <= 65535 to a
+// tile), so the contended global atomics of a plain histogram never happen.
+//   count:   chunk histogram rows -> chunk_off[chunk][tile]
+//   colscan: per tile, exclusive scan over chunks (in place) + tile totals
+//   emit:    chunk c writes its pairs of tile t at
+//            tile_start[t] + chunk_off[c][t] + (LDS slot counter)
+__device__ __forceinline__ void lds_zero(uint32_t* cnt, int words) {
+  for (int i = threadIdx.x; i < words; i += blockDim.x) cnt[i] = 0;
+}
+
+__global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers b) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
+  const int T = fp.n_tiles;
+  lds_zero(cnt, (T + 1) >> 1);
+  __syncthreads();
+  const int c = blockIdx.x;
+  const int g0 = c * fp.chunk_size;
+  const int g1 = min(fp.n, g0 + fp.chunk_size);
+  for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
+    const uint2 r = b.rect[i];
+    const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+    if (x0 > x1) continue;
+    for (uint32_t y = y0; y <= y1; ++y)
+      for (uint32_t x = x0; x <= x1; ++x) {
+        const uint32_t t = y * fp.tiles_x + x;
+        atomicAdd(&cnt[t >> 1], 1u << ((t & 1u) * 16u));
+      }
+  }
+  __syncthreads();
+  uint32_t* row = b.chunk_off + (size_t)c * T;
+  for (int t = threadIdx.x; t < T; t += 1024) row[t] = (cnt[t >> 1] >> ((t & 1) * 16)) & 0xFFFFu;
+}
+
+// 64 tiles per workgroup (one per lane), the chunk rows split over 16 waves.
+__global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffers b) {
+  __shared__ uint32_t wsum[16][64];
+  const int T = fp.n_tiles, NC = fp.n_chunks;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = blockIdx.x * 64 + lane;
+  const int rows = (NC + 15) / 16;
+  const int c0 = wave * rows, c1 = min(NC, c0 + rows);
+  uint32_t sum = 0;
+  if (t < T)
+    for (int c = c0; c < c1; ++c) sum += b.chunk_off[(size_t)c * T + t];
+  wsum[wave][lane] = sum;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int w = 0; w < wave; ++w) base += wsum[w][lane];
+  if (t < T) {
+    uint32_t run = base;
+    for (int c = c0; c < c1; ++c) {
+      uint32_t* p = b.chunk_off + (size_t)c * T + t;
+      const uint32_t v = *p;
+      *p = run;
+      run += v;
+    }
+    if (wave == 15) b.tile_count[t] = run;
+  }
+}
+
+__global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buffers b) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
+  const int T = fp.n_tiles;
+  lds_zero(cnt, (T + 1) >> 1);
+  __syncthreads();
+  const int c = blockIdx.x;
+  const int g0 = c * fp.chunk_size;
+  const int g1 = min(fp.n, g0 + fp.chunk_size);
+  const uint32_t* row = b.chunk_off + (size_t)c * T;
+  for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
+    const uint2 r = b.rect[i];
+    const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+    if (x0 > x1) continue;
+    const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | (uint32_t)i;
+    for (uint32_t y = y0; y <= y1; ++y)
+      for (uint32_t x = x0; x <= x1; ++x) {
+        const uint32_t t = y * fp.tiles_x + x;
+        const uint32_t sh = (t & 1u) * 16u;
+        const uint32_t slot = (atomicAdd(&cnt[t >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        const uint32_t pos = b.tile_start[t] + row[t] + slot;
+        if (pos < fp.pair_cap) b.pairs[pos] = key;
+      }
+  }
+}
+
 // --------------------------------------------------------------------- emit
+// Fallback emit (tile grids too large for an LDS histogram): global cursors.
 __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= fp.n) return;
@@ -498,12 +667,39 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   const int chunk = wid - tile * fp.chunks_per_tile;
   if (tile >= fp.n_tiles) return;
   const int lane = threadIdx.x & 63;
-  const int lp = chunk * 64 + lane;
-  const int lx = lp % fp.tile_w, ly = lp / fp.tile_w;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
-  const int px = tx * fp.tile_w + lx;
-  const int py = (fp.band_ty0 + tyb) * fp.tile_h + ly;
-  const bool valid = lp < fp.tile_w * fp.tile_h && px < fp.width && py < fp.height;
+  const int tile_x0 = tx * fp.tile_w;
+  const int tile_y0 = (fp.band_ty0 + tyb) * fp.tile_h;
+  // pixel footprint of this wave: an 8x8 block when the tile is a multiple of
+  // 8 in both directions, else 64 consecutive tile-local pixels (x + y*tw)
+  int lx, ly, bx0, bx1, by0, by1;
+  bool in_tile;
+  if (fp.block8) {
+    const int bpr = fp.tile_w >> 3;
+    const int cbx = (chunk % bpr) << 3, cby = (chunk / bpr) << 3;
+    lx = cbx + (lane & 7);
+    ly = cby + (lane >> 3);
+    in_tile = true;
+    bx0 = tile_x0 + cbx;
+    bx1 = bx0 + 7;
+    by0 = tile_y0 + cby;
+    by1 = by0 + 7;
+  } else {
+    const int np = fp.tile_w * fp.tile_h;
+    const int lp = chunk * 64 + lane;
+    lx = lp % fp.tile_w;
+    ly = lp / fp.tile_w;
+    in_tile = lp < np;
+    const int lp0 = chunk * 64, lp1 = min(lp0 + 63, np - 1);
+    const int r0 = lp0 / fp.tile_w, r1 = lp1 / fp.tile_w;
+    by0 = tile_y0 + r0;
+    by1 = tile_y0 + r1;
+    bx0 = tile_x0 + (r0 == r1 ? lp0 % fp.tile_w : 0);
+    bx1 = tile_x0 + (r0 == r1 ? lp1 % fp.tile_w : fp.tile_w - 1);
+  }
+  const int px = tile_x0 + lx;
+  const int py = tile_y0 + ly;
+  const bool valid = in_tile && px < fp.width && py < fp.height;
   const float pfx = (float)px, pfy = (float)py;
 
   uint32_t s, L;
@@ -518,16 +714,22 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     if (__ballot(!done) == 0ull) break;
     const uint32_t g = __builtin_amdgcn_readfirstlane(list[k]);
     if (g >= (uint32_t)fp.n) continue;  // defensive: never read past the records
-    const float* r = recf + 12 * (size_t)g;
+    const float* r = recf + 16 * (size_t)g;
     const float mx = r[0], my = r[1], k0 = r[2], k1 = r[3];
     const float k2 = r[4], k3 = r[5], cr = r[6], cg = r[7];
-    const float cb = r[8];
+    const float cb = r[8], pcut = r[9];
+    const uint32_t boxx = __float_as_uint(r[10]), boxy = __float_as_uint(r[11]);
     if (k3 == 0.0f) continue;  // con_o.w == 0 (codelets.cpp:389)
+    // wave-uniform footprint test (scalar): every pixel of this wave would skip
+    if ((int)(boxx << 16) >> 16 > bx1 || (int)boxx >> 16 < bx0 ||
+        (int)(boxy << 16) >> 16 > by1 || (int)boxy >> 16 < by0)
+      continue;
     if (!done) {
       const float dx = mx - pfx;
       const float dy = my - pfy;
       const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
-      if (!(power > 0.0f)) {
+      // power < pcut: alpha < 1/255 guaranteed (the reference's `continue`)
+      if (!(power > 0.0f) && !(power < pcut)) {
         const float v = k3 * gs_expf_nonpos(power);
         const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
         if (!(alpha < 1.0f / 255.0f)) {
@@ -562,12 +764,34 @@ void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   gs_project_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
 }
 
+size_t bin_lds_bytes(int n_tiles) { return (size_t)((n_tiles + 1) / 2) * 4; }
+
+bool bin_lds_fits(int n_tiles) { return bin_lds_bytes(n_tiles) <= kBinLdsMax; }
+
+hipError_t init_kernel_attributes() {
+  hipError_t e = hipFuncSetAttribute((const void*)gs_count_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLdsMax);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)gs_emit_chunk_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBinLdsMax);
+}
+
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (!fp.bin_global && fp.n_chunks > 0 && fp.n_tiles > 0) {
+    const size_t lds = bin_lds_bytes(fp.n_tiles);
+    gs_count_kernel<<<fp.n_chunks, 1024, lds, s>>>(fp, b);
+    gs_colscan_kernel<<<(fp.n_tiles + 63) / 64, 1024, 0, s>>>(fp, b);
+  }
   gs_scan_kernel<<<1, 1024, 0, s>>>(fp, b);
 }
 
 void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
+  if (!fp.bin_global) {
+    if (fp.n_chunks > 0 && fp.n_tiles > 0)
+      gs_emit_chunk_kernel<<<fp.n_chunks, 1024, bin_lds_bytes(fp.n_tiles), s>>>(fp, b);
+    return;
+  }
   gs_emit_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
 }
 

@@ -27,9 +27,13 @@ struct FrameParams {
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
   int chunks_per_tile;  // ceil(tw*th / 64): one wave per 64-pixel chunk
+  int block8;           // tw % 8 == 0 && th % 8 == 0: waves own 8x8 pixel blocks
   unsigned long long pair_cap;
   int write_rgba;
   int bgr_pitch;      // bytes per row of the BGR8 output
+  int bin_global;     // 1: fallback binning with global atomics
+  int chunk_size;     // Gaussians per binning chunk (<= 65535)
+  int n_chunks;
 };
 
 // Device workspace of one renderer.
@@ -40,7 +44,7 @@ struct Buffers {
   const float4* rot;        // quaternion (w x y z)
   const float4* scale_gid;  // sx sy sz gid
   // per-Gaussian projection outputs
-  float4* rec;              // 3 x float4: mx my cx cy | cz cw r g | b radius clipz 0
+  float4* rec;              // 4 x float4 (64 B): mx my k0 k1 | k2 k3 r g | b pcut boxx boxy | radius clipz 0 0
   uint32_t* depth_key;      // order-preserving key of clip z
   uint2* rect;              // (tx0 | tx1 << 16, ty0 | ty1 << 16), band-relative rows
   // binning
@@ -51,6 +55,8 @@ struct Buffers {
   unsigned long long* pairs_alt;  // [pair_cap]  scratch of the large-list sort
   uint32_t* list;           // [pair_cap]  depth-sorted Gaussian indices
   uint32_t* big_tiles;      // [n_tiles]
+  uint32_t* chunk_off;      // [n_chunks][n_tiles] chunk histograms -> offsets
+  uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
   uint32_t* counters;       // [8]: 0 n_big, 1 big_next, 2 n_rendered, 3 overflow,
                             //      4 max_list, 5 n_pairs (low), 6 n_pairs (high)
   // outputs
@@ -60,6 +66,11 @@ struct Buffers {
 
 constexpr int GS_STAGE_EVENTS = 6;  // profile events: before project .. after blend
 constexpr int kSortLdsCap = 4096;  // largest tile list sorted in LDS by one workgroup
+constexpr size_t kBinLdsMax = 160 * 1024;  // LDS of one CU: chunk histograms up to 81920 tiles
+
+size_t bin_lds_bytes(int n_tiles);
+bool bin_lds_fits(int n_tiles);
+hipError_t init_kernel_attributes();
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s);

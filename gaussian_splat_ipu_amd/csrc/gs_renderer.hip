@@ -57,6 +57,8 @@ struct gs_renderer {
   void* d_tiles = nullptr;      // tile_start[n_tiles+1], tile_cursor, big_tiles
   void* d_pairs = nullptr;      // pairs, pairs_alt, list
   void* d_out = nullptr;        // rgba f32 + bgr8
+  void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
+  int bin_global = 0, chunk_size = 0, n_chunks = 0;
   size_t zero_bytes = 0;
   size_t bgr_bytes = 0;
   gsk::Buffers buf{};
@@ -117,7 +119,7 @@ void release(gs_renderer* r) {
   if (!r) return;
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
-  for (void* p : {r->d_scene, r->d_gauss, r->d_zero, r->d_tiles, r->d_out})
+  for (void* p : {r->d_scene, r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk})
     if (p) (void)hipFree(p);
   free_pairs(r);
   if (r->h_counters) (void)hipHostFree(r->h_counters);
@@ -161,9 +163,13 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.n = (int)r->n;
   fp.n_tiles = r->n_tiles;
   fp.chunks_per_tile = (int)((r->cfg.tile_width * r->cfg.tile_height + 63) / 64);
+  fp.block8 = (r->cfg.tile_width % 8 == 0 && r->cfg.tile_height % 8 == 0) ? 1 : 0;
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
+  fp.bin_global = r->bin_global;
+  fp.chunk_size = r->chunk_size;
+  fp.n_chunks = r->n_chunks;
   return fp;
 }
 
@@ -357,11 +363,15 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   r->buf.rot = sc + 2 * nn;
   r->buf.scale_gid = sc + 3 * nn;
 
-  if ((e = hipMalloc(&r->d_gauss, nn * (48 + 4 + 8))) != hipSuccess)
+  // per Gaussian: 64-B record, 8-B tile rectangle, 4-B depth key; plus V per
+  // project workgroup
+  const size_t nblk = (nn + 255) / 256;
+  if ((e = hipMalloc(&r->d_gauss, nn * (64 + 8 + 4) + nblk * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(per-Gaussian)"));
   r->buf.rec = (float4*)r->d_gauss;
-  r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 48);
-  r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 56);
+  r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 64);
+  r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
+  r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 76);
 
   const size_t T = (size_t)std::max(r->n_tiles, 1);
   r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
@@ -375,6 +385,20 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   r->buf.big_tiles = r->buf.tile_cursor + T;
   if ((e = hipMemset(r->d_tiles, 0, (T + 1 + T + T) * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(tiles)"));
+
+  // binning mode: chunked LDS histograms unless the band's tile grid is too
+  // large for one CU's LDS (or the caller asks for the global-atomic path)
+  r->bin_global = ((cfg->flags & GS_FLAG_BIN_GLOBAL) || !gsk::bin_lds_fits(r->n_tiles)) ? 1 : 0;
+  if (!r->bin_global && n > 0 && r->n_tiles > 0) {
+    if ((e = gsk::init_kernel_attributes()) != hipSuccess) return fail(hip_fail(e, "hipFuncSetAttribute"));
+    size_t cs = std::max<size_t>(4096, (n + 255) / 256);
+    cs = std::min<size_t>(cs, 65535);
+    r->chunk_size = (int)cs;
+    r->n_chunks = (int)((n + cs - 1) / cs);
+    if ((e = hipMalloc(&r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4)) != hipSuccess)
+      return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
+    r->buf.chunk_off = (uint32_t*)r->d_chunk;
+  }
 
   uint64_t cap = cfg->pair_capacity;
   if (cap == 0) cap = std::max<uint64_t>(1u << 20, 8ull * n);
@@ -582,14 +606,14 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
-  std::vector<float> rec(r->n * 12);
+  std::vector<float> rec(r->n * 16);
   std::vector<uint32_t> rect(r->n * 2);
   if (r->n) {
-    GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 48, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 64, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(rect.data(), r->buf.rect, r->n * 8, hipMemcpyDeviceToHost));
   }
   for (size_t i = 0; i < r->n; ++i) {
-    const float* q = &rec[i * 12];
+    const float* q = &rec[i * 16];
     float* o = dst + i * 12;
     o[0] = q[0];  // mean2d
     o[1] = q[1];
@@ -597,8 +621,8 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     o[3] = q[3];
     o[4] = q[4];
     o[5] = q[5];
-    o[6] = q[10];  // clip z
-    o[7] = q[9];   // radius
+    o[6] = q[13];  // clip z
+    o[7] = q[12];  // radius
     const uint32_t rx = rect[i * 2], ry = rect[i * 2 + 1];
     o[8] = (float)(rx & 0xFFFF);
     o[9] = (float)(ry & 0xFFFF);

@@ -21,6 +21,7 @@ import numpy as np
 
 from . import camera
 from ._lib import (
+    GS_FLAG_BIN_GLOBAL,
     GS_FLAG_NO_RGBA32F,
     GS_FLAG_PROFILE,
     GS_K_COUNT,
@@ -58,6 +59,7 @@ class GpuSplatter:
         pair_capacity: int = 0,
         write_rgba: bool = True,
         profile: bool = False,
+        bin_global: bool = False,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -75,7 +77,11 @@ class GpuSplatter:
         cfg.device = device
         cfg.band_index, cfg.band_count = band_index, band_count
         cfg.pair_capacity = pair_capacity
-        cfg.flags = (0 if write_rgba else GS_FLAG_NO_RGBA32F) | (GS_FLAG_PROFILE if profile else 0)
+        cfg.flags = (
+            (0 if write_rgba else GS_FLAG_NO_RGBA32F)
+            | (GS_FLAG_PROFILE if profile else 0)
+            | (GS_FLAG_BIN_GLOBAL if bin_global else 0)
+        )
         self.cfg = cfg
         h = C.c_void_p()
         gp = g.ctypes.data_as(C.POINTER(Gaussian3D)) if self.n else None

@@ -64,6 +64,8 @@ typedef struct gs_config {
 
 #define GS_FLAG_NO_RGBA32F 1u  /* skip the RGBA f32 framebuffer store (BGR8 only) */
 #define GS_FLAG_PROFILE 2u     /* record HIP events around every kernel     */
+#define GS_FLAG_BIN_GLOBAL 4u  /* bin with global atomics instead of the chunked
+                                  LDS histograms (automatic for > 81920 tiles) */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */

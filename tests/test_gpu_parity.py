@@ -31,7 +31,7 @@ def assert_same_bits(a, b, what=""):
 
 
 def _frame_pair(g, view, proj, W, H, TW, TH, scale_div, fov=None, guard_tile=None, band=None, band_count=1,
-                band_index=0, pair_capacity=0):
+                band_index=0, pair_capacity=0, bin_global=False):
     from gaussian_splat_ipu_amd import camera
     from gaussian_splat_ipu_amd.splatter import GpuSplatter
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
@@ -40,7 +40,7 @@ def _frame_pair(g, view, proj, W, H, TW, TH, scale_div, fov=None, guard_tile=Non
     fov = camera.FOV_DEFAULT if fov is None else fov
     fb = TiledFramebuffer(W, H, TW, TH)
     s = GpuSplatter(g, fb, device=0, guard_tile=guard_tile, band_index=band_index, band_count=band_count,
-                    pair_capacity=pair_capacity)
+                    pair_capacity=pair_capacity, bin_global=bin_global)
     s.set_view_wire(view)
     s.set_projection_wire(proj)
     s.update_focal_lengths(fov, scale_div)
@@ -104,15 +104,16 @@ def test_pc12_reference_geometry_720p(pc12, scale_div):
     assert ref["stats"]["n_pairs"] > 50000
 
 
-@pytest.mark.parametrize("tw,th", [(16, 16), (48, 30), (32, 20)])
-def test_pc12_1080p(pc12, tw, th):
+@pytest.mark.parametrize("tw,th,bin_global", [(16, 16, False), (16, 16, True), (48, 30, False), (32, 20, False)])
+def test_pc12_1080p(pc12, tw, th, bin_global):
     """config 2: point_cloud_12 at 1920x1080 (16x16 production tiles, 48x30 =
-    the reference macros at 1080p, 32x20); 1080/16 leaves a partial tile row."""
+    the reference macros at 1080p, 32x20); 1080/16 leaves a partial tile row.
+    Both binning paths (chunked LDS histograms, global atomics)."""
     from gaussian_splat_ipu_amd import camera
 
     g, bb = pc12
     view, proj = camera.headless(bb, 1920, 1080)
-    s, f = _frame_pair(g, view, proj, 1920, 1080, tw, th, 1.0)
+    s, f = _frame_pair(g, view, proj, 1920, 1080, tw, th, 1.0, bin_global=bin_global)
     _assert_parity(s, f, g)
 
 
@@ -188,6 +189,28 @@ def test_edge_cases(built):
     s, f = _frame_pair(a[:0], view, proj, 800, 600, 16, 16, 1.0)
     assert s.stats()["n_pairs"] == 0
     assert not s.get_frame_buffer().any()
+
+
+@pytest.mark.parametrize("tw,th", [(16, 16), (32, 20)])
+def test_blend_culling_is_decision_preserving(built, tw, th):
+    """Stress the blend's footprint culling (pcut + wave boxes): strongly
+    anisotropic Gaussians and opacities around the 1/255 threshold, negative,
+    tiny and huge.  The frame must stay bit-identical to the oracle, which
+    evaluates every list entry."""
+    from gaussian_splat_ipu_amd import camera, scene
+
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=30000, seed=11, sh_degree=0, log_scale_mu=-4.0)))
+    a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
+    rng = np.random.default_rng(5)
+    n = a.shape[0]
+    # anisotropy: one axis up to e^4 larger
+    a[:, 12] += rng.uniform(0.0, 4.0, n).astype(np.float32)
+    ops = np.array([-3.0, 0.0, 1 / 255 - 1e-6, 1 / 255, 1 / 255 + 1e-6, 0.004, 0.01, 0.3, 1.0, 8.0, 50.0, 1e6],
+                   np.float32)
+    a[:, 7] = ops[rng.integers(0, ops.size, n)]
+    view, proj = camera.headless(bb, 1280, 720)
+    s, f = _frame_pair(a, view, proj, 1280, 720, tw, th, 1.0)
+    _assert_parity(s, f, a)
 
 
 def test_overflow_grows_capacity(pc12):
