@@ -705,46 +705,70 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   uint32_t s, L;
   tile_segment(fp, b, tile, s, L);
   const uint32_t* __restrict__ list = b.list + s;
-  const float* __restrict__ recf = reinterpret_cast<const float*>(b.rec);
+
+  // wave-private staging of one batch of 64 records (48 B each) in LDS
+  __shared__ float4 s_rec[4][3][64];
+  float4(*const st)[64] = s_rec[wave];
 
   float T = 1.0f;
   float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
   bool done = !valid;
-  for (uint32_t k = 0; k < L; ++k) {
+  for (uint32_t base = 0; base < L; base += 64) {
     if (__ballot(!done) == 0ull) break;
-    const uint32_t g = __builtin_amdgcn_readfirstlane(list[k]);
-    if (g >= (uint32_t)fp.n) continue;  // defensive: never read past the records
-    const float* r = recf + 16 * (size_t)g;
-    const float mx = r[0], my = r[1], k0 = r[2], k1 = r[3];
-    const float k2 = r[4], k3 = r[5], cr = r[6], cg = r[7];
-    const float cb = r[8], pcut = r[9];
-    const uint32_t boxx = __float_as_uint(r[10]), boxy = __float_as_uint(r[11]);
-    if (k3 == 0.0f) continue;  // con_o.w == 0 (codelets.cpp:389)
-    // wave-uniform footprint test (scalar): every pixel of this wave would skip
-    if ((int)(boxx << 16) >> 16 > bx1 || (int)boxx >> 16 < bx0 ||
-        (int)(boxy << 16) >> 16 > by1 || (int)boxy >> 16 < by0)
-      continue;
-    if (!done) {
-      const float dx = mx - pfx;
-      const float dy = my - pfy;
-      const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
-      // power < pcut: alpha < 1/255 guaranteed (the reference's `continue`)
-      if (!(power > 0.0f) && !(power < pcut)) {
-        const float v = k3 * gs_expf_nonpos(power);
-        const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
-        if (!(alpha < 1.0f / 255.0f)) {
-          const float test_T = T * (1.0f - alpha);
-          if (test_T < 0.0001f) {
-            done = true;  // break (codelets.cpp:406-408)
-          } else {
-            C0 = C0 + (cr * alpha) * T;  // colour += gCont * alpha * T
-            C1 = C1 + (cg * alpha) * T;
-            C2 = C2 + (cb * alpha) * T;
-            C3 = C3 + (k3 * alpha) * T;
-            T = test_T;
+    // one coalesced load of 64 list entries + one gather of their records;
+    // the footprint test runs lane-parallel and leaves a mask of the entries
+    // that can change a pixel of this wave (the others all `continue`)
+    const uint32_t k = base + lane;
+    bool rel = false;
+    if (k < L) {
+      const uint32_t g = list[k];
+      if (g < (uint32_t)fp.n) {  // defensive: never read past the records
+        const float4* q = b.rec + 4 * (size_t)g;
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+        const uint32_t boxx = __float_as_uint(q2.z), boxy = __float_as_uint(q2.w);
+        rel = !(q1.y == 0.0f) &&  // con_o.w == 0 (codelets.cpp:389)
+              !((int)(boxx << 16) >> 16 > bx1 || (int)boxx >> 16 < bx0 ||
+                (int)(boxy << 16) >> 16 > by1 || (int)boxy >> 16 < by0);
+        st[0][lane] = q0;
+        st[1][lane] = q1;
+        st[2][lane] = q2;
+      }
+    }
+    unsigned long long mask = __ballot(rel);
+    // the lanes' LDS stores precede the broadcast reads below (same wave)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    while (mask) {
+      const int j = __builtin_ctzll(mask);  // list order: ascending bits
+      mask &= mask - 1ull;
+      const float4 q0 = st[0][j], q1 = st[1][j], q2 = st[2][j];
+      const float mx = q0.x, my = q0.y, k0 = q0.z, k1 = q0.w;
+      const float k2 = q1.x, k3 = q1.y, cr = q1.z, cg = q1.w;
+      const float cb = q2.x, pcut = q2.y;
+      if (!done) {
+        const float dx = mx - pfx;
+        const float dy = my - pfy;
+        const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
+        // power < pcut: alpha < 1/255 guaranteed (the reference's `continue`)
+        if (!(power > 0.0f) && !(power < pcut)) {
+          const float v = k3 * gs_expf_nonpos(power);
+          const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
+          if (!(alpha < 1.0f / 255.0f)) {
+            const float test_T = T * (1.0f - alpha);
+            if (test_T < 0.0001f) {
+              done = true;  // break (codelets.cpp:406-408)
+            } else {
+              C0 = C0 + (cr * alpha) * T;  // colour += gCont * alpha * T
+              C1 = C1 + (cg * alpha) * T;
+              C2 = C2 + (cb * alpha) * T;
+              C3 = C3 + (k3 * alpha) * T;
+              T = test_T;
+            }
           }
         }
       }
+      if (__ballot(!done) == 0ull) break;
     }
   }
   if (!valid) return;

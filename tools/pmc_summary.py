@@ -1,0 +1,90 @@
+"""Summarise rocprofv3 output of tools/profile.sh into per-kernel averages.
+
+    python tools/pmc_summary.py gpurun_out/prof [--config 1000000@1920x1080/t16/w1] [--json out.json]
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half of the bytes of a
+wide streaming read, so reads are doubled ("corrected"); both the raw and the
+corrected numbers are written.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+
+
+def short(name: str) -> str:
+    m = re.search(r"(gs_[a-z_0-9]+)_kernel", name)
+    if m:
+        return m.group(1)
+    return name.split("(")[0][:40]
+
+
+def load_counters(d):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def load_stats(d):
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                out[short(row["Name"])] = {
+                    "calls": int(row["Calls"]),
+                    "avg_us": float(row["AverageNs"]) / 1e3,
+                    "pct": float(row["Percentage"]),
+                }
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--config", default="1000000@1920x1080/t16/w1")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    ctr = load_counters(a.dir)
+    st = load_stats(a.dir)
+    kernels = {}
+    for k in sorted(set(ctr) | set(st)):
+        c = ctr.get(k, {})
+        e = dict(st.get(k, {}))
+        if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
+            rd = c.get("FETCH_SIZE", 0.0) * 1024
+            wr = c.get("WRITE_SIZE", 0.0) * 1024
+            e["fetch_bytes_raw"] = rd
+            e["write_bytes"] = wr
+            e["hbm_bytes_per_launch"] = 2 * rd + wr
+        for name in sorted(c):
+            if name not in ("FETCH_SIZE", "WRITE_SIZE"):
+                e[name] = c[name]
+        if "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"] > 0:
+            wc = c["SQ_WAVE_CYCLES"]
+            e["frac_wait_any"] = c.get("SQ_WAIT_ANY", 0) / wc
+            e["frac_valu_active"] = c.get("SQ_ACTIVE_INST_VALU", 0) / wc
+            if "SQ_WAIT_INST_ANY" in c:
+                e["frac_wait_inst"] = c["SQ_WAIT_INST_ANY"] / wc
+        if "SQ_WAVES" in c and c["SQ_WAVES"] > 0:
+            e["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
+            e["smem_insts_per_wave"] = c.get("SQ_INSTS_SMEM", 0) / c["SQ_WAVES"]
+        kernels[k] = e
+    out = {"config": a.config, "source": os.path.abspath(a.dir), "kernels": kernels}
+    for k, e in kernels.items():
+        keys = ["avg_us", "hbm_bytes_per_launch", "frac_wait_any", "frac_valu_active", "valu_insts_per_wave"]
+        print(k, {x: (round(e[x], 3) if isinstance(e.get(x), float) else e.get(x)) for x in keys if x in e})
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
