@@ -508,41 +508,193 @@ __device__ __forceinline__ void tile_segment(const FrameParams& fp, const Buffer
 // Small and medium lists: bitonic network over the padded power-of-two list
 // in LDS (32 KB), 256 threads.  Keys are unique (the index is in the low
 // word), so the order is total and deterministic.
-__global__ __launch_bounds__(256) void gs_sort_kernel(FrameParams fp, Buffers b) {
-  __shared__ unsigned long long keys[kSortLdsCap];
-  const int t = blockIdx.x;
-  const int tid = threadIdx.x;
+// Register bitonic sort of E*64 keys held by one wave: element i = lane*E + e
+// (each lane owns E consecutive keys).  Strides < E compare two registers of
+// the same lane; strides >= E exchange register e with lane ^ (j / E)
+// (ds_bpermute).  No LDS arrays, no barriers.  The k / j loops stay rolled (the
+// network runs once per wave; a fully unrolled one is instruction-fetch bound).
+template <int E, int J>
+__device__ __forceinline__ void reg_stage(unsigned long long (&v)[E], int i0, int k) {
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int pe = e ^ J;
+    if (pe > e) {
+      const bool asc = ((i0 + e) & k) == 0;  // i0 = global index of the lane's first key
+      const unsigned long long a = v[e], c = v[pe];
+      const bool sw = (a > c) == asc;
+      v[e] = sw ? c : a;
+      v[pe] = sw ? a : c;
+    }
+  }
+}
+
+// In-wave stages j = jmax .. 1 of bitonic step k; ibase = global index of this
+// wave's first key (the direction of a compare depends on the global index).
+template <int E>
+__device__ __forceinline__ void wave_merge(unsigned long long (&v)[E], int lane, int ibase, int k,
+                                           int jmax) {
+  for (int j = jmax; j > 0; j >>= 1) {
+    if (j < E) {
+      const int i0 = ibase + lane * E;
+      switch (j) {
+        case 1: if constexpr (E > 1) reg_stage<E, 1>(v, i0, k); break;
+        case 2: if constexpr (E > 2) reg_stage<E, 2>(v, i0, k); break;
+        case 4: if constexpr (E > 4) reg_stage<E, 4>(v, i0, k); break;
+        default: break;
+      }
+    } else {
+      const int lj = j / E;
+      const bool lower = (lane & lj) == 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = ibase + lane * E + e;
+        const unsigned long long o = __shfl_xor(v[e], lj, 64);
+        const bool asc = (i & k) == 0;
+        const bool take_min = lower == asc;
+        const bool gt = v[e] > o;
+        v[e] = (take_min == gt) ? o : v[e];
+      }
+    }
+  }
+}
+
+template <int E>
+__device__ __forceinline__ void wave_bitonic(unsigned long long (&v)[E], int lane) {
+  constexpr int n = E * 64;
+  for (int k = 2; k <= n; k <<= 1) wave_merge<E>(v, lane, 0, k, k >> 1);
+}
+
+// W waves x 64 lanes x E keys = up to W*64*E keys per workgroup: every wave
+// sorts its slice in registers; the strides >= 64*E (3 of them for 2048 keys)
+// exchange through LDS between barriers.
+template <int E, int W>
+__device__ __forceinline__ void block_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
+                                                unsigned long long* lds) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  constexpr int WN = 64 * E;
+  const int ibase = wave * WN;
+  uint32_t n2 = WN;
+  while (n2 < L) n2 <<= 1;
+  unsigned long long v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t i = (uint32_t)(ibase + lane * E + e);
+    v[e] = i < L ? b.pairs[s + i] : ~0ull;
+  }
+  for (int k = 2; k <= (int)n2; k <<= 1) {
+    int j = k >> 1;
+    for (; j >= WN; j >>= 1) {  // cross-wave stage through LDS
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e) lds[ibase + lane * E + e] = v[e];
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = ibase + lane * E + e;
+        const unsigned long long o = lds[i ^ j];
+        const bool asc = (i & k) == 0;
+        const bool take_min = ((i & j) == 0) == asc;
+        const bool gt = v[e] > o;
+        v[e] = (take_min == gt) ? o : v[e];
+      }
+    }
+    if (ibase < (int)n2) wave_merge<E>(v, lane, ibase, k, j);
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t i = (uint32_t)(ibase + lane * E + e);
+    if (i < L) b.list[s + i] = (uint32_t)v[e];
+  }
+}
+
+template <int E>
+__device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uint32_t L, int lane) {
+  unsigned long long v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t i = (uint32_t)(lane * E + e);
+    v[e] = i < L ? b.pairs[s + i] : ~0ull;
+  }
+  wave_bitonic<E>(v, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t i = (uint32_t)(lane * E + e);
+    if (i < L) b.list[s + i] = (uint32_t)v[e];
+  }
+}
+
+// One wave per tile: lists up to 1024 keys are sorted in registers; longer
+// lists are queued for the LDS sort (<= kSortLdsCap) or the radix sort.
+__global__ __launch_bounds__(256) void gs_sort_small_kernel(FrameParams fp, Buffers b) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = blockIdx.x * 4 + wave;
+  const int lane = threadIdx.x & 63;
+  if (t >= fp.n_tiles) return;
   uint32_t s, L;
   tile_segment(fp, b, t, s, L);
   if (L == 0) return;
-  if (L > (uint32_t)kSortLdsCap) {
-    if (tid == 0) b.big_tiles[atomicAdd(&b.counters[0], 1u)] = (uint32_t)t;
-    return;
-  }
-  if (L == 1) {
-    if (tid == 0) b.list[s] = (uint32_t)b.pairs[s];
-    return;
-  }
-  uint32_t n2 = 2;
-  while (n2 < L) n2 <<= 1;
-  for (uint32_t i = tid; i < n2; i += 256) keys[i] = i < L ? b.pairs[s + i] : ~0ull;
-  __syncthreads();
-  for (uint32_t k = 2; k <= n2; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < (n2 >> 1); i += 256) {
-        const uint32_t lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
-        const uint32_t hi = lo + j;
-        const bool asc = (lo & k) == 0;
-        const unsigned long long x = keys[lo], y = keys[hi];
-        if ((x > y) == asc) {
-          keys[lo] = y;
-          keys[hi] = x;
-        }
-      }
-      __syncthreads();
+  if (L > kSortRegCap) {
+    if (lane == 0) {
+      if (L > (uint32_t)kSortLdsCap)
+        b.big_tiles[atomicAdd(&b.counters[0], 1u)] = (uint32_t)t;
+      else
+        b.medium_tiles[atomicAdd(&b.counters[7], 1u)] = (uint32_t)t;
     }
+    return;
   }
-  for (uint32_t i = tid; i < L; i += 256) b.list[s + i] = (uint32_t)keys[i];
+  if (L <= 64u)
+    wave_sort_tile<1>(b, s, L, lane);
+  else if (L <= 128u)
+    wave_sort_tile<2>(b, s, L, lane);
+  else if (L <= 256u)
+    wave_sort_tile<4>(b, s, L, lane);
+  else
+    wave_sort_tile<8>(b, s, L, lane);
+}
+
+// Medium lists (1024 < L <= kSortLdsCap): bitonic network over the padded
+// power-of-two list in LDS (32 KB), 256 threads; workgroups pull tiles from the
+// queue the small-sort kernel filled.  Keys are unique (the index is in the
+// low word), so the order is total and deterministic.
+__global__ __launch_bounds__(256) void gs_sort_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long keys[kSortLdsCap];
+  __shared__ uint32_t s_item;
+  const int tid = threadIdx.x;
+  const uint32_t n_med = b.counters[7];
+  // one workgroup per queued tile (grid = n_tiles; the surplus exits at once)
+  for (uint32_t item = blockIdx.x; item < n_med; item += gridDim.x) {
+    (void)s_item;
+    const int t = (int)b.medium_tiles[item];
+    uint32_t s, L;
+    tile_segment(fp, b, t, s, L);
+    if (L <= 2048u) {  // 4 waves x 512 keys in registers, 3 LDS exchanges
+      block_sort_tile<8, 4>(b, s, L, keys);
+      __syncthreads();
+      continue;
+    }
+    uint32_t n2 = 2;
+    while (n2 < L) n2 <<= 1;
+    for (uint32_t i = tid; i < n2; i += 256) keys[i] = i < L ? b.pairs[s + i] : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = tid; i < (n2 >> 1); i += 256) {
+          const uint32_t lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+          const uint32_t hi = lo + j;
+          const bool asc = (lo & k) == 0;
+          const unsigned long long x = keys[lo], y = keys[hi];
+          if ((x > y) == asc) {
+            keys[lo] = y;
+            keys[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (uint32_t i = tid; i < L; i += 256) b.list[s + i] = (uint32_t)keys[i];
+    __syncthreads();
+  }
 }
 
 // Large lists: a block-wide stable LSD radix sort (8 passes x 8 bits) over the
@@ -821,6 +973,7 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
+  gs_sort_small_kernel<<<(fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
   gs_sort_kernel<<<fp.n_tiles, 256, 0, s>>>(fp, b);
   gs_sort_big_kernel<<<64, 1024, 0, s>>>(fp, b);
 }
