@@ -328,60 +328,106 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
 }
 
 // --------------------------------------------------------------------- scan
-// One workgroup of 1024 threads: tile_start = exclusive scan(tile_count).
+// One workgroup of 1024 threads, rounds of 8192 tiles (8 per thread, held in
+// registers): tile_start = exclusive scan(tile_count), max list length, and
+// the sort queues -- tiles too long for the one-wave register sort are
+// compacted into medium_tiles / big_tiles here (no contended atomics).
+__device__ __forceinline__ int sort_class(uint32_t L) {
+  return L <= kSortRegCap ? 0 : (L <= (uint32_t)kSortLdsCap ? 1 : 2);
+}
+
 __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b) {
   __shared__ unsigned long long wsum[16];
+  __shared__ uint32_t wq[16];  // per wave: medium count | big count << 16
   __shared__ uint32_t wmax[16];
   __shared__ uint32_t wvis[16];
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int per = (T + 1023) / 1024;
-  const int beg = min(T, tid * per), end = min(T, beg + per);
-  unsigned long long sum = 0;
-  uint32_t mx = 0;
-  for (int i = beg; i < end; ++i) {
-    const uint32_t v = b.tile_count[i];
-    sum += v;
-    mx = max(mx, v);
-  }
-  // wave inclusive scan
-  unsigned long long inc = sum;
+  unsigned long long carry = 0;
+  uint32_t med_base = 0, big_base = 0, mx = 0;
+  for (int r0 = 0; r0 < T; r0 += 8192) {
+    const int i0 = r0 + tid * 8;
+    uint32_t c[8];
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned long long o = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += o;
+    for (int j = 0; j < 8; ++j) c[j] = (i0 + j < T) ? b.tile_count[i0 + j] : 0u;
+    unsigned long long sum = 0;
+    uint32_t q = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sum += c[j];
+      mx = max(mx, c[j]);
+      const int cl = sort_class(c[j]);
+      q += cl == 1 ? 1u : (cl == 2 ? 0x10000u : 0u);
+    }
+    unsigned long long inc = sum;
+    uint32_t qinc = q;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long o = __shfl_up(inc, d, 64);
+      const uint32_t oq = __shfl_up(qinc, d, 64);
+      if (lane >= d) {
+        inc += o;
+        qinc += oq;
+      }
+    }
+    if (lane == 63) {
+      wsum[wave] = inc;
+      wq[wave] = qinc;
+    }
+    __syncthreads();
+    unsigned long long base = carry, total = carry;
+    uint32_t qbase = 0, qtot = 0;
+    for (int w = 0; w < 16; ++w) {
+      if (w < wave) {
+        base += wsum[w];
+        qbase += wq[w];
+      }
+      total += wsum[w];
+      qtot += wq[w];
+    }
+    unsigned long long run = base + inc - sum;
+    uint32_t med = med_base + (qbase & 0xFFFFu) + ((qinc - q) & 0xFFFFu);
+    uint32_t big = big_base + (qbase >> 16) + ((qinc - q) >> 16);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = i0 + j;
+      if (i < T) {
+        b.tile_start[i] = (uint32_t)run;
+        if (fp.bin_global) b.tile_cursor[i] = (uint32_t)run;
+        const int cl = sort_class(c[j]);
+        if (cl == 1) b.medium_tiles[med++] = (uint32_t)i;
+        if (cl == 2) b.big_tiles[big++] = (uint32_t)i;
+      }
+      run += c[j];
+    }
+    carry = total;
+    med_base += qtot & 0xFFFFu;
+    big_base += qtot >> 16;
+    __syncthreads();  // wsum / wq are rewritten by the next round
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-  if (lane == 63) wsum[wave] = inc;
-  if (lane == 0) wmax[wave] = mx;
-  __syncthreads();
-  unsigned long long base = 0;
-  for (int w = 0; w < wave; ++w) base += wsum[w];
-  unsigned long long run = base + inc - sum;  // exclusive prefix of this thread
-  for (int i = beg; i < end; ++i) {
-    b.tile_start[i] = (uint32_t)run;
-    b.tile_cursor[i] = (uint32_t)run;
-    run += b.tile_count[i];
-  }
   // V = sum of the project workgroups' counts
   uint32_t vsum = 0;
   const int nb = (fp.n + 255) / 256;
   for (int i = tid; i < nb; i += 1024) vsum += b.block_rendered[i];
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
-  if (lane == 0) wvis[wave] = vsum;
+  if (lane == 0) {
+    wvis[wave] = vsum;
+    wmax[wave] = mx;
+  }
   __syncthreads();
-  if (tid == 1023) {
-    uint32_t vis = 0;
-    for (int w = 0; w < 16; ++w) vis += wvis[w];
-    b.counters[2] = vis;
-    unsigned long long total = 0;
-    uint32_t m = 0;
+  if (tid == 0) {
+    uint32_t vis = 0, m = 0;
     for (int w = 0; w < 16; ++w) {
-      total += wsum[w];
+      vis += wvis[w];
       m = max(m, wmax[w]);
     }
+    b.counters[0] = big_base;
+    b.counters[2] = vis;
+    b.counters[7] = med_base;
+    const unsigned long long total = carry;
     b.tile_start[T] = (uint32_t)(total < 0xFFFFFFFFull ? total : 0xFFFFFFFFull);
     b.counters[3] = total > fp.pair_cap ? 1u : 0u;
     b.counters[4] = m;
@@ -528,6 +574,50 @@ __device__ __forceinline__ void reg_stage(unsigned long long (&v)[E], int i0, in
   }
 }
 
+// Value of lane ^ lj (lj = 1 .. 32, wave-uniform) without an LDS round trip:
+// DPP quad_perm for 1 / 2, row_shl / row_shr for 4 / 8 (lane i reads i + n /
+// i - n inside its row of 16), v_permlane16_swap / v_permlane32_swap for 16 / 32.
+template <int LJ>
+__device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x, int lane) {
+  if constexpr (LJ == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  } else if constexpr (LJ == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  } else if constexpr (LJ == 4 || LJ == 8) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x100 | LJ, 0xF, 0xF, false);
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x110 | LJ, 0xF, 0xF, false);
+    return (lane & LJ) ? dn : up;
+  } else if constexpr (LJ == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (lane & 16) ? p[0] : p[1];
+  } else {
+    const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (lane & 32) ? p[0] : p[1];
+  }
+}
+
+template <int LJ>
+__device__ __forceinline__ unsigned long long xor_lane_u64(unsigned long long x, int lane) {
+  const uint32_t lo = xor_lane_u32<LJ>((uint32_t)x, lane);
+  const uint32_t hi = xor_lane_u32<LJ>((uint32_t)(x >> 32), lane);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// One cross-lane stage: every register exchanged with lane ^ LJ.
+template <int E, int LJ>
+__device__ __forceinline__ void lane_stage(unsigned long long (&v)[E], int lane, int ibase, int k) {
+  const bool lower = (lane & LJ) == 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = ibase + lane * E + e;
+    const unsigned long long o = xor_lane_u64<LJ>(v[e], lane);
+    const bool asc = (i & k) == 0;
+    const bool take_min = lower == asc;
+    const bool gt = v[e] > o;
+    v[e] = (take_min == gt) ? o : v[e];
+  }
+}
+
 // In-wave stages j = jmax .. 1 of bitonic step k; ibase = global index of this
 // wave's first key (the direction of a compare depends on the global index).
 template <int E>
@@ -543,16 +633,13 @@ __device__ __forceinline__ void wave_merge(unsigned long long (&v)[E], int lane,
         default: break;
       }
     } else {
-      const int lj = j / E;
-      const bool lower = (lane & lj) == 0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = ibase + lane * E + e;
-        const unsigned long long o = __shfl_xor(v[e], lj, 64);
-        const bool asc = (i & k) == 0;
-        const bool take_min = lower == asc;
-        const bool gt = v[e] > o;
-        v[e] = (take_min == gt) ? o : v[e];
+      switch (j / E) {
+        case 1: lane_stage<E, 1>(v, lane, ibase, k); break;
+        case 2: lane_stage<E, 2>(v, lane, ibase, k); break;
+        case 4: lane_stage<E, 4>(v, lane, ibase, k); break;
+        case 8: lane_stage<E, 8>(v, lane, ibase, k); break;
+        case 16: lane_stage<E, 16>(v, lane, ibase, k); break;
+        default: lane_stage<E, 32>(v, lane, ibase, k); break;
       }
     }
   }
@@ -631,18 +718,11 @@ __global__ __launch_bounds__(256) void gs_sort_small_kernel(FrameParams fp, Buff
   const int t = blockIdx.x * 4 + wave;
   const int lane = threadIdx.x & 63;
   if (t >= fp.n_tiles) return;
+  // longer lists were queued for the medium / big sorts by the scan kernel
+  if (sort_class(b.tile_count[t]) != 0) return;
   uint32_t s, L;
   tile_segment(fp, b, t, s, L);
   if (L == 0) return;
-  if (L > kSortRegCap) {
-    if (lane == 0) {
-      if (L > (uint32_t)kSortLdsCap)
-        b.big_tiles[atomicAdd(&b.counters[0], 1u)] = (uint32_t)t;
-      else
-        b.medium_tiles[atomicAdd(&b.counters[7], 1u)] = (uint32_t)t;
-    }
-    return;
-  }
   if (L <= 64u)
     wave_sort_tile<1>(b, s, L, lane);
   else if (L <= 128u)

@@ -22,5 +22,6 @@ for p in ${PASSES:-stats fetch write sq1 sq2}; do
     write) run pmc_write 600 --pmc WRITE_SIZE ;;
     sq1) run pmc_sq1 600 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU ;;
     sq2) run pmc_sq2 600 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE ;;
+    lds) run pmc_lds 600 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_UNALIGNED_STALL SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU ;;
   esac
 done
