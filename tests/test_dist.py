@@ -1,0 +1,70 @@
+"""Multi-process path on CPU (gloo, world size 2 and 3): every rank renders
+its row band (here with the CPU oracle -- the GPU path's bands are checked
+against the same oracle in test_gpu_parity.py), pads it, and one all_gather
+assembles the frame.  The assembled frame must equal the single-process
+frame bit for bit, and the max-over-ranks timing reduction must work."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gaussian_splat_ipu_amd import camera, dist as gdist, scene
+        from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+        from oracle import oracle as O
+
+        g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=4, sh_degree=0)))
+        W, H, T = 640, 360, 16
+        fb = TiledFramebuffer(W, H, T, T)
+        view, proj = camera.headless(bb, W, H)
+        ty0, ty1, _, rows = fb.band_rows(world)[rank]
+        f = O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
+        band = O.render(g, f, nthreads=2)["bgr"]
+        assert band.shape[0] == rows
+        padded = torch.from_numpy(gdist.pad_band(band, fb, world).reshape(-1))
+        out = torch.empty(padded.numel() * world, dtype=torch.uint8)
+        dist.all_gather_into_tensor(out, padded)
+        frame = gdist.assemble(out.numpy(), fb, world)
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            full = O.render(g, O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0), nthreads=2)["bgr"]
+            q.put((np.array_equal(frame, full), float(t.item()), frame.shape))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_band_allgather_equals_single_frame(built, world):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    same, tmax, shape = q.get(timeout=10)
+    assert same
+    assert tmax == float(world)
+    assert shape == (360, 640, 3)

@@ -213,6 +213,23 @@ def test_blend_culling_is_decision_preserving(built, tw, th):
     _assert_parity(s, f, a)
 
 
+def test_gpu_against_committed_golden(built):
+    """The HIP path against the committed fixtures (tests/golden/oracle_golden.npz,
+    tools/make_golden.py): frame digests, histogram, list offsets and digests,
+    an RGBA crop and the first 256 projection records, bit for bit."""
+    from tools_golden import CASES, GOLDEN_PATH, gpu_case
+
+    gold = np.load(GOLDEN_PATH, allow_pickle=False)
+    for name in CASES:
+        got = gpu_case(name)
+        for key, val in got.items():
+            want = gold[f"{name}/{key}"]
+            if val.dtype == np.float32:
+                assert_same_bits(val, want, f"{name}/{key}")
+            else:
+                np.testing.assert_array_equal(val, want, err_msg=f"{name}/{key}")
+
+
 def test_overflow_grows_capacity(pc12):
     from gaussian_splat_ipu_amd import camera
 

@@ -1,0 +1,168 @@
+"""Host-side data path (CPU): PLY/XYZ ingest, scene preparation, synthetic
+scenes, camera -- the callers and data formats either side of the frame path
+(SURVEY §8 f1/f2)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import PC12
+
+REF_DATA = "/root/reference/data"
+
+
+def test_pc12_loads_like_happly(built):
+    """Values verified with the reference's vendored happly.h (SURVEY §8 c):
+    n = 37941, x[0] = 1.89972973, opacity[0] = 7.54005623."""
+    from gaussian_splat_ipu_amd import scene
+
+    ply = scene.load_ply(PC12)
+    assert len(ply) == 37941
+    assert ply["x"][0] == np.float32(1.89972973)
+    assert ply["opacity"][0] == np.float32(7.54005623)
+    for k in ["x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2", "opacity", "scale_0", "scale_1",
+              "scale_2", "rot_0", "rot_1", "rot_2", "rot_3"]:
+        assert ply.has(k), k
+    assert not ply.has("f_rest_0")  # SH degree 0 only (verified in the survey)
+
+
+def test_raw_bytes_of_pc12(built):
+    """The loader returns the file's float32 values bit for bit."""
+    from gaussian_splat_ipu_amd import scene
+
+    raw = open(PC12, "rb").read()
+    body = raw[raw.index(b"end_header\n") + len(b"end_header\n"):]
+    a = np.frombuffer(body, np.float32).reshape(37941, 17)
+    ply = scene.load_ply(PC12)
+    names = ["x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2", "opacity", "scale_0", "scale_1",
+             "scale_2", "rot_0", "rot_1", "rot_2", "rot_3"]
+    for j, k in enumerate(names):
+        np.testing.assert_array_equal(ply[k].view(np.uint32), a[:, j].view(np.uint32))
+
+
+def test_missing_required_property_is_an_error(built, tmp_path):
+    from gaussian_splat_ipu_amd import GsError, scene
+
+    p = tmp_path / "bad.ply"
+    p.write_bytes(b"ply\nformat ascii 1.0\nelement vertex 1\nproperty float x\nproperty float y\n"
+                  b"property float z\nend_header\n1 2 3\n")
+    with pytest.raises(GsError, match="missing required vertex property"):
+        scene.load_ply(str(p))
+    with pytest.raises(GsError, match="Unsupported file extension"):
+        scene.load_ply(str(tmp_path / "x.obj"))
+
+
+def test_ascii_big_endian_and_round_trip(built, tmp_path):
+    from gaussian_splat_ipu_amd import scene
+
+    ply = scene.synthetic(scene.SynthSpec(n=50, seed=9, sh_degree=3))
+    out = tmp_path / "s.ply"
+    ply.save(str(out))
+    back = scene.load_ply(str(out))
+    for k in ["x", "f_dc_2", "f_rest_44", "rot_3", "opacity"]:
+        np.testing.assert_array_equal(back[k], ply[k])
+    # ascii and big-endian versions of the same vertices
+    names = ["x", "y", "z", "f_dc_0", "f_dc_1", "f_dc_2", "opacity", "scale_0", "scale_1", "scale_2",
+             "rot_0", "rot_1", "rot_2", "rot_3"]
+    cols = np.stack([ply[k] for k in names], 1)
+    hdr = "".join(f"property float {k}\n" for k in names)
+    asc = tmp_path / "a.ply"
+    with open(asc, "w") as fh:
+        fh.write(f"ply\nformat ascii 1.0\nelement vertex 50\n{hdr}element face 0\n"
+                 "property list uchar int vertex_indices\nend_header\n")
+        for r in cols:
+            fh.write(" ".join(repr(float(v)) for v in r) + "\n")
+    be = tmp_path / "b.ply"
+    with open(be, "wb") as fh:
+        fh.write(f"ply\nformat binary_big_endian 1.0\nelement vertex 50\n{hdr}end_header\n".encode())
+        fh.write(cols.astype(">f4").tobytes())
+    for path in (asc, be):
+        q = scene.load_ply(str(path))
+        for j, k in enumerate(names):
+            np.testing.assert_array_equal(q[k], cols[:, j])
+
+
+def test_xyz_loader(built, tmp_path):
+    from gaussian_splat_ipu_amd import scene
+
+    p = tmp_path / "pts.XYZ"
+    p.write_text("1 2 3\n4.5 5.5 6.5\n\n7 8 9\n")
+    ply = scene.load_ply(str(p))
+    assert len(ply) == 3
+    np.testing.assert_array_equal(ply["z"], np.float32([3, 6.5, 9]))
+    g, bb = scene.prepare_scene(ply)
+    # splat.cpp:157-160 defaults for point clouds without 3DGS properties
+    np.testing.assert_array_equal(g["colour"][0], np.float32([0.05, 0.05, 0.05, 1.0]))
+    np.testing.assert_array_equal(g["scale"][0], np.float32([1, 1, 1]))
+
+
+def test_scene_preparation(built):
+    """splat.cpp:83-163: centre the bbox, negate z, SH-DC colour clamped at 0,
+    raw opacity/scale/rotation, gid = i + 1."""
+    from gaussian_splat_ipu_amd import scene
+
+    ply = scene.load_ply(PC12)
+    g, bb = scene.prepare_scene(ply)
+    x, y, z = ply["x"], ply["y"], ply["z"]
+    cx = np.float32((x.max() + x.min()) * np.float32(0.5))
+    cz = np.float32((z.max() + z.min()) * np.float32(0.5))
+    np.testing.assert_array_equal(g["mean"][:, 0], x - cx)
+    np.testing.assert_array_equal(g["mean"][:, 2], -(z - cz))
+    assert (g["mean"][:, 3] == 1).all()
+    c = np.float32(0.28209479177387814) * ply["f_dc_1"] + np.float32(0.5)
+    np.testing.assert_array_equal(g["colour"][:, 1], np.where(c < 0, np.float32(0), c))
+    np.testing.assert_array_equal(g["colour"][:, 3], ply["opacity"])
+    np.testing.assert_array_equal(g["scale"][:, 2], ply["scale_2"])
+    np.testing.assert_array_equal(g["rot"][:, 0], ply["rot_0"])
+    np.testing.assert_array_equal(g["gid"], np.arange(1, 37942, dtype=np.float32))
+    np.testing.assert_allclose(bb[:3], -bb[3:], rtol=0, atol=1e-6)
+
+
+def test_synthetic_is_seeded(built):
+    from gaussian_splat_ipu_amd import scene
+
+    a = scene.synthetic(scene.SynthSpec(n=1000, seed=5, sh_degree=3))
+    b = scene.synthetic(scene.SynthSpec(n=1000, seed=5, sh_degree=3))
+    c = scene.synthetic(scene.SynthSpec(n=1000, seed=6, sh_degree=3))
+    for k in ["x", "scale_1", "rot_2", "opacity", "f_rest_17"]:
+        np.testing.assert_array_equal(a[k], b[k])
+    assert not np.array_equal(a["x"], c["x"])
+    op = a["opacity"]
+    assert op.min() >= 0.5 and op.max() <= 8.0
+    assert a["x"].min() >= -4.36 and a["x"].max() <= 4.36
+    cl = np.zeros((2, 3), np.float32)
+    cl[1] = 10
+    d = scene.synthetic(scene.SynthSpec(n=2000, seed=8, sh_degree=0, cluster_xyz=cl, cluster_sigma=0.02))
+    xs = d["x"]
+    assert ((np.abs(xs) < 0.2) | (np.abs(xs - 10) < 0.2)).all()
+
+
+def test_headless_camera(built, pc12_scene):
+    """splat.cpp:186-199,235-244: view = mvpStart; projection =
+    fitFrustumToBoundingBox(eye-space bbox, 40 deg, aspect); row-major wire."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = pc12_scene
+    view, proj = camera.headless(bb, 1280, 720)
+    np.testing.assert_array_equal(view, camera.to_wire(camera.mvp_start()))
+    P = np.asarray(proj).reshape(4, 4)  # row-major
+    assert P[3, 2] == -1.0 and P[2, 3] < 0 and P[0, 1] == 0
+    # aspect: P00 / P11 = 1 / aspect
+    np.testing.assert_allclose(P[1, 1] / P[0, 0], 1280 / 720, rtol=1e-6)
+    # near plane = r / tan(fov): the frustum's f and n recovered from P
+    A, B = P[2, 2], P[2, 3]
+    n, f = B / (A - 1), B / (A + 1)
+    r = 0.5 * np.linalg.norm(bb[3:] - bb[:3])
+    np.testing.assert_allclose(n, r / np.tan(camera.FOV_DEFAULT), rtol=1e-5)
+    np.testing.assert_allclose(f - n, 20 * r, rtol=1e-5)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DATA), reason="reference data not mounted")
+@pytest.mark.parametrize("name", ["point_cloud_9.ply", "point_cloud_10.ply", "point_cloud_11.ply", "point_cloud_12.ply"])
+def test_reference_data_files_load(built, name):
+    from gaussian_splat_ipu_amd import scene
+
+    ply = scene.load_ply(os.path.join(REF_DATA, name))
+    assert len(ply) in (44087, 25161, 33073, 37941)
+    g, _ = scene.prepare_scene(ply)
+    assert np.isfinite(g["mean"]).all()
