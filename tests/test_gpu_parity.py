@@ -277,3 +277,36 @@ def test_orbit_frames(pc12):
         f = O.make_frame(view, proj, 1280, 720, 16, 16, camera.FOV_DEFAULT, 1.0)
         ref = O.render(g, f)
         assert_same_bits(s.get_rgba(), ref["rgba"], f"orbit frame {k}")
+
+
+def test_render_server_cli(built, tmp_path):
+    """The headless render server on the C ABI: same flow and
+    log line as splat.cpp; its test.png equals the renderer's BGR8 frame."""
+    import os
+    import struct
+    import subprocess
+    import zlib
+
+    from conftest import ROOT
+
+    exe = os.path.join(ROOT, "gaussian_splat_ipu_amd", "bin", "splat")
+    out = tmp_path / "test.png"
+    r = subprocess.run([exe, "--input", PC12, "--device", "gpu", "--out", str(out), "--frames", "2"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Splat time:" in r.stdout and "points/sec:" in r.stdout
+    data = out.read_bytes()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    w, h = struct.unpack(">II", data[16:24])
+    assert (w, h) == (1280, 720)
+    idat = data[data.index(b"IDAT") + 4:data.index(b"IEND") - 8]
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + w * 3)[:, 1:].reshape(h, w, 3)
+    from gaussian_splat_ipu_amd import camera, scene
+    from oracle import oracle as O
+
+    g, bb = scene.prepare_scene(scene.load_ply(PC12))
+    view, proj = camera.headless(bb, 1280, 720)
+    ref = O.render(g, O.make_frame(view, proj, 1280, 720, 32, 20, camera.FOV_DEFAULT, 0.1))
+    np.testing.assert_array_equal(raw[:, :, ::-1], ref["bgr"])
+    bad = subprocess.run([exe, "--input", PC12, "--ui-port", "5000"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "remote UI" in bad.stderr
