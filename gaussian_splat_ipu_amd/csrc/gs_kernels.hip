@@ -59,10 +59,6 @@ __device__ __forceinline__ float gs_expf(float x) {
   return (x != x) ? x : res;
 }
 
-// blend variant: the argument is known <= 0 and not NaN-producing paths are
-// kept identical (same ops, same order) -- only the overflow branch is dead.
-__device__ __forceinline__ float gs_expf_nonpos(float x) { return gs_expf(x); }
-
 __device__ __forceinline__ float smax(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float smin(float a, float b) { return a < b ? a : b; }
 
@@ -159,8 +155,9 @@ __device__ __forceinline__ uint32_t pack_i16x2(double lo, double hi) {
 //   pcut: a lane with power < pcut has op * expf(power) < 1/255, i.e. the
 //         reference would `continue` (codelets.cpp:401-403);
 //   box:  integer pixel box (x0,x1 | y0,y1) outside of which every pixel has
-//         power < pcut (the ellipse { d^T Q d <= -2 pcut } of the conic Q,
-//         widened by 0.1% + 1 px, computed in fp64).
+//         power < pcut (the bounding box of the ellipse { d^T Q d <= -2 pcut }
+//         of the conic Q, half-widths widened by 0.1%, computed in fp64; pixel
+//         centres are the integer coordinates the blend evaluates).
 // Both only ever remove evaluations whose outcome is "skip", so the blended
 // result is bit-identical to evaluating every list entry.
 __device__ __forceinline__ void alpha_footprint(float mx, float my, float k0, float k1, float k2,
@@ -191,10 +188,14 @@ __device__ __forceinline__ void alpha_footprint(float mx, float my, float k0, fl
   // margin of pcut ("blend culling").
   if (a > 0.0 && c > 0.0 && det > 1e-3 * a * c) {
     const double R = -2.0 * pc;
-    const double ex = sqrt(R * c / det) * 1.001 + 1.0;
-    const double ey = sqrt(R * a / det) * 1.001 + 1.0;
-    box_x = pack_i16x2(floor((double)mx - ex), ceil((double)mx + ex));
-    box_y = pack_i16x2(floor((double)my - ey), ceil((double)my + ey));
+    // The integer pixels within the widened half-widths: a pixel outside has
+    // |d| beyond 1.001x the ellipse's extent, so d^T Q d > 1.002 R exactly and
+    // the fp32 power (relative error < 7.2e-4) is < 1.0012 pc < pcut.  The
+    // 1e-6 absorbs the fp64 rounding of mx -/+ ex for vanishing ellipses.
+    const double ex = sqrt(R * c / det) * 1.001 + 1e-6;
+    const double ey = sqrt(R * a / det) * 1.001 + 1e-6;
+    box_x = pack_i16x2(ceil((double)mx - ex), floor((double)mx + ex));
+    box_y = pack_i16x2(ceil((double)my - ey), floor((double)my + ey));
   }
 }
 
@@ -889,9 +890,90 @@ __device__ __forceinline__ uint8_t to_u8(float v) {
   return (uint8_t)r;
 }
 
-// One wave = 64 consecutive pixels (tile-local index x + y*tw) of one tile;
-// the wave walks the tile's depth-sorted list with wave-uniform (SMEM) loads
-// of the index and the 48-B record and stops when all its pixels saturate.
+// Per-pixel blend state: position, transmittance, accumulated colour, and
+// whether the pixel has saturated (the reference's `break`).
+struct Px {
+  float fx, fy, T, C0, C1, C2, C3;
+  bool done;
+};
+
+__device__ __forceinline__ float gs_expf_inrange(float x) {
+  // gs_expf for x in [-80, 0]: the same ops minus the clamps / selects, which
+  // are no-ops there.  Outside that range the result is unused (selected away).
+  const float k = __builtin_rintf(x * 1.44269502162933349609f);
+  float r = __builtin_fmaf(k, -0.693145751953125f, x);
+  r = __builtin_fmaf(k, -1.428606765330187045e-06f, r);
+  float p = 1.9875691500e-4f;
+  p = __builtin_fmaf(p, r, 1.3981999507e-3f);
+  p = __builtin_fmaf(p, r, 8.3334519073e-3f);
+  p = __builtin_fmaf(p, r, 4.1665795894e-2f);
+  p = __builtin_fmaf(p, r, 1.6666665459e-1f);
+  p = __builtin_fmaf(p, r, 5.0000001201e-1f);
+  const float r2 = r * r;
+  p = __builtin_fmaf(p, r2, r);
+  p = p + 1.0f;
+  return p * __uint_as_float((uint32_t)((int)k + 127) << 23);
+}
+
+// One pixel's front-to-back step for one record (renderTile inner loop,
+// codelets.cpp:385-411), branch-free: every quantity is computed and the
+// state update is selected, so the pixels of a lane form independent chains.
+// FAST: the record's pcut >= -80, so any power the update accepts lies in
+// [-80, 0] where gs_expf_inrange == gs_expf bit for bit.
+template <bool FAST>
+__device__ __forceinline__ void blend_step(Px& q, float mx, float my, float k0, float k1, float k2,
+                                           float k3, float cr, float cg, float cb, float pcut) {
+  const float dx = mx - q.fx;
+  const float dy = my - q.fy;
+  const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
+  const float e = FAST ? gs_expf_inrange(power) : gs_expf(power);
+  const float v = k3 * e;
+  const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
+  const float test_T = q.T * (1.0f - alpha);
+  // power > 0: skipped; power < pcut: alpha < 1/255 guaranteed (`continue`)
+  const bool hit = !q.done && !(power > 0.0f) && !(power < pcut) && !(alpha < 1.0f / 255.0f);
+  const bool brk = hit && test_T < 0.0001f;  // break (codelets.cpp:406-408)
+  const bool upd = hit && !brk;
+  q.C0 = upd ? q.C0 + (cr * alpha) * q.T : q.C0;  // colour += gCont * alpha * T
+  q.C1 = upd ? q.C1 + (cg * alpha) * q.T : q.C1;
+  q.C2 = upd ? q.C2 + (cb * alpha) * q.T : q.C2;
+  q.C3 = upd ? q.C3 + (k3 * alpha) * q.T : q.C3;
+  q.T = upd ? test_T : q.T;
+  q.done = q.done || brk;
+}
+
+__device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers& b, int px, int py,
+                                            const Px& q) {
+  const int row = py - fp.band_py0;
+  const float o0 = 0.0f + q.C0, o1 = 0.0f + q.C1, o2 = 0.0f + q.C2, o3 = 0.0f + q.C3;
+  if (fp.write_rgba) b.rgba[(size_t)row * fp.width + px] = make_float4(o0, o1, o2, o3);
+  uint8_t* dst = b.bgr + (size_t)row * fp.bgr_pitch + 3 * (size_t)px;
+  dst[0] = to_u8(o2);  // RGBA2BGR
+  dst[1] = to_u8(o1);
+  dst[2] = to_u8(o0);
+}
+
+// all four lanes of this lane's quad (lanes 4q..4q+3) have p
+__device__ __forceinline__ bool quad_all(bool p) {
+  int v = p ? 1 : 0;
+  v &= __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  v &= __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  return v != 0;
+}
+
+// One wave = 16 pixel quads (2x2) of one tile, one lane per pixel: an 8x8
+// block when the tile is a multiple of 8 x 8, else 16 consecutive quads in
+// quad-row-major order.  Every quad keeps its own record queue.  The wave
+// walks the tile's depth-sorted list in batches of 64: one coalesced load of
+// the indices, one gather of the records into wave-private LDS, and a
+// lane-parallel footprint test of each record against each quad's 2x2 box
+// (16 ballots).  Each quad then evaluates only the records whose footprint
+// touches it, in list order, reading the next record from LDS while the
+// current one is blended; a quad stops when its four pixels have saturated
+// and the wave when all quads have.  The per-pixel arithmetic and record
+// order are those of renderTile (codelets.cpp:385-411): a record is skipped
+// for a quad only when no pixel of the quad can take it (DESIGN.md,
+// "blend culling").
 __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wid = blockIdx.x * 4 + wave;
@@ -899,40 +981,45 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   const int chunk = wid - tile * fp.chunks_per_tile;
   if (tile >= fp.n_tiles) return;
   const int lane = threadIdx.x & 63;
+  const int myq = lane >> 2;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
   const int tile_x0 = tx * fp.tile_w;
   const int tile_y0 = (fp.band_ty0 + tyb) * fp.tile_h;
-  // pixel footprint of this wave: an 8x8 block when the tile is a multiple of
-  // 8 in both directions, else 64 consecutive tile-local pixels (x + y*tw)
-  int lx, ly, bx0, bx1, by0, by1;
-  bool in_tile;
+
+  // quad walk (wave-uniform): the wave's first quad, the row wrap, the count
+  int q_x, q_y, wrap_x0, wrap_x1, nq_wave;
+  const int qw = (fp.tile_w + 1) >> 1;
   if (fp.block8) {
     const int bpr = fp.tile_w >> 3;
-    const int cbx = (chunk % bpr) << 3, cby = (chunk / bpr) << 3;
-    lx = cbx + (lane & 7);
-    ly = cby + (lane >> 3);
-    in_tile = true;
-    bx0 = tile_x0 + cbx;
-    bx1 = bx0 + 7;
-    by0 = tile_y0 + cby;
-    by1 = by0 + 7;
+    q_x = (chunk % bpr) << 3;
+    q_y = (chunk / bpr) << 3;
+    wrap_x0 = q_x;
+    wrap_x1 = q_x + 8;
+    nq_wave = 16;
   } else {
-    const int np = fp.tile_w * fp.tile_h;
-    const int lp = chunk * 64 + lane;
-    lx = lp % fp.tile_w;
-    ly = lp / fp.tile_w;
-    in_tile = lp < np;
-    const int lp0 = chunk * 64, lp1 = min(lp0 + 63, np - 1);
-    const int r0 = lp0 / fp.tile_w, r1 = lp1 / fp.tile_w;
-    by0 = tile_y0 + r0;
-    by1 = tile_y0 + r1;
-    bx0 = tile_x0 + (r0 == r1 ? lp0 % fp.tile_w : 0);
-    bx1 = tile_x0 + (r0 == r1 ? lp1 % fp.tile_w : fp.tile_w - 1);
+    const int nq = qw * ((fp.tile_h + 1) >> 1);
+    const int qi0 = chunk * 16;
+    q_x = (qi0 % qw) << 1;
+    q_y = (qi0 / qw) << 1;
+    wrap_x0 = 0;
+    wrap_x1 = qw << 1;
+    nq_wave = min(16, nq - qi0);
   }
-  const int px = tile_x0 + lx;
-  const int py = tile_y0 + ly;
-  const bool valid = in_tile && px < fp.width && py < fp.height;
-  const float pfx = (float)px, pfy = (float)py;
+  // this lane's pixel
+  int lqx, lqy;
+  if (fp.block8) {
+    lqx = wrap_x0 + ((myq & 3) << 1);
+    lqy = q_y + ((myq >> 2) << 1);
+  } else {
+    const int qi = chunk * 16 + myq;
+    lqx = (qi % qw) << 1;
+    lqy = (qi / qw) << 1;
+  }
+  const int lx = lqx + (lane & 1), ly = lqy + ((lane >> 1) & 1);
+  const int px = tile_x0 + lx, py = tile_y0 + ly;
+  const bool valid = myq < nq_wave && lx < fp.tile_w && ly < fp.tile_h && px < fp.width &&
+                     py < fp.height;
+  Px q{(float)px, (float)py, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f, !valid};
 
   uint32_t s, L;
   tile_segment(fp, b, tile, s, L);
@@ -942,75 +1029,71 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   __shared__ float4 s_rec[4][3][64];
   float4(*const st)[64] = s_rec[wave];
 
-  float T = 1.0f;
-  float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
-  bool done = !valid;
   for (uint32_t base = 0; base < L; base += 64) {
-    if (__ballot(!done) == 0ull) break;
-    // one coalesced load of 64 list entries + one gather of their records;
-    // the footprint test runs lane-parallel and leaves a mask of the entries
-    // that can change a pixel of this wave (the others all `continue`)
+    if (__ballot(!q.done) == 0ull) break;
     const uint32_t k = base + lane;
-    bool rel = false;
+    bool rok = false;
+    int rx0 = 0, rx1 = -1, ry0 = 0, ry1 = -1;
     if (k < L) {
       const uint32_t g = list[k];
       if (g < (uint32_t)fp.n) {  // defensive: never read past the records
-        const float4* q = b.rec + 4 * (size_t)g;
-        const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+        const float4* qq = b.rec + 4 * (size_t)g;
+        const float4 q0 = qq[0], q1 = qq[1], q2 = qq[2];
         const uint32_t boxx = __float_as_uint(q2.z), boxy = __float_as_uint(q2.w);
-        rel = !(q1.y == 0.0f) &&  // con_o.w == 0 (codelets.cpp:389)
-              !((int)(boxx << 16) >> 16 > bx1 || (int)boxx >> 16 < bx0 ||
-                (int)(boxy << 16) >> 16 > by1 || (int)boxy >> 16 < by0);
+        rx0 = (int)(boxx << 16) >> 16;
+        rx1 = (int)boxx >> 16;
+        ry0 = (int)(boxy << 16) >> 16;
+        ry1 = (int)boxy >> 16;
+        rok = !(q1.y == 0.0f);  // con_o.w == 0 (codelets.cpp:389)
         st[0][lane] = q0;
         st[1][lane] = q1;
         st[2][lane] = q2;
       }
     }
-    unsigned long long mask = __ballot(rel);
-    // the lanes' LDS stores precede the broadcast reads below (same wave)
+    // footprint x quad: 16 ballots, lane keeps its quad's mask
+    unsigned long long m = 0ull;
+    {
+      int cx = q_x, cy = q_y;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int X0 = tile_x0 + cx, Y0 = tile_y0 + cy;
+        const bool hit = rok && t < nq_wave && !(rx0 > X0 + 1 || rx1 < X0 || ry0 > Y0 + 1 || ry1 < Y0);
+        const unsigned long long bt = __ballot(hit);
+        m = (myq == t) ? bt : m;
+        cx += 2;
+        if (cx >= wrap_x1) {
+          cx = wrap_x0;
+          cy += 2;
+        }
+      }
+    }
+    // the lanes' LDS stores precede the reads below (same wave)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    while (mask) {
-      const int j = __builtin_ctzll(mask);  // list order: ascending bits
-      mask &= mask - 1ull;
-      const float4 q0 = st[0][j], q1 = st[1][j], q2 = st[2][j];
-      const float mx = q0.x, my = q0.y, k0 = q0.z, k1 = q0.w;
-      const float k2 = q1.x, k3 = q1.y, cr = q1.z, cg = q1.w;
-      const float cb = q2.x, pcut = q2.y;
-      if (!done) {
-        const float dx = mx - pfx;
-        const float dy = my - pfy;
-        const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
-        // power < pcut: alpha < 1/255 guaranteed (the reference's `continue`)
-        if (!(power > 0.0f) && !(power < pcut)) {
-          const float v = k3 * gs_expf_nonpos(power);
-          const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
-          if (!(alpha < 1.0f / 255.0f)) {
-            const float test_T = T * (1.0f - alpha);
-            if (test_T < 0.0001f) {
-              done = true;  // break (codelets.cpp:406-408)
-            } else {
-              C0 = C0 + (cr * alpha) * T;  // colour += gCont * alpha * T
-              C1 = C1 + (cg * alpha) * T;
-              C2 = C2 + (cb * alpha) * T;
-              C3 = C3 + (k3 * alpha) * T;
-              T = test_T;
-            }
-          }
-        }
+    if (quad_all(q.done)) m = 0ull;
+    if (m) {
+      int j = __builtin_ctzll(m);  // list order: ascending bits
+      float4 r0 = st[0][j], r1 = st[1][j], r2 = st[2][j];
+      for (;;) {
+        m &= m - 1ull;
+        const int jn = m ? __builtin_ctzll(m) : j;
+        // next record's read in flight during this record's math
+        const float4 n0 = st[0][jn], n1 = st[1][jn], n2 = st[2][jn];
+        const float pcut = r2.y;
+        if (pcut >= -80.0f)
+          blend_step<true>(q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, pcut);
+        else
+          blend_step<false>(q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, pcut);
+        if (quad_all(q.done)) m = 0ull;
+        if (!m) break;
+        r0 = n0;
+        r1 = n1;
+        r2 = n2;
       }
-      if (__ballot(!done) == 0ull) break;
     }
   }
-  if (!valid) return;
-  const int row = py - fp.band_py0;
-  const float o0 = 0.0f + C0, o1 = 0.0f + C1, o2 = 0.0f + C2, o3 = 0.0f + C3;
-  if (fp.write_rgba) b.rgba[(size_t)row * fp.width + px] = make_float4(o0, o1, o2, o3);
-  uint8_t* dst = b.bgr + (size_t)row * fp.bgr_pitch + 3 * (size_t)px;
-  dst[0] = to_u8(o2);  // RGBA2BGR
-  dst[1] = to_u8(o1);
-  dst[2] = to_u8(o0);
+  if (valid) store_pixel(fp, b, px, py, q);
 }
 
 }  // namespace

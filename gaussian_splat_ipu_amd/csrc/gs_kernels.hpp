@@ -26,8 +26,8 @@ struct FrameParams {
   int band_rows;      // pixel rows of this band (<= (ty1-ty0)*th)
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
-  int chunks_per_tile;  // ceil(tw*th / 64): one wave per 64-pixel chunk
-  int block8;           // tw % 8 == 0 && th % 8 == 0: waves own 8x8 pixel blocks
+  int chunks_per_tile;  // blend waves per tile (16 pixel quads each)
+  int block8;           // tw % 8 == 0 && th % 8 == 0: blend waves own 8x8 blocks
   unsigned long long pair_cap;
   int write_rgba;
   int bgr_pitch;      // bytes per row of the BGR8 output

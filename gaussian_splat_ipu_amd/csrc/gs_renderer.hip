@@ -162,8 +162,12 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.band_rows = r->band_rows;
   fp.n = (int)r->n;
   fp.n_tiles = r->n_tiles;
-  fp.chunks_per_tile = (int)((r->cfg.tile_width * r->cfg.tile_height + 63) / 64);
-  fp.block8 = (r->cfg.tile_width % 8 == 0 && r->cfg.tile_height % 8 == 0) ? 1 : 0;
+  // blend: one wave per 16 pixel quads, an 8 x 8 block when the tile is a
+  // multiple of it
+  const uint32_t tw = r->cfg.tile_width, th = r->cfg.tile_height;
+  fp.block8 = (tw % 8 == 0 && th % 8 == 0) ? 1 : 0;
+  fp.chunks_per_tile = fp.block8 ? (int)((tw / 8) * (th / 8))
+                                 : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
