@@ -279,9 +279,9 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     float pcut;
     uint32_t b01, b23;
     alpha_footprint(vx, vy, k0, k1, k2, k3, fp, pcut, b01, b23);
-    rec[0] = make_float4(vx, vy, k0, k1);
-    rec[1] = make_float4(k2, k3, col.x, col.y);
-    rec[2] = make_float4(col.z, pcut, __uint_as_float(b01), __uint_as_float(b23));
+    rec[0] = make_float4(vx, vy, k0, k2);
+    rec[1] = make_float4(k1, pcut, col.x, col.y);
+    rec[2] = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
     rec[3] = make_float4(radius, cz, 0.0f, 0.0f);
     if (within && cz < 0.0f) {  // codelets.cpp:493
       rendered = true;
@@ -309,8 +309,8 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     }
   } else {
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    rec[1] = make_float4(0.0f, 0.0f, col.x, col.y);
-    rec[2] = make_float4(col.z, __builtin_huge_valf(), __uint_as_float(kEmptyBox),
+    rec[1] = make_float4(0.0f, __builtin_huge_valf(), col.x, col.y);
+    rec[2] = make_float4(col.z, 0.0f, __uint_as_float(kEmptyBox),
                          __uint_as_float(kEmptyBox));
     rec[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
@@ -890,10 +890,14 @@ __device__ __forceinline__ uint8_t to_u8(float v) {
   return (uint8_t)r;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // Per-pixel blend state: position, transmittance, accumulated colour, and
 // whether the pixel has saturated (the reference's `break`).
 struct Px {
-  float fx, fy, T, C0, C1, C2, C3;
+  f32x2 p;         // pixel centre (x, y)
+  float T;
+  f32x2 c01, c23;  // colour accumulators (r, g), (b, a)
   bool done;
 };
 
@@ -915,29 +919,38 @@ __device__ __forceinline__ float gs_expf_inrange(float x) {
   return p * __uint_as_float((uint32_t)((int)k + 127) << 23);
 }
 
+// One staged record (48 B, see the project kernel):
+//   r0 = (mx, my, k0, k2)   r1 = (k1, pcut, r, g)   r2 = (b, opacity, box_x, box_y)
 // One pixel's front-to-back step for one record (renderTile inner loop,
 // codelets.cpp:385-411), branch-free: every quantity is computed and the
-// state update is selected, so the pixels of a lane form independent chains.
-// FAST: the record's pcut >= -80, so any power the update accepts lies in
-// [-80, 0] where gs_expf_inrange == gs_expf bit for bit.
+// state update is selected.  The pairs (dx, dy), (k0 dx, k2 dy), (r, g) and
+// (b, opacity) are computed as packed fp32 (each half is the same IEEE
+// operation as the scalar expression).  FAST: the record's pcut >= -80, so
+// any power the update accepts lies in [-80, 0], where gs_expf_inrange ==
+// gs_expf bit for bit.
 template <bool FAST>
-__device__ __forceinline__ void blend_step(Px& q, float mx, float my, float k0, float k1, float k2,
-                                           float k3, float cr, float cg, float cb, float pcut) {
-  const float dx = mx - q.fx;
-  const float dy = my - q.fy;
-  const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
+__device__ __forceinline__ void blend_step(Px& q, const float4& r0, const float4& r1,
+                                           const float4& r2) {
+  const f32x2 m = {r0.x, r0.y}, kd = {r0.z, r0.w};
+  const float k1 = r1.x, pcut = r1.y, op = r2.y;
+  const f32x2 d = m - q.p;          // (mx - px, my - py)
+  const f32x2 kdd = (kd * d) * d;   // (k0 * dx * dx, k2 * dy * dy)
+  const float power = -0.5f * (kdd.x + kdd.y) - k1 * d.x * d.y;
   const float e = FAST ? gs_expf_inrange(power) : gs_expf(power);
-  const float v = k3 * e;
+  const float v = op * e;
   const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
   const float test_T = q.T * (1.0f - alpha);
   // power > 0: skipped; power < pcut: alpha < 1/255 guaranteed (`continue`)
   const bool hit = !q.done && !(power > 0.0f) && !(power < pcut) && !(alpha < 1.0f / 255.0f);
   const bool brk = hit && test_T < 0.0001f;  // break (codelets.cpp:406-408)
   const bool upd = hit && !brk;
-  q.C0 = upd ? q.C0 + (cr * alpha) * q.T : q.C0;  // colour += gCont * alpha * T
-  q.C1 = upd ? q.C1 + (cg * alpha) * q.T : q.C1;
-  q.C2 = upd ? q.C2 + (cb * alpha) * q.T : q.C2;
-  q.C3 = upd ? q.C3 + (k3 * alpha) * q.T : q.C3;
+  const f32x2 crg = {r1.z, r1.w}, cbo = {r2.x, op};
+  const f32x2 n01 = q.c01 + (crg * alpha) * q.T;  // colour += gCont * alpha * T
+  const f32x2 n23 = q.c23 + (cbo * alpha) * q.T;
+  q.c01.x = upd ? n01.x : q.c01.x;
+  q.c01.y = upd ? n01.y : q.c01.y;
+  q.c23.x = upd ? n23.x : q.c23.x;
+  q.c23.y = upd ? n23.y : q.c23.y;
   q.T = upd ? test_T : q.T;
   q.done = q.done || brk;
 }
@@ -945,7 +958,7 @@ __device__ __forceinline__ void blend_step(Px& q, float mx, float my, float k0, 
 __device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers& b, int px, int py,
                                             const Px& q) {
   const int row = py - fp.band_py0;
-  const float o0 = 0.0f + q.C0, o1 = 0.0f + q.C1, o2 = 0.0f + q.C2, o3 = 0.0f + q.C3;
+  const float o0 = 0.0f + q.c01.x, o1 = 0.0f + q.c01.y, o2 = 0.0f + q.c23.x, o3 = 0.0f + q.c23.y;
   if (fp.write_rgba) b.rgba[(size_t)row * fp.width + px] = make_float4(o0, o1, o2, o3);
   uint8_t* dst = b.bgr + (size_t)row * fp.bgr_pitch + 3 * (size_t)px;
   dst[0] = to_u8(o2);  // RGBA2BGR
@@ -961,19 +974,20 @@ __device__ __forceinline__ bool quad_all(bool p) {
   return v != 0;
 }
 
-// One wave = 16 pixel quads (2x2) of one tile, one lane per pixel: an 8x8
-// block when the tile is a multiple of 8 x 8, else 16 consecutive quads in
-// quad-row-major order.  Every quad keeps its own record queue.  The wave
-// walks the tile's depth-sorted list in batches of 64: one coalesced load of
-// the indices, one gather of the records into wave-private LDS, and a
-// lane-parallel footprint test of each record against each quad's 2x2 box
-// (16 ballots).  Each quad then evaluates only the records whose footprint
-// touches it, in list order, reading the next record from LDS while the
-// current one is blended; a quad stops when its four pixels have saturated
-// and the wave when all quads have.  The per-pixel arithmetic and record
-// order are those of renderTile (codelets.cpp:385-411): a record is skipped
-// for a quad only when no pixel of the quad can take it (DESIGN.md,
-// "blend culling").
+// One wave = 16 pixel quads (2x2) of one tile, one lane per pixel: a block of
+// bqw x (16 / bqw) quads (8x8 or 16x4 pixels) when the tile is a multiple of
+// it, else 16 consecutive quads in quad-row-major order.  Every quad keeps its
+// own record queue.  The wave walks the tile's depth-sorted list in batches
+// of 64 (the next batch's indices and records are loaded while this one is
+// blended): the records are staged in wave-private LDS and each record's
+// footprint box is turned into the set of quads it touches (16 ballots, one
+// 64-bit mask per quad).  Each quad then evaluates only its records, in list
+// order, reading the next record from LDS while the current one is blended;
+// a quad stops when its four pixels have saturated and the wave when all
+// quads have.  The per-pixel arithmetic and record order are those of
+// renderTile (codelets.cpp:385-411): a record is skipped for a quad only when
+// no pixel of the quad can take it ("blend culling").
+template <int BQW>
 __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wid = blockIdx.x * 4 + wave;
@@ -985,31 +999,28 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
   const int tile_x0 = tx * fp.tile_w;
   const int tile_y0 = (fp.band_ty0 + tyb) * fp.tile_h;
+  constexpr int bqw = BQW;  // 4 | 8: block of quads; 0: quad-row-major run
 
-  // quad walk (wave-uniform): the wave's first quad, the row wrap, the count
-  int q_x, q_y, wrap_x0, wrap_x1, nq_wave;
+  // the wave's first quad (tile-local pixel coordinates) and quad count
+  int q_x, q_y, nq_wave;
   const int qw = (fp.tile_w + 1) >> 1;
-  if (fp.block8) {
-    const int bpr = fp.tile_w >> 3;
-    q_x = (chunk % bpr) << 3;
-    q_y = (chunk / bpr) << 3;
-    wrap_x0 = q_x;
-    wrap_x1 = q_x + 8;
+  if (bqw) {
+    const int bpr = fp.tile_w / (2 * bqw);
+    q_x = (chunk % bpr) * (2 * bqw);
+    q_y = (chunk / bpr) * (32 / bqw);
     nq_wave = 16;
   } else {
     const int nq = qw * ((fp.tile_h + 1) >> 1);
     const int qi0 = chunk * 16;
     q_x = (qi0 % qw) << 1;
     q_y = (qi0 / qw) << 1;
-    wrap_x0 = 0;
-    wrap_x1 = qw << 1;
     nq_wave = min(16, nq - qi0);
   }
   // this lane's pixel
   int lqx, lqy;
-  if (fp.block8) {
-    lqx = wrap_x0 + ((myq & 3) << 1);
-    lqy = q_y + ((myq >> 2) << 1);
+  if (bqw) {
+    lqx = q_x + ((myq % bqw) << 1);
+    lqy = q_y + ((myq / bqw) << 1);
   } else {
     const int qi = chunk * 16 + myq;
     lqx = (qi % qw) << 1;
@@ -1019,7 +1030,12 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   const int px = tile_x0 + lx, py = tile_y0 + ly;
   const bool valid = myq < nq_wave && lx < fp.tile_w && ly < fp.tile_h && px < fp.width &&
                      py < fp.height;
-  Px q{(float)px, (float)py, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f, !valid};
+  Px q;
+  q.p = f32x2{(float)px, (float)py};
+  q.T = 1.0f;
+  q.c01 = f32x2{0.0f, 0.0f};
+  q.c23 = f32x2{0.0f, 0.0f};
+  q.done = !valid;
 
   uint32_t s, L;
   tile_segment(fp, b, tile, s, L);
@@ -1029,40 +1045,79 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   __shared__ float4 s_rec[4][3][64];
   float4(*const st)[64] = s_rec[wave];
 
+  // software pipeline: records of batch `base`, index of batch `base + 64`
+  auto load_idx = [&](uint32_t k) -> uint32_t {
+    uint32_t g = 0xFFFFFFFFu;
+    if (k < L) g = list[k];
+    return g < (uint32_t)fp.n ? g : 0xFFFFFFFFu;  // defensive: never read past the records
+  };
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
+  uint32_t g_cur = load_idx(lane);
+  if (g_cur != 0xFFFFFFFFu) {
+    const float4* qq = b.rec + 4 * (size_t)g_cur;
+    a0 = qq[0];
+    a1 = qq[1];
+    a2 = qq[2];
+  }
+  uint32_t g_next = load_idx(64 + lane);
+
   for (uint32_t base = 0; base < L; base += 64) {
     if (__ballot(!q.done) == 0ull) break;
-    const uint32_t k = base + lane;
-    bool rok = false;
-    int rx0 = 0, rx1 = -1, ry0 = 0, ry1 = -1;
-    if (k < L) {
-      const uint32_t g = list[k];
-      if (g < (uint32_t)fp.n) {  // defensive: never read past the records
-        const float4* qq = b.rec + 4 * (size_t)g;
-        const float4 q0 = qq[0], q1 = qq[1], q2 = qq[2];
-        const uint32_t boxx = __float_as_uint(q2.z), boxy = __float_as_uint(q2.w);
-        rx0 = (int)(boxx << 16) >> 16;
-        rx1 = (int)boxx >> 16;
-        ry0 = (int)(boxy << 16) >> 16;
-        ry1 = (int)boxy >> 16;
-        rok = !(q1.y == 0.0f);  // con_o.w == 0 (codelets.cpp:389)
-        st[0][lane] = q0;
-        st[1][lane] = q1;
-        st[2][lane] = q2;
-      }
+    // stage this batch
+    const bool have = g_cur != 0xFFFFFFFFu;
+    st[0][lane] = a0;
+    st[1][lane] = a1;
+    st[2][lane] = a2;
+    const uint32_t boxx = __float_as_uint(a2.z), boxy = __float_as_uint(a2.w);
+    const int rx0 = (int)(boxx << 16) >> 16, rx1 = (int)boxx >> 16;
+    const int ry0 = (int)(boxy << 16) >> 16, ry1 = (int)boxy >> 16;
+    const bool rok = have && !(a2.y == 0.0f) &&  // con_o.w == 0 (codelets.cpp:389)
+                     rx0 <= rx1 && ry0 <= ry1;
+    // prefetch the next batch
+    g_cur = g_next;
+    a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g_cur != 0xFFFFFFFFu) {
+      const float4* qq = b.rec + 4 * (size_t)g_cur;
+      a0 = qq[0];
+      a1 = qq[1];
+      a2 = qq[2];
     }
-    // footprint x quad: 16 ballots, lane keeps its quad's mask
+    g_next = load_idx(base + 128 + lane);
+
+    // m = the batch's records whose box touches this lane's quad (bit k =
+    // record k).  Blocks: per quad column / row one ballot, then each lane
+    // ANDs its column's and row's masks; quad runs: one ballot per quad.
     unsigned long long m = 0ull;
-    {
+    if constexpr (BQW != 0) {
+      const int bx = tile_x0 + q_x, by = tile_y0 + q_y;
+      const int c0 = (rx0 - bx) >> 1, c1 = (rx1 - bx) >> 1;  // quad columns / rows
+      const int w0 = (ry0 - by) >> 1, w1 = (ry1 - by) >> 1;
+      const int qx = myq % bqw, qy = myq / bqw;
+      unsigned long long mc = 0ull, mr = 0ull;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (c >= bqw) break;
+        const unsigned long long bc = __ballot(rok && c0 <= c && c <= c1);
+        mc = (qx == c) ? bc : mc;
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if (w >= 16 / bqw) break;
+        const unsigned long long br = __ballot(rok && w0 <= w && w <= w1);
+        mr = (qy == w) ? br : mr;
+      }
+      m = mc & mr;
+    } else {
       int cx = q_x, cy = q_y;
 #pragma unroll
       for (int t = 0; t < 16; ++t) {
         const int X0 = tile_x0 + cx, Y0 = tile_y0 + cy;
-        const bool hit = rok && t < nq_wave && !(rx0 > X0 + 1 || rx1 < X0 || ry0 > Y0 + 1 || ry1 < Y0);
-        const unsigned long long bt = __ballot(hit);
+        const bool h = rok && t < nq_wave && !(rx0 > X0 + 1 || rx1 < X0 || ry0 > Y0 + 1 || ry1 < Y0);
+        const unsigned long long bt = __ballot(h);
         m = (myq == t) ? bt : m;
         cx += 2;
-        if (cx >= wrap_x1) {
-          cx = wrap_x0;
+        if (cx >= (qw << 1)) {
+          cx = 0;
           cy += 2;
         }
       }
@@ -1080,11 +1135,10 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
         const int jn = m ? __builtin_ctzll(m) : j;
         // next record's read in flight during this record's math
         const float4 n0 = st[0][jn], n1 = st[1][jn], n2 = st[2][jn];
-        const float pcut = r2.y;
-        if (pcut >= -80.0f)
-          blend_step<true>(q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, pcut);
+        if (r1.y >= -80.0f)  // pcut
+          blend_step<true>(q, r0, r1, r2);
         else
-          blend_step<false>(q, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, pcut);
+          blend_step<false>(q, r0, r1, r2);
         if (quad_all(q.done)) m = 0ull;
         if (!m) break;
         r0 = n0;
@@ -1092,6 +1146,8 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
         r2 = n2;
       }
     }
+    // the next batch's LDS stores come after every lane's reads of this one
+    __builtin_amdgcn_wave_barrier();
   }
   if (valid) store_pixel(fp, b, px, py, q);
 }
@@ -1144,7 +1200,13 @@ void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
   if (waves == 0) return;
-  gs_blend_kernel<<<(unsigned)((waves + 3) / 4), 256, 0, s>>>(fp, b);
+  const unsigned grid = (unsigned)((waves + 3) / 4);
+  if (fp.blend_bqw == 4)
+    gs_blend_kernel<4><<<grid, 256, 0, s>>>(fp, b);
+  else if (fp.blend_bqw == 8)
+    gs_blend_kernel<8><<<grid, 256, 0, s>>>(fp, b);
+  else
+    gs_blend_kernel<0><<<grid, 256, 0, s>>>(fp, b);
 }
 
 }  // namespace gsk

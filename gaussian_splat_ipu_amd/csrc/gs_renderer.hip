@@ -162,12 +162,13 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.band_rows = r->band_rows;
   fp.n = (int)r->n;
   fp.n_tiles = r->n_tiles;
-  // blend: one wave per 16 pixel quads, an 8 x 8 block when the tile is a
-  // multiple of it
+  // blend: one wave per 16 pixel quads -- an 8x8 or 16x4 pixel block when the
+  // tile is a multiple of it, else a run of quads
   const uint32_t tw = r->cfg.tile_width, th = r->cfg.tile_height;
-  fp.block8 = (tw % 8 == 0 && th % 8 == 0) ? 1 : 0;
-  fp.chunks_per_tile = fp.block8 ? (int)((tw / 8) * (th / 8))
-                                 : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
+  fp.blend_bqw = (tw % 8 == 0 && th % 8 == 0) ? 4 : ((tw % 16 == 0 && th % 4 == 0) ? 8 : 0);
+  fp.chunks_per_tile = fp.blend_bqw == 4   ? (int)((tw / 8) * (th / 8))
+                       : fp.blend_bqw == 8 ? (int)((tw / 16) * (th / 4))
+                                           : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
@@ -622,10 +623,10 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     float* o = dst + i * 12;
     o[0] = q[0];  // mean2d
     o[1] = q[1];
-    o[2] = q[2];  // conic
-    o[3] = q[3];
-    o[4] = q[4];
-    o[5] = q[5];
+    o[2] = q[2];  // conic (k0, k1, k2, opacity)
+    o[3] = q[4];
+    o[4] = q[3];
+    o[5] = q[9];
     o[6] = q[13];  // clip z
     o[7] = q[12];  // radius
     const uint32_t rx = rect[i * 2], ry = rect[i * 2 + 1];
