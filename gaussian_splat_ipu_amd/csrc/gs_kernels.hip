@@ -344,6 +344,20 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
   __shared__ uint32_t wvis[16];
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // V = sum of the project workgroups' counts (loads issued up front)
+  uint32_t vsum = 0;
+  {
+    const int nb = (fp.n + 255) / 256;
+    uint32_t vr[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = tid + k * 1024;
+      vr[k] = i < nb ? b.block_rendered[i] : 0u;
+    }
+    for (int i = tid + 8 * 1024; i < nb; i += 1024) vsum += b.block_rendered[i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) vsum += vr[k];
+  }
   unsigned long long carry = 0;
   uint32_t med_base = 0, big_base = 0, mx = 0;
   for (int r0 = 0; r0 < T; r0 += 8192) {
@@ -408,10 +422,6 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-  // V = sum of the project workgroups' counts
-  uint32_t vsum = 0;
-  const int nb = (fp.n + 255) / 256;
-  for (int i = tid; i < nb; i += 1024) vsum += b.block_rendered[i];
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
   if (lane == 0) {
@@ -473,7 +483,8 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
   for (int t = threadIdx.x; t < T; t += 1024) row[t] = (cnt[t >> 1] >> ((t & 1) * 16)) & 0xFFFFu;
 }
 
-// 64 tiles per workgroup (one per lane), the chunk rows split over 16 waves.
+// 64 tiles per workgroup (one per lane), the chunk rows split over 16 waves
+// (n_chunks <= 256: at most 16 rows per wave, held in registers).
 __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffers b) {
   __shared__ uint32_t wsum[16][64];
   const int T = fp.n_tiles, NC = fp.n_chunks;
@@ -481,20 +492,22 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
   const int t = blockIdx.x * 64 + lane;
   const int rows = (NC + 15) / 16;
   const int c0 = wave * rows, c1 = min(NC, c0 + rows);
+  uint32_t v[16];
   uint32_t sum = 0;
-  if (t < T)
-    for (int c = c0; c < c1; ++c) sum += b.chunk_off[(size_t)c * T + t];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = (t < T && c0 + k < c1) ? b.chunk_off[(size_t)(c0 + k) * T + t] : 0u;
+    sum += v[k];
+  }
   wsum[wave][lane] = sum;
   __syncthreads();
-  uint32_t base = 0;
-  for (int w = 0; w < wave; ++w) base += wsum[w][lane];
+  uint32_t run = 0;
+  for (int w = 0; w < wave; ++w) run += wsum[w][lane];
   if (t < T) {
-    uint32_t run = base;
-    for (int c = c0; c < c1; ++c) {
-      uint32_t* p = b.chunk_off + (size_t)c * T + t;
-      const uint32_t v = *p;
-      *p = run;
-      run += v;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (c0 + k < c1) b.chunk_off[(size_t)(c0 + k) * T + t] = run;
+      run += v[k];
     }
     if (wave == 15) b.tile_count[t] = run;
   }
