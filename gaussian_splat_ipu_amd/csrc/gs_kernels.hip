@@ -935,35 +935,41 @@ __device__ __forceinline__ float gs_expf_inrange(float x) {
 // One staged record (48 B, see the project kernel):
 //   r0 = (mx, my, k0, k2)   r1 = (k1, pcut, r, g)   r2 = (b, opacity, box_x, box_y)
 // One pixel's front-to-back step for one record (renderTile inner loop,
-// codelets.cpp:385-411), branch-free: every quantity is computed and the
-// state update is selected.  The pairs (dx, dy), (k0 dx, k2 dy), (r, g) and
-// (b, opacity) are computed as packed fp32 (each half is the same IEEE
-// operation as the scalar expression).  FAST: the record's pcut >= -80, so
-// any power the update accepts lies in [-80, 0], where gs_expf_inrange ==
-// gs_expf bit for bit.
+// codelets.cpp:385-411), split in two: blend_power_exp (independent of the
+// pixel's state, so two records' exponentials overlap) and blend_composite
+// (branch-free: every quantity is computed and the state update selected).
+// The pairs (dx, dy), (k0 dx, k2 dy), (r, g) and (b, opacity) are computed as
+// packed fp32 (each half is the same IEEE operation as the scalar
+// expression).  FAST: the record's pcut >= -80, so any power the update
+// accepts lies in [-80, 0], where gs_expf_inrange == gs_expf bit for bit.
 template <bool FAST>
-__device__ __forceinline__ void blend_step(Px& q, const float4& r0, const float4& r1,
-                                           const float4& r2) {
-  const f32x2 m = {r0.x, r0.y}, kd = {r0.z, r0.w};
-  const float k1 = r1.x, pcut = r1.y, op = r2.y;
-  const f32x2 d = m - q.p;          // (mx - px, my - py)
-  const f32x2 kdd = (kd * d) * d;   // (k0 * dx * dx, k2 * dy * dy)
-  const float power = -0.5f * (kdd.x + kdd.y) - k1 * d.x * d.y;
-  const float e = FAST ? gs_expf_inrange(power) : gs_expf(power);
+__device__ __forceinline__ float blend_power_exp(const Px& q, const float4& r0, const float4& r1,
+                                                 float& power) {
+  const float dx = r0.x - q.p.x, dy = r0.y - q.p.y;
+  const float k0 = r0.z, k2 = r0.w, k1 = r1.x;
+  power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
+  return FAST ? gs_expf_inrange(power) : gs_expf(power);
+}
+
+__device__ __forceinline__ void blend_composite(Px& q, float power, float e, const float4& r1,
+                                                const float4& r2, bool ok) {
+  const float pcut = r1.y, op = r2.y;
   const float v = op * e;
   const float alpha = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
   const float test_T = q.T * (1.0f - alpha);
   // power > 0: skipped; power < pcut: alpha < 1/255 guaranteed (`continue`)
-  const bool hit = !q.done && !(power > 0.0f) && !(power < pcut) && !(alpha < 1.0f / 255.0f);
+  const bool hit =
+      ok && !q.done && !(power > 0.0f) && !(power < pcut) && !(alpha < 1.0f / 255.0f);
   const bool brk = hit && test_T < 0.0001f;  // break (codelets.cpp:406-408)
   const bool upd = hit && !brk;
-  const f32x2 crg = {r1.z, r1.w}, cbo = {r2.x, op};
-  const f32x2 n01 = q.c01 + (crg * alpha) * q.T;  // colour += gCont * alpha * T
-  const f32x2 n23 = q.c23 + (cbo * alpha) * q.T;
-  q.c01.x = upd ? n01.x : q.c01.x;
-  q.c01.y = upd ? n01.y : q.c01.y;
-  q.c23.x = upd ? n23.x : q.c23.x;
-  q.c23.y = upd ? n23.y : q.c23.y;
+  const float n0 = q.c01.x + (r1.z * alpha) * q.T;  // colour += gCont * alpha * T
+  const float n1 = q.c01.y + (r1.w * alpha) * q.T;
+  const float n2 = q.c23.x + (r2.x * alpha) * q.T;
+  const float n3 = q.c23.y + (op * alpha) * q.T;
+  q.c01.x = upd ? n0 : q.c01.x;
+  q.c01.y = upd ? n1 : q.c01.y;
+  q.c23.x = upd ? n2 : q.c23.x;
+  q.c23.y = upd ? n3 : q.c23.y;
   q.T = upd ? test_T : q.T;
   q.done = q.done || brk;
 }
@@ -1140,24 +1146,26 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (quad_all(q.done)) m = 0ull;
-    if (m) {
-      int j = __builtin_ctzll(m);  // list order: ascending bits
-      float4 r0 = st[0][j], r1 = st[1][j], r2 = st[2][j];
-      for (;;) {
-        m &= m - 1ull;
-        const int jn = m ? __builtin_ctzll(m) : j;
-        // next record's read in flight during this record's math
-        const float4 n0 = st[0][jn], n1 = st[1][jn], n2 = st[2][jn];
-        if (r1.y >= -80.0f)  // pcut
-          blend_step<true>(q, r0, r1, r2);
-        else
-          blend_step<false>(q, r0, r1, r2);
-        if (quad_all(q.done)) m = 0ull;
-        if (!m) break;
-        r0 = n0;
-        r1 = n1;
-        r2 = n2;
+    // two records per iteration, in list order (ascending bits): their
+    // exponentials are independent, the compositing is sequential
+    while (m) {
+      const int ja = __builtin_ctzll(m);
+      m &= m - 1ull;
+      const bool two = m != 0ull;
+      const int jb = two ? __builtin_ctzll(m) : ja;
+      m &= m - 1ull;
+      const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
+      const float4 b0 = st[0][jb], b1 = st[1][jb], b2 = st[2][jb];
+      float pa, pb, ea, eb;
+      if (a1.y >= -80.0f && b1.y >= -80.0f) {  // pcut
+        ea = blend_power_exp<true>(q, a0, a1, pa);
+        eb = blend_power_exp<true>(q, b0, b1, pb);
+      } else {
+        ea = blend_power_exp<false>(q, a0, a1, pa);
+        eb = blend_power_exp<false>(q, b0, b1, pb);
       }
+      blend_composite(q, pa, ea, a1, a2, true);
+      blend_composite(q, pb, eb, b1, b2, two);
     }
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
