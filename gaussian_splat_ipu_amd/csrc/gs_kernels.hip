@@ -339,7 +339,7 @@ __device__ __forceinline__ int sort_class(uint32_t L) {
 
 __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b) {
   __shared__ unsigned long long wsum[16];
-  __shared__ uint32_t wq[16];  // per wave: medium count | big count << 16
+  __shared__ uint32_t wq[16];  // per wave: small | medium << 10 | big << 20 (<= 512 each)
   __shared__ uint32_t wmax[16];
   __shared__ uint32_t wvis[16];
   const int T = fp.n_tiles;
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
     for (int k = 0; k < 8; ++k) vsum += vr[k];
   }
   unsigned long long carry = 0;
-  uint32_t med_base = 0, big_base = 0, mx = 0;
+  uint32_t sml_base = 0, med_base = 0, big_base = 0, mx = 0;
   for (int r0 = 0; r0 < T; r0 += 8192) {
     const int i0 = r0 + tid * 8;
     uint32_t c[8];
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
       sum += c[j];
       mx = max(mx, c[j]);
       const int cl = sort_class(c[j]);
-      q += cl == 1 ? 1u : (cl == 2 ? 0x10000u : 0u);
+      q += cl == 0 ? (c[j] != 0u ? 1u : 0u) : (cl == 1 ? (1u << 10) : (1u << 20));
     }
     unsigned long long inc = sum;
     uint32_t qinc = q;
@@ -391,18 +391,21 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
     }
     __syncthreads();
     unsigned long long base = carry, total = carry;
-    uint32_t qbase = 0, qtot = 0;
+    uint32_t qb[3] = {0, 0, 0}, qt[3] = {0, 0, 0};
     for (int w = 0; w < 16; ++w) {
+      const uint32_t v = wq[w];
       if (w < wave) {
         base += wsum[w];
-        qbase += wq[w];
+        for (int k = 0; k < 3; ++k) qb[k] += (v >> (10 * k)) & 1023u;
       }
       total += wsum[w];
-      qtot += wq[w];
+      for (int k = 0; k < 3; ++k) qt[k] += (v >> (10 * k)) & 1023u;
     }
     unsigned long long run = base + inc - sum;
-    uint32_t med = med_base + (qbase & 0xFFFFu) + ((qinc - q) & 0xFFFFu);
-    uint32_t big = big_base + (qbase >> 16) + ((qinc - q) >> 16);
+    const uint32_t qx = qinc - q;  // this lane's exclusive counts in the wave
+    uint32_t sml = sml_base + qb[0] + (qx & 1023u);
+    uint32_t med = med_base + qb[1] + ((qx >> 10) & 1023u);
+    uint32_t big = big_base + qb[2] + ((qx >> 20) & 1023u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = i0 + j;
@@ -410,14 +413,16 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
         b.tile_start[i] = (uint32_t)run;
         if (fp.bin_global) b.tile_cursor[i] = (uint32_t)run;
         const int cl = sort_class(c[j]);
+        if (cl == 0 && c[j] != 0u) b.small_tiles[sml++] = (uint32_t)i;
         if (cl == 1) b.medium_tiles[med++] = (uint32_t)i;
         if (cl == 2) b.big_tiles[big++] = (uint32_t)i;
       }
       run += c[j];
     }
     carry = total;
-    med_base += qtot & 0xFFFFu;
-    big_base += qtot >> 16;
+    sml_base += qt[0];
+    med_base += qt[1];
+    big_base += qt[2];
     __syncthreads();  // wsum / wq are rewritten by the next round
   }
 #pragma unroll
@@ -438,6 +443,7 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
     b.counters[0] = big_base;
     b.counters[2] = vis;
     b.counters[7] = med_base;
+    b.counters[9] = sml_base;
     const unsigned long long total = carry;
     b.tile_start[T] = (uint32_t)(total < 0xFFFFFFFFull ? total : 0xFFFFFFFFull);
     b.counters[3] = total > fp.pair_cap ? 1u : 0u;
@@ -725,18 +731,31 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
   }
 }
 
-// One wave per tile: lists up to 1024 keys are sorted in registers; longer
-// lists are queued for the LDS sort (<= kSortLdsCap) or the radix sort.
-__global__ __launch_bounds__(256) void gs_sort_small_kernel(FrameParams fp, Buffers b) {
+// Small and medium lists in one launch.  Workgroups [0, n_medium) each sort
+// one medium list (512 < L <= 2048: 4 waves x E keys in registers, the strides
+// >= 64 E through LDS); the following workgroups give each of their waves one
+// small list (L <= 512, sorted in one wave's registers).  The long sorts have
+// the low workgroup ids, so they start first.  Keys are unique (the index is
+// in the low word), so the order is total and deterministic.
+__global__ __launch_bounds__(256) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long keys[kSortLdsCap];
+  const uint32_t n_med = b.counters[7], n_small = b.counters[9];
+  const uint32_t item = blockIdx.x;
+  if (item < n_med) {
+    uint32_t s, L;
+    tile_segment(fp, b, (int)b.medium_tiles[item], s, L);
+    if (L <= 1024u)
+      block_sort_tile<4, 4>(b, s, L, keys);
+    else
+      block_sort_tile<8, 4>(b, s, L, keys);
+    return;
+  }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int t = blockIdx.x * 4 + wave;
+  const uint32_t k = (item - n_med) * 4u + (uint32_t)wave;
+  if (k >= n_small) return;
   const int lane = threadIdx.x & 63;
-  if (t >= fp.n_tiles) return;
-  // longer lists were queued for the medium / big sorts by the scan kernel
-  if (sort_class(b.tile_count[t]) != 0) return;
   uint32_t s, L;
-  tile_segment(fp, b, t, s, L);
-  if (L == 0) return;
+  tile_segment(fp, b, (int)b.small_tiles[k], s, L);
   if (L <= 64u)
     wave_sort_tile<1>(b, s, L, lane);
   else if (L <= 128u)
@@ -745,50 +764,6 @@ __global__ __launch_bounds__(256) void gs_sort_small_kernel(FrameParams fp, Buff
     wave_sort_tile<4>(b, s, L, lane);
   else
     wave_sort_tile<8>(b, s, L, lane);
-}
-
-// Medium lists (1024 < L <= kSortLdsCap): bitonic network over the padded
-// power-of-two list in LDS (32 KB), 256 threads; workgroups pull tiles from the
-// queue the small-sort kernel filled.  Keys are unique (the index is in the
-// low word), so the order is total and deterministic.
-__global__ __launch_bounds__(256) void gs_sort_kernel(FrameParams fp, Buffers b) {
-  __shared__ unsigned long long keys[kSortLdsCap];
-  __shared__ uint32_t s_item;
-  const int tid = threadIdx.x;
-  const uint32_t n_med = b.counters[7];
-  // one workgroup per queued tile (grid = n_tiles; the surplus exits at once)
-  for (uint32_t item = blockIdx.x; item < n_med; item += gridDim.x) {
-    (void)s_item;
-    const int t = (int)b.medium_tiles[item];
-    uint32_t s, L;
-    tile_segment(fp, b, t, s, L);
-    if (L <= 2048u) {  // 4 waves x 512 keys in registers, 3 LDS exchanges
-      block_sort_tile<8, 4>(b, s, L, keys);
-      __syncthreads();
-      continue;
-    }
-    uint32_t n2 = 2;
-    while (n2 < L) n2 <<= 1;
-    for (uint32_t i = tid; i < n2; i += 256) keys[i] = i < L ? b.pairs[s + i] : ~0ull;
-    __syncthreads();
-    for (uint32_t k = 2; k <= n2; k <<= 1) {
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        for (uint32_t i = tid; i < (n2 >> 1); i += 256) {
-          const uint32_t lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
-          const uint32_t hi = lo + j;
-          const bool asc = (lo & k) == 0;
-          const unsigned long long x = keys[lo], y = keys[hi];
-          if ((x > y) == asc) {
-            keys[lo] = y;
-            keys[hi] = x;
-          }
-        }
-        __syncthreads();
-      }
-    }
-    for (uint32_t i = tid; i < L; i += 256) b.list[s + i] = (uint32_t)keys[i];
-    __syncthreads();
-  }
 }
 
 // Large lists: a block-wide stable LSD radix sort (8 passes x 8 bits) over the
@@ -1166,6 +1141,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
       }
       blend_composite(q, pa, ea, a1, a2, true);
       blend_composite(q, pb, eb, b1, b2, two);
+      if (quad_all(q.done)) m = 0ull;  // the quad has saturated
     }
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
@@ -1213,8 +1189,7 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
-  gs_sort_small_kernel<<<(fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
-  gs_sort_kernel<<<fp.n_tiles, 256, 0, s>>>(fp, b);
+  gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
   gs_sort_big_kernel<<<64, 1024, 0, s>>>(fp, b);
 }
 

@@ -55,19 +55,20 @@ struct Buffers {
   unsigned long long* pairs_alt;  // [pair_cap]  scratch of the large-list sort
   uint32_t* list;           // [pair_cap]  depth-sorted Gaussian indices
   uint32_t* big_tiles;      // [n_tiles]  lists > kSortLdsCap (radix sort queue)
-  uint32_t* medium_tiles;   // [n_tiles]  lists in (1024, kSortLdsCap] (LDS sort queue)
+  uint32_t* medium_tiles;   // [n_tiles]  lists in (kSortRegCap, kSortLdsCap] (block sort queue)
+  uint32_t* small_tiles;    // [n_tiles]  lists in [1, kSortRegCap] (one-wave sort queue)
   uint32_t* chunk_off;      // [n_chunks][n_tiles] chunk histograms -> offsets
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
   uint32_t* counters;       // [16]: 0 n_big, 1 big_next, 2 n_rendered, 3 overflow,
                             //  4 max_list, 5 n_pairs (low), 6 n_pairs (high),
-                            //  7 n_medium, 8 medium_next
+                            //  7 n_medium, 8 medium_next, 9 n_small
   // outputs
   float4* rgba;             // band_rows x width, row-major
   uint8_t* bgr;             // band rows (padded) x width x 3
 };
 
 constexpr int GS_STAGE_EVENTS = 6;  // profile events: before project .. after blend
-constexpr int kSortLdsCap = 4096;  // largest tile list sorted in LDS by one workgroup
+constexpr int kSortLdsCap = 2048;  // largest tile list sorted by one workgroup (registers + LDS)
 constexpr uint32_t kSortRegCap = 512;  // largest tile list sorted in the registers of one wave
 constexpr size_t kBinLdsMax = 160 * 1024;  // LDS of one CU: chunk histograms up to 81920 tiles
 
