@@ -532,7 +532,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
     const uint2 r = b.rect[i];
     const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
     if (x0 > x1) continue;
-    const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | (uint32_t)i;
+    const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
     for (uint32_t y = y0; y <= y1; ++y)
       for (uint32_t x = x0; x <= x1; ++x) {
         const uint32_t t = y * fp.tiles_x + x;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b)
   const uint2 r = b.rect[i];
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   if (x0 > x1) return;
-  const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | (uint32_t)i;
+  const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
   for (uint32_t y = y0; y <= y1; ++y)
     for (uint32_t x = x0; x <= x1; ++x) {
       const uint32_t pos = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], 1u);
@@ -711,7 +711,7 @@ __device__ __forceinline__ void block_sort_tile(const Buffers& b, uint32_t s, ui
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const uint32_t i = (uint32_t)(ibase + lane * E + e);
-    if (i < L) b.list[s + i] = (uint32_t)v[e];
+    if (i < L) b.list[s + i] = b.inv_perm[(uint32_t)v[e]];
   }
 }
 
@@ -727,7 +727,7 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const uint32_t i = (uint32_t)(lane * E + e);
-    if (i < L) b.list[s + i] = (uint32_t)v[e];
+    if (i < L) b.list[s + i] = b.inv_perm[(uint32_t)v[e]];
   }
 }
 
@@ -861,7 +861,7 @@ __global__ __launch_bounds__(1024) void gs_sort_big_kernel(FrameParams fp, Buffe
       src = dst;
       dst = tmp;
     }
-    for (uint32_t i = tid; i < L; i += 1024) b.list[s + i] = (uint32_t)src[i];
+    for (uint32_t i = tid; i < L; i += 1024) b.list[s + i] = b.inv_perm[(uint32_t)src[i]];
     __syncthreads();
   }
 }

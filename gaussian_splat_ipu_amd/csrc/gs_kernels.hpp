@@ -43,6 +43,10 @@ struct Buffers {
   const float4* colour;     // r g b opacity
   const float4* rot;        // quaternion (w x y z)
   const float4* scale_gid;  // sx sy sz gid
+  // device order: record i is the input Gaussian perm[i] (3D Morton order by
+  // default); the depth sort breaks ties by the input index, as the reference
+  const uint32_t* perm;     // [n] device index -> input index
+  const uint32_t* inv_perm; // [n] input index -> device index
   // per-Gaussian projection outputs
   float4* rec;              // 4 x float4 (64 B): mx my k0 k1 | k2 k3 r g | b pcut boxx boxy | radius clipz 0 0
   uint32_t* depth_key;      // order-preserving key of clip z
@@ -51,9 +55,9 @@ struct Buffers {
   uint32_t* tile_count;     // [n_tiles]      (memset 0 each frame)
   uint32_t* tile_start;     // [n_tiles + 1]
   uint32_t* tile_cursor;    // [n_tiles]
-  unsigned long long* pairs;      // [pair_cap]  (depth_key << 32 | index)
+  unsigned long long* pairs;      // [pair_cap]  (depth_key << 32 | input index)
   unsigned long long* pairs_alt;  // [pair_cap]  scratch of the large-list sort
-  uint32_t* list;           // [pair_cap]  depth-sorted Gaussian indices
+  uint32_t* list;           // [pair_cap]  depth-sorted Gaussians (device indices)
   uint32_t* big_tiles;      // [n_tiles]  lists > kSortLdsCap (radix sort queue)
   uint32_t* medium_tiles;   // [n_tiles]  lists in (kSortRegCap, kSortLdsCap] (block sort queue)
   uint32_t* small_tiles;    // [n_tiles]  lists in [1, kSortRegCap] (one-wave sort queue)

@@ -45,6 +45,8 @@ struct gs_renderer {
   float fov = 0.6981317f;  // glm::radians(40.f) (splat.cpp:170)
   float scale_div = 0.1f;  // lambda1 / 10 with lambda1 = 1 (InterfaceServer.hpp:238)
 
+  std::vector<uint32_t> perm;  // device index -> input index
+
   // geometry
   int tiles_x = 0, tiles_y = 0, band_ty0 = 0, band_ty1 = 0, band_py0 = 0, band_rows = 0;
   int band_rows_padded = 0, n_tiles = 0;
@@ -101,6 +103,51 @@ int select_device(gs_renderer* r) {
 void free_pairs(gs_renderer* r) {
   if (r->d_pairs) (void)hipFree(r->d_pairs);
   r->d_pairs = nullptr;
+}
+
+// Device order of the Gaussians: 3D Morton order of the means (21 bits per
+// axis over their bounding box; non-finite coordinates count as the box
+// minimum), ties by input index.  Neighbours in this order are neighbours on
+// screen, so a binning chunk's entries of one tile are contiguous and a tile's
+// records share cache lines.  The order is an internal layout: keys carry the
+// input index, so the depth order (ties by input index) is unchanged.
+std::vector<uint32_t> morton_order(const gs_gaussian3d* g, size_t n, bool keep) {
+  std::vector<uint32_t> perm(n);
+  for (size_t i = 0; i < n; ++i) perm[i] = (uint32_t)i;
+  if (keep || n < 2) return perm;
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (size_t i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) {
+      const float v = g[i].mean[a];
+      if (std::isfinite(v)) {
+        lo[a] = std::min(lo[a], v);
+        hi[a] = std::max(hi[a], v);
+      }
+    }
+  auto spread = [](uint64_t v) {  // 21 bits -> every third bit
+    v &= 0x1FFFFFull;
+    v = (v | (v << 32)) & 0x1F00000000FFFFull;
+    v = (v | (v << 16)) & 0x1F0000FF0000FFull;
+    v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+    v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+    v = (v | (v << 2)) & 0x1249249249249249ull;
+    return v;
+  };
+  std::vector<std::pair<uint64_t, uint32_t>> key(n);
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t c = 0;
+    for (int a = 0; a < 3; ++a) {
+      const float v = g[i].mean[a];
+      double t = 0.0;
+      if (std::isfinite(v) && hi[a] > lo[a]) t = ((double)v - lo[a]) / ((double)hi[a] - lo[a]);
+      const uint64_t q = (uint64_t)std::min(2097151.0, std::max(0.0, t * 2097151.0));
+      c |= spread(q) << a;
+    }
+    key[i] = {c, (uint32_t)i};
+  }
+  std::sort(key.begin(), key.end());
+  for (size_t i = 0; i < n; ++i) perm[i] = key[i].second;
+  return perm;
 }
 
 int alloc_pairs(gs_renderer* r, uint64_t cap) {
@@ -345,28 +392,40 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
     return fail(hip_fail(e, "hipStreamCreate"));
   r->stream = r->own_stream;
 
-  // scene: SoA of the 64-B records
+  // scene: SoA of the 64-B records, in device order (3D Morton order of the
+  // means unless GS_FLAG_INPUT_ORDER), plus the permutation both ways
   const size_t nn = std::max<size_t>(n, 1);
-  if ((e = hipMalloc(&r->d_scene, nn * 64)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(scene)"));
+  r->perm = morton_order(g, n, (cfg->flags & GS_FLAG_INPUT_ORDER) != 0);
+  if ((e = hipMalloc(&r->d_scene, nn * (64 + 8))) != hipSuccess)
+    return fail(hip_fail(e, "hipMalloc(scene)"));
   {
     std::vector<float> soa(nn * 16, 0.0f);
+    std::vector<uint32_t> pi(nn * 2, 0u);
     for (size_t i = 0; i < n; ++i) {
-      const float* s = reinterpret_cast<const float*>(&g[i]);
+      const uint32_t o = r->perm[i];
+      const float* s = reinterpret_cast<const float*>(&g[o]);
       for (int k = 0; k < 4; ++k) {
         soa[(0 * nn + i) * 4 + k] = s[0 + k];
         soa[(1 * nn + i) * 4 + k] = s[4 + k];
         soa[(2 * nn + i) * 4 + k] = s[8 + k];
         soa[(3 * nn + i) * 4 + k] = s[12 + k];
       }
+      pi[i] = o;
+      pi[nn + o] = (uint32_t)i;
     }
     if ((e = hipMemcpy(r->d_scene, soa.data(), nn * 64, hipMemcpyHostToDevice)) != hipSuccess)
       return fail(hip_fail(e, "hipMemcpy(scene)"));
+    if ((e = hipMemcpy((char*)r->d_scene + nn * 64, pi.data(), nn * 8, hipMemcpyHostToDevice)) !=
+        hipSuccess)
+      return fail(hip_fail(e, "hipMemcpy(permutation)"));
   }
   const float4* sc = (const float4*)r->d_scene;
   r->buf.mean = sc;
   r->buf.colour = sc + nn;
   r->buf.rot = sc + 2 * nn;
   r->buf.scale_gid = sc + 3 * nn;
+  r->buf.perm = (const uint32_t*)(sc + 4 * nn);
+  r->buf.inv_perm = r->buf.perm + nn;
 
   // per Gaussian: 64-B record, 8-B tile rectangle, 4-B depth key; plus V per
   // project workgroup
@@ -599,8 +658,11 @@ int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t*
   std::vector<uint32_t> ts(T + 1);
   GS_HIP(hipMemcpy(ts.data(), r->buf.tile_start, (T + 1) * 4, hipMemcpyDeviceToHost));
   for (size_t i = 0; i <= T; ++i) tile_start[i] = ts[i];
-  if (r->stats.n_pairs)
+  if (r->stats.n_pairs) {
     GS_HIP(hipMemcpy(list, r->buf.list, r->stats.n_pairs * 4, hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < r->stats.n_pairs; ++k)  // device -> input indices
+      list[k] = list[k] < r->n ? r->perm[list[k]] : list[k];
+  }
   return GS_OK;
 }
 
@@ -621,7 +683,7 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
   }
   for (size_t i = 0; i < r->n; ++i) {
     const float* q = &rec[i * 16];
-    float* o = dst + i * 12;
+    float* o = dst + (size_t)r->perm[i] * 12;  // in input order
     o[0] = q[0];  // mean2d
     o[1] = q[1];
     o[2] = q[2];  // conic (k0, k1, k2, opacity)

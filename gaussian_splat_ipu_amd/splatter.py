@@ -22,6 +22,7 @@ import numpy as np
 from . import camera
 from ._lib import (
     GS_FLAG_BIN_GLOBAL,
+    GS_FLAG_INPUT_ORDER,
     GS_FLAG_NO_RGBA32F,
     GS_FLAG_PROFILE,
     GS_K_COUNT,
@@ -60,6 +61,7 @@ class GpuSplatter:
         write_rgba: bool = True,
         profile: bool = False,
         bin_global: bool = False,
+        input_order: bool = False,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -81,6 +83,7 @@ class GpuSplatter:
             (0 if write_rgba else GS_FLAG_NO_RGBA32F)
             | (GS_FLAG_PROFILE if profile else 0)
             | (GS_FLAG_BIN_GLOBAL if bin_global else 0)
+            | (GS_FLAG_INPUT_ORDER if input_order else 0)
         )
         self.cfg = cfg
         h = C.c_void_p()

@@ -66,6 +66,10 @@ typedef struct gs_config {
 #define GS_FLAG_PROFILE 2u     /* record HIP events around every kernel     */
 #define GS_FLAG_BIN_GLOBAL 4u  /* bin with global atomics instead of the chunked
                                   LDS histograms (automatic for > 81920 tiles) */
+#define GS_FLAG_INPUT_ORDER 8u /* keep the Gaussians in input order on the device
+                                  (default: 3D Morton order, which makes the
+                                  binning writes and the blend's record reads
+                                  local; results are identical either way) */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */

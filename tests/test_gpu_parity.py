@@ -31,7 +31,7 @@ def assert_same_bits(a, b, what=""):
 
 
 def _frame_pair(g, view, proj, W, H, TW, TH, scale_div, fov=None, guard_tile=None, band=None, band_count=1,
-                band_index=0, pair_capacity=0, bin_global=False):
+                band_index=0, pair_capacity=0, bin_global=False, input_order=False):
     from gaussian_splat_ipu_amd import camera
     from gaussian_splat_ipu_amd.splatter import GpuSplatter
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
@@ -40,7 +40,7 @@ def _frame_pair(g, view, proj, W, H, TW, TH, scale_div, fov=None, guard_tile=Non
     fov = camera.FOV_DEFAULT if fov is None else fov
     fb = TiledFramebuffer(W, H, TW, TH)
     s = GpuSplatter(g, fb, device=0, guard_tile=guard_tile, band_index=band_index, band_count=band_count,
-                    pair_capacity=pair_capacity, bin_global=bin_global)
+                    pair_capacity=pair_capacity, bin_global=bin_global, input_order=input_order)
     s.set_view_wire(view)
     s.set_projection_wire(proj)
     s.update_focal_lengths(fov, scale_div)
@@ -104,16 +104,20 @@ def test_pc12_reference_geometry_720p(pc12, scale_div):
     assert ref["stats"]["n_pairs"] > 50000
 
 
-@pytest.mark.parametrize("tw,th,bin_global", [(16, 16, False), (16, 16, True), (48, 30, False), (32, 20, False)])
-def test_pc12_1080p(pc12, tw, th, bin_global):
+@pytest.mark.parametrize("tw,th,bin_global,input_order", [
+    (16, 16, False, False), (16, 16, True, False), (16, 16, False, True), (48, 30, False, False),
+    (32, 20, False, False)])
+def test_pc12_1080p(pc12, tw, th, bin_global, input_order):
     """config 2: point_cloud_12 at 1920x1080 (16x16 production tiles, 48x30 =
     the reference macros at 1080p, 32x20); 1080/16 leaves a partial tile row.
-    Both binning paths (chunked LDS histograms, global atomics)."""
+    Both binning paths (chunked LDS histograms, global atomics), and both
+    device orders of the Gaussians (Morton, input)."""
     from gaussian_splat_ipu_amd import camera
 
     g, bb = pc12
     view, proj = camera.headless(bb, 1920, 1080)
-    s, f = _frame_pair(g, view, proj, 1920, 1080, tw, th, 1.0, bin_global=bin_global)
+    s, f = _frame_pair(g, view, proj, 1920, 1080, tw, th, 1.0, bin_global=bin_global,
+                       input_order=input_order)
     _assert_parity(s, f, g)
 
 
