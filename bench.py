@@ -43,6 +43,16 @@ def parse():
     return ap.parse_args()
 
 
+# the kernels behind each timed stage (rocprof short names)
+STAGE_KERNELS = {
+    "project": ["gs_project"],
+    "scan": ["gs_count", "gs_colscan", "gs_scan"],
+    "emit": ["gs_emit_chunk", "gs_emit"],
+    "sort": ["gs_sort_tiles", "gs_sort_big"],
+    "blend": ["gs_blend"],
+}
+
+
 def alg_bytes(kernel: str, st: dict, n: int, px: int) -> float:
     """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md)."""
     T, P = st["n_tiles"], st["n_pairs"]
@@ -138,12 +148,16 @@ def main():
             "alg_GBps": round(b / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None,
         }
     dom = max(kern, key=lambda k: kern[k]["avg_ms"])
+    # HBM bytes per launch of the same stage, from the committed PMC summary of
+    # this workload (tools/profile.sh + tools/pmc_summary.py), when it matches
     pmc = None
     if os.path.exists(a.pmc_json):
         try:
             pm = json.load(open(a.pmc_json))
-            if pm.get("config") == f"{a.n}@{W}x{H}/t{TW}/w{world}" and dom in pm.get("kernels", {}):
-                pmc = pm["kernels"][dom].get("hbm_bytes_per_launch")
+            ks = pm.get("kernels", {})
+            names = [k for k in STAGE_KERNELS[dom] if k in ks]
+            if pm.get("config") == f"{a.n}@{W}x{H}/t{TW}/w{world}" and names:
+                pmc = int(sum(ks[k]["hbm_bytes_per_launch"] for k in names))
         except Exception:
             pmc = None
     dk = kern[dom]
