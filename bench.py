@@ -91,22 +91,39 @@ def main():
     del ply
     view, proj = camera.headless(bb, W, H)
     fb = TiledFramebuffer(W, H, TW, TW)
-    s = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=True)
+    # N > 1: interleaved tile-row bands (rank r owns rows r, r + N, ...), so
+    # every rank gets an equal share of the scene's dense centre rows
+    s = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=True,
+                    band_interleaved=world > 1)
     s.set_view_wire(view)
     s.set_projection_wire(proj)
     s.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
     stream = torch.cuda.current_stream()
     s.set_stream(stream.cuda_stream)
 
+    # N > 1: frame k's band is copied out and all-gathered (RCCL) on a second
+    # stream while frame k+1 renders; two band / frame buffers alternate.
     band_bytes = fb.rows_per_band_padded(world) * W * 3
-    band = torch.empty(band_bytes, dtype=torch.uint8, device="cuda")
-    frame = torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") if world > 1 else None
+    nbuf = 2 if world > 1 else 0
+    band = [torch.empty(band_bytes, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
+    frame = [torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
+    comm = torch.cuda.Stream() if world > 1 else None
+    ev_copy = [torch.cuda.Event() for _ in range(nbuf)]
+    ev_free = [torch.cuda.Event() for _ in range(nbuf)]
+    nframe = [0]
 
     def one_frame():
         s.execute_async()
         if world > 1:
-            s.copy_bgr8_device(band.data_ptr(), band_bytes)
-            dist.all_gather_into_tensor(frame, band)
+            i = nframe[0] % 2
+            stream.wait_event(ev_free[i])  # the gather of frame k-2 read band[i]
+            s.copy_bgr8_device(band[i].data_ptr(), band_bytes)
+            ev_copy[i].record(stream)
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev_copy[i])
+                dist.all_gather_into_tensor(frame[i], band[i])
+                ev_free[i].record(comm)
+        nframe[0] += 1
 
     # warm-up (the first blocking render sizes the pair buffer)
     s.execute()
@@ -216,7 +233,7 @@ def main():
                 "gaussians": a.n,
                 "resolution": [W, H],
                 "tile": [TW, TW],
-                "parallelism": f"row-band x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"row-band x{world}" + (" (interleaved tile rows) + RCCL all-gather" if world > 1 else ""),
             },
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "max_list", "n_tiles", "n_big_tiles")},
             "kernels": kern,

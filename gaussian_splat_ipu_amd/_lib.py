@@ -19,6 +19,7 @@ GS_FLAG_NO_RGBA32F = 1
 GS_FLAG_PROFILE = 2
 GS_FLAG_BIN_GLOBAL = 4
 GS_FLAG_INPUT_ORDER = 8
+GS_FLAG_BAND_INTERLEAVED = 16
 GS_LAYOUT_ROW_MAJOR = 0
 GS_LAYOUT_REF_TILE_MAJOR = 1
 GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_COUNT = range(6)
@@ -88,6 +89,7 @@ class FrameStats(C.Structure):
         ("band_y0", C.c_uint32),
         ("band_rows", C.c_uint32),
         ("n_big_tiles", C.c_uint32),
+        ("band_stride", C.c_uint32),
     ]
 
     def as_dict(self):

@@ -291,16 +291,21 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       float fx1 = __builtin_floorf(__builtin_ceilf(maxx) / fp.tw);
       float fy0 = __builtin_floorf(__builtin_floorf(miny) / fp.th);
       float fy1 = __builtin_floorf(__builtin_ceilf(maxy) / fp.th);
-      const float gx1 = (float)(fp.tiles_x - 1);
-      const float gy0 = (float)fp.band_ty0, gy1 = (float)(fp.band_ty1 - 1);
+      const float gx1 = (float)(fp.tiles_x - 1), gy1 = (float)(fp.tiles_y - 1);
       if (fx0 < 0.0f) fx0 = 0.0f;
       if (fx1 > gx1) fx1 = gx1;
-      if (fy0 < gy0) fy0 = gy0;
+      if (fy0 < 0.0f) fy0 = 0.0f;
       if (fy1 > gy1) fy1 = gy1;
-      if (fx0 <= fx1 && fy0 <= fy1) {
+      // this band's rows among the absolute rows [fy0, fy1]
+      int yb0 = 0, yb1 = -1;
+      if (fy0 <= fy1) {
+        const int a0 = (int)fy0 - fp.band_ty0, a1 = (int)fy1 - fp.band_ty0, S = fp.band_stride;
+        yb0 = a0 <= 0 ? 0 : (a0 + S - 1) / S;
+        yb1 = a1 < 0 ? -1 : min(a1 / S, fp.band_nrows - 1);
+      }
+      if (fx0 <= fx1 && yb0 <= yb1) {
         const uint32_t x0 = (uint32_t)(int)fx0, x1 = (uint32_t)(int)fx1;
-        const uint32_t y0 = (uint32_t)((int)fy0 - fp.band_ty0);
-        const uint32_t y1 = (uint32_t)((int)fy1 - fp.band_ty0);
+        const uint32_t y0 = (uint32_t)yb0, y1 = (uint32_t)yb1;
         rect = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
         if (fp.bin_global)  // fallback binning: per-tile lengths by global atomics
           for (uint32_t y = y0; y <= y1; ++y)
@@ -949,9 +954,9 @@ __device__ __forceinline__ void blend_composite(Px& q, float power, float e, con
   q.done = q.done || brk;
 }
 
-__device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers& b, int px, int py,
+// row: the pixel's row in this band's output
+__device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers& b, int px, int row,
                                             const Px& q) {
-  const int row = py - fp.band_py0;
   const float o0 = 0.0f + q.c01.x, o1 = 0.0f + q.c01.y, o2 = 0.0f + q.c23.x, o3 = 0.0f + q.c23.y;
   if (fp.write_rgba) b.rgba[(size_t)row * fp.width + px] = make_float4(o0, o1, o2, o3);
   uint8_t* dst = b.bgr + (size_t)row * fp.bgr_pitch + 3 * (size_t)px;
@@ -992,7 +997,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   const int myq = lane >> 2;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
   const int tile_x0 = tx * fp.tile_w;
-  const int tile_y0 = (fp.band_ty0 + tyb) * fp.tile_h;
+  const int tile_y0 = (fp.band_ty0 + tyb * fp.band_stride) * fp.tile_h;
   constexpr int bqw = BQW;  // 4 | 8: block of quads; 0: quad-row-major run
 
   // the wave's first quad (tile-local pixel coordinates) and quad count
@@ -1146,7 +1151,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
   }
-  if (valid) store_pixel(fp, b, px, py, q);
+  if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
 
 }  // namespace

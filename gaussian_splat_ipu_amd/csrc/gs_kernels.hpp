@@ -21,9 +21,10 @@ struct FrameParams {
   int tile_w, tile_h;
   int tiles_x;        // ceil(W / tw)
   int band_ty0;       // first tile row of this band (absolute)
-  int band_ty1;       // one past the last tile row of this band
-  int band_py0;       // first pixel row of this band
-  int band_rows;      // pixel rows of this band (<= (ty1-ty0)*th)
+  int band_stride;    // tile-row stride: band row k is absolute row band_ty0 + k * stride
+  int band_nrows;     // tile rows in this band
+  int tiles_y;        // tile rows of the whole frame
+  int band_rows;      // pixel rows of this band's output
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
   int chunks_per_tile;  // blend waves per tile (16 pixel quads each)

@@ -48,7 +48,8 @@ struct gs_renderer {
   std::vector<uint32_t> perm;  // device index -> input index
 
   // geometry
-  int tiles_x = 0, tiles_y = 0, band_ty0 = 0, band_ty1 = 0, band_py0 = 0, band_rows = 0;
+  int tiles_x = 0, tiles_y = 0, band_ty0 = 0, band_stride = 1, band_nrows = 0, band_py0 = 0,
+      band_rows = 0;
   int band_rows_padded = 0, n_tiles = 0;
   uint64_t pair_cap = 0;
 
@@ -204,8 +205,9 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tile_h = (int)r->cfg.tile_height;
   fp.tiles_x = r->tiles_x;
   fp.band_ty0 = r->band_ty0;
-  fp.band_ty1 = r->band_ty1;
-  fp.band_py0 = r->band_py0;
+  fp.band_stride = r->band_stride;
+  fp.band_nrows = r->band_nrows;
+  fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.n = (int)r->n;
   fp.n_tiles = r->n_tiles;
@@ -375,15 +377,30 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
     return fail(GS_EINVAL);
   }
   const int rpb = (r->tiles_y + (int)cfg->band_count - 1) / (int)cfg->band_count;
-  r->band_ty0 = std::min(r->tiles_y, (int)cfg->band_index * rpb);
-  r->band_ty1 = std::min(r->tiles_y, r->band_ty0 + rpb);
-  r->band_py0 = r->band_ty0 * (int)cfg->tile_height;
-  r->band_rows = std::max(0, std::min((int)cfg->height, r->band_ty1 * (int)cfg->tile_height) - r->band_py0);
-  r->band_rows_padded = rpb * (int)cfg->tile_height;
-  r->n_tiles = r->tiles_x * (r->band_ty1 - r->band_ty0);
+  const int th_px = (int)cfg->tile_height;
+  if (cfg->flags & GS_FLAG_BAND_INTERLEAVED) {
+    // rows band_index, band_index + band_count, ...; output = those tile rows
+    // back to back (whole tiles; rows past the image stay 0)
+    const int bc = (int)cfg->band_count, bi = (int)cfg->band_index;
+    r->band_ty0 = std::min(r->tiles_y, bi);
+    r->band_stride = bc;
+    r->band_nrows = r->tiles_y > bi ? (r->tiles_y - bi + bc - 1) / bc : 0;
+    r->band_py0 = r->band_ty0 * th_px;
+    r->band_rows = r->band_nrows * th_px;
+  } else {
+    r->band_ty0 = std::min(r->tiles_y, (int)cfg->band_index * rpb);
+    const int ty1 = std::min(r->tiles_y, r->band_ty0 + rpb);
+    r->band_stride = 1;
+    r->band_nrows = ty1 - r->band_ty0;
+    r->band_py0 = r->band_ty0 * th_px;
+    r->band_rows = std::max(0, std::min((int)cfg->height, ty1 * th_px) - r->band_py0);
+  }
+  r->band_rows_padded = rpb * th_px;
+  r->n_tiles = r->tiles_x * r->band_nrows;
   r->stats.n_tiles = (uint32_t)r->n_tiles;
   r->stats.tiles_x = (uint32_t)r->tiles_x;
-  r->stats.tiles_y = (uint32_t)(r->band_ty1 - r->band_ty0);
+  r->stats.tiles_y = (uint32_t)r->band_nrows;
+  r->stats.band_stride = (uint32_t)r->band_stride;
   r->stats.band_y0 = (uint32_t)r->band_py0;
   r->stats.band_rows = (uint32_t)r->band_rows;
 

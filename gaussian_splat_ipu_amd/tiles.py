@@ -149,5 +149,11 @@ class TiledFramebuffer:
             out.append((ty0, ty1, py0, rows))
         return out
 
+    def interleaved_tile_rows(self, band_count: int, band_index: int):
+        """Tile rows of an interleaved band (GS_FLAG_BAND_INTERLEAVED): rows
+        band_index, band_index + band_count, ...; the band's output holds them
+        back to back, tile_height pixel rows each."""
+        return list(range(band_index, self.tiles_down, band_count))
+
     def rows_per_band_padded(self, band_count: int) -> int:
         return math.ceil(self.tiles_down / band_count) * self.tile_height

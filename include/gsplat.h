@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 1
+#define GSPLAT_ABI_VERSION 2
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -57,7 +57,10 @@ typedef struct gs_config {
   float guard_band;                   /* clipSize (15)                      */
   int32_t device;                     /* HIP device ordinal, -1 = current   */
   uint32_t band_index, band_count;    /* row-band shard: tile rows split into
-                                         band_count contiguous bands         */
+                                         band_count contiguous bands, or
+                                         interleaved (GS_FLAG_BAND_INTERLEAVED:
+                                         rows r with r % band_count ==
+                                         band_index)                         */
   uint64_t pair_capacity;             /* initial (tile,Gaussian) capacity, 0 = auto */
   uint32_t flags;                     /* GS_FLAG_*                          */
 } gs_config;
@@ -70,6 +73,9 @@ typedef struct gs_config {
                                   (default: 3D Morton order, which makes the
                                   binning writes and the blend's record reads
                                   local; results are identical either way) */
+#define GS_FLAG_BAND_INTERLEAVED 16u /* band = tile rows band_index,
+                                  band_index + band_count, ...: every band gets
+                                  an equal share of a scene's dense rows */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */
@@ -86,8 +92,12 @@ typedef struct gs_frame_stats {
   uint64_t pair_capacity;
   uint32_t n_tiles;       /* tiles in this renderer's band      */
   uint32_t tiles_x, tiles_y;
-  uint32_t band_y0, band_rows;  /* pixel rows of this band          */
+  uint32_t band_y0, band_rows;  /* pixel rows of this band: contiguous
+                                   bands start at band_y0; interleaved bands
+                                   hold their tile rows back to back, padded
+                                   to whole tiles                   */
   uint32_t n_big_tiles;   /* tiles sorted by the large-list path */
+  uint32_t band_stride;   /* tile-row stride of the band (1: contiguous) */
 } gs_frame_stats;
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, interleaved=False):
     import torch
     import torch.distributed as dist
 
@@ -34,14 +34,24 @@ def _worker(rank, world, port, q):
         W, H, T = 640, 360, 16
         fb = TiledFramebuffer(W, H, T, T)
         view, proj = camera.headless(bb, W, H)
-        ty0, ty1, _, rows = fb.band_rows(world)[rank]
-        f = O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
-        band = O.render(g, f, nthreads=2)["bgr"]
-        assert band.shape[0] == rows
+        if interleaved:
+            # tile rows rank, rank + world, ...: each rendered as a one-row
+            # oracle band (the GPU renders them in one pass; test_gpu_parity)
+            parts = []
+            for ty in fb.interleaved_tile_rows(world, rank):
+                f = O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0, band=(ty, ty + 1))
+                b1 = O.render(g, f, nthreads=2)["bgr"]
+                parts.append(np.concatenate([b1, np.zeros((T - b1.shape[0],) + b1.shape[1:], b1.dtype)]))
+            band = np.concatenate(parts) if parts else np.zeros((0, W, 3), np.uint8)
+        else:
+            ty0, ty1, _, rows = fb.band_rows(world)[rank]
+            f = O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
+            band = O.render(g, f, nthreads=2)["bgr"]
+            assert band.shape[0] == rows
         padded = torch.from_numpy(gdist.pad_band(band, fb, world).reshape(-1))
         out = torch.empty(padded.numel() * world, dtype=torch.uint8)
         dist.all_gather_into_tensor(out, padded)
-        frame = gdist.assemble(out.numpy(), fb, world)
+        frame = gdist.assemble(out.numpy(), fb, world, interleaved=interleaved)
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if rank == 0:
@@ -51,14 +61,14 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_band_allgather_equals_single_frame(built, world):
+@pytest.mark.parametrize("world,interleaved", [(2, False), (3, False), (3, True)])
+def test_band_allgather_equals_single_frame(built, world, interleaved):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, interleaved)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -145,6 +145,42 @@ def test_large_tile_lists_take_the_radix_path(built):
     assert s.stats()["n_big_tiles"] > 0
 
 
+@pytest.mark.parametrize("band_count", [3, 8])
+def test_interleaved_bands_equal_full_frame_rows(pc12, band_count):
+    """GS_FLAG_BAND_INTERLEAVED (the multi-GPU default in bench.py): band b
+    renders tile rows b, b + band_count, ...  Its RGBA, BGR8 and per-tile list
+    lengths equal those rows of the single-renderer frame (itself checked
+    against the oracle), and the all-gather layout assembles back to it."""
+    from gaussian_splat_ipu_amd import camera, dist as gdist
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    g, bb = pc12
+    W, H, TW, TH = 1920, 1080, 16, 16
+    view, proj = camera.headless(bb, W, H)
+    full, f = _frame_pair(g, view, proj, W, H, TW, TH, 1.0)
+    _assert_parity(full, f, g, check_proj=False)
+    fb = TiledFramebuffer(W, H, TW, TH)
+    rgba, bgr = full.get_rgba(), full.get_frame_buffer()
+    hist = full.get_histogram().reshape(fb.tiles_down, fb.tiles_across)
+    gathered = []
+    for b in range(band_count):
+        s = GpuSplatter(g, fb, device=0, band_index=b, band_count=band_count, band_interleaved=True)
+        s.set_view_wire(view)
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        s.execute()
+        rows = fb.interleaved_tile_rows(band_count, b)
+        assert s.stats()["band_stride"] == band_count
+        assert_same_bits(s.get_rgba(), gdist.extract_band(rgba, fb, band_count, b, True), f"band {b} rgba")
+        band_bgr = s.get_frame_buffer()
+        np.testing.assert_array_equal(band_bgr, gdist.extract_band(bgr, fb, band_count, b, True))
+        np.testing.assert_array_equal(s.get_histogram(), hist[rows].reshape(-1))
+        gathered.append(gdist.pad_band(band_bgr, fb, band_count))
+        s.close()
+    np.testing.assert_array_equal(gdist.assemble(np.stack(gathered), fb, band_count, interleaved=True), bgr)
+
+
 @pytest.mark.parametrize("band_count", [2, 3, 8])
 def test_row_bands_union_equals_full_frame(pc12, band_count):
     """The multi-GPU decomposition: each band renders its tile rows; every band
