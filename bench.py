@@ -37,6 +37,10 @@ def parse():
     ap.add_argument("--scale-div", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--sh-degree", type=int, default=3)
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="frames in flight: independent renderers, each on its own stream "
+                    "(> 1 raises throughput; kernel durations then include the other frames' "
+                    "kernels, so the roofline is quoted at the default 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
@@ -92,19 +96,28 @@ def main():
     view, proj = camera.headless(bb, W, H)
     fb = TiledFramebuffer(W, H, TW, TW)
     # N > 1: interleaved tile-row bands (rank r owns rows r, r + N, ...), so
-    # every rank gets an equal share of the scene's dense centre rows
-    s = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=True,
-                    band_interleaved=world > 1)
-    s.set_view_wire(view)
-    s.set_projection_wire(proj)
-    s.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
-    stream = torch.cuda.current_stream()
-    s.set_stream(stream.cuda_stream)
+    # every rank gets an equal share of the scene's dense centre rows.
+    # F frames in flight: F renderers (own buffers, own stream) take frames
+    # round-robin, so one frame's latency-bound kernels (scans, list tails)
+    # overlap the next frame's work.  Every frame is rendered in full.
+    F = max(1, a.inflight)
+    R, streams = [], []
+    for f in range(F):
+        r = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=(f == 0),
+                        band_interleaved=world > 1)
+        r.set_view_wire(view)
+        r.set_projection_wire(proj)
+        r.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
+        st = torch.cuda.Stream()
+        r.set_stream(st.cuda_stream)
+        R.append(r)
+        streams.append(st)
+    s = R[0]
 
-    # N > 1: frame k's band is copied out and all-gathered (RCCL) on a second
-    # stream while frame k+1 renders; two band / frame buffers alternate.
+    # N > 1: frame k's band is copied out and all-gathered (RCCL) on a comm
+    # stream while later frames render; one band / frame buffer per renderer.
     band_bytes = fb.rows_per_band_padded(world) * W * 3
-    nbuf = 2 if world > 1 else 0
+    nbuf = F if world > 1 else 0
     band = [torch.empty(band_bytes, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     frame = [torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     comm = torch.cuda.Stream() if world > 1 else None
@@ -113,23 +126,26 @@ def main():
     nframe = [0]
 
     def one_frame():
-        s.execute_async()
+        i = nframe[0] % F
+        r, st = R[i], streams[i]
+        r.execute_async()
         if world > 1:
-            i = nframe[0] % 2
-            stream.wait_event(ev_free[i])  # the gather of frame k-2 read band[i]
-            s.copy_bgr8_device(band[i].data_ptr(), band_bytes)
-            ev_copy[i].record(stream)
+            st.wait_event(ev_free[i])  # the gather of frame k-F read band[i]
+            r.copy_bgr8_device(band[i].data_ptr(), band_bytes)
+            ev_copy[i].record(st)
             with torch.cuda.stream(comm):
                 comm.wait_event(ev_copy[i])
                 dist.all_gather_into_tensor(frame[i], band[i])
                 ev_free[i].record(comm)
         nframe[0] += 1
 
-    # warm-up (the first blocking render sizes the pair buffer)
-    s.execute()
+    # warm-up (the first blocking render sizes the pair buffers)
+    for r in R:
+        r.execute()
     for _ in range(a.warmup):
         one_frame()
-    s.sync()
+    for r in R:
+        r.sync()
     torch.cuda.synchronize()
     s.reset_kernel_times()
     if world > 1:
@@ -142,7 +158,8 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    s.sync()  # raises on pair overflow
+    for r in R:
+        r.sync()  # raises on pair overflow
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -191,6 +208,15 @@ def main():
         "avg_launch_ms": dk["avg_ms"],
     }
 
+    # single-frame latency (one frame in flight, blocking), for reference
+    lat = []
+    for _ in range(10):
+        torch.cuda.synchronize()
+        tl = time.perf_counter()
+        R[-1].execute()
+        lat.append(time.perf_counter() - tl)
+    latency_ms = round(1e3 * sorted(lat)[len(lat) // 2], 4)
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O
@@ -223,6 +249,7 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "frame_latency_ms": latency_ms,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -233,6 +260,7 @@ def main():
                 "gaussians": a.n,
                 "resolution": [W, H],
                 "tile": [TW, TW],
+                "frames_in_flight": F,
                 "parallelism": f"row-band x{world}" + (" (interleaved tile rows) + RCCL all-gather" if world > 1 else ""),
             },
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "max_list", "n_tiles", "n_big_tiles")},
@@ -241,7 +269,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    s.close()
+    for r in R:
+        r.close()
     if world > 1:
         dist.destroy_process_group()
 
