@@ -445,7 +445,12 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
       vis += wvis[w];
       m = max(m, wmax[w]);
     }
+    // every counter of the frame is (re)set here: the chunked path needs no
+    // per-frame memset (colscan writes every tile_count)
     b.counters[0] = big_base;
+    b.counters[1] = 0;  // (unused)
+    b.counters[8] = 0;  // medium_next
+    for (int k = 10; k < 16; ++k) b.counters[k] = 0;
     b.counters[2] = vis;
     b.counters[7] = med_base;
     b.counters[9] = sml_base;
@@ -576,9 +581,6 @@ __device__ __forceinline__ void tile_segment(const FrameParams& fp, const Buffer
   L = en - st;
 }
 
-// Small and medium lists: bitonic network over the padded power-of-two list
-// in LDS (32 KB), 256 threads.  Keys are unique (the index is in the low
-// word), so the order is total and deterministic.
 // Register bitonic sort of E*64 keys held by one wave: element i = lane*E + e
 // (each lane owns E consecutive keys).  Strides < E compare two registers of
 // the same lane; strides >= E exchange register e with lane ^ (j / E)
@@ -736,16 +738,113 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
   }
 }
 
-// Small and medium lists in one launch.  Workgroups [0, n_medium) each sort
-// one medium list (512 < L <= 2048: 4 waves x E keys in registers, the strides
-// >= 64 E through LDS); the following workgroups give each of their waves one
-// small list (L <= 512, sorted in one wave's registers).  The long sorts have
-// the low workgroup ids, so they start first.  Keys are unique (the index is
-// in the low word), so the order is total and deterministic.
+// Large lists (> kSortLdsCap, clustered scenes): a block-wide stable LSD
+// radix sort (8 passes x 8 bits) over the tile's segment in global memory,
+// pairs <-> pairs_alt, by one NT-thread workgroup.  Ranking inside each
+// NT-key chunk: wave64 ballot multisplit (8 ballots give each lane the mask of
+// lanes holding the same digit), then a per-digit prefix over the waves.
+// Passes whose digit is the same for every key are skipped.
+template <int NT>
+__device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buffers& b, int t,
+                                                uint32_t* hist, uint32_t* base,
+                                                uint32_t (*wcnt)[256]) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  uint32_t s, L;
+  tile_segment(fp, b, t, s, L);
+  unsigned long long* src = b.pairs + s;
+  unsigned long long* dst = b.pairs_alt + s;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = pass * 8;
+    for (int k = tid; k < 256; k += NT) hist[k] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < L; i += NT) atomicAdd(&hist[(uint32_t)(src[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    const bool trivial = hist[(uint32_t)(src[0] >> shift) & 255u] == L;
+    if (trivial) {
+      __syncthreads();
+      continue;  // every key has the same digit: order unchanged
+    }
+    if (wave == 0) {  // exclusive scan of 256 bins, 4 per lane
+      uint32_t v[4], tot = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] = hist[lane * 4 + k];
+        tot += v[k];
+      }
+      uint32_t inc = tot;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+      }
+      uint32_t run = inc - tot;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        base[lane * 4 + k] = run;
+        run += v[k];
+      }
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < L; c0 += NT) {
+      const uint32_t i = c0 + tid;
+      const bool valid = i < L;
+      const unsigned long long key = valid ? src[i] : 0ull;
+      const uint32_t d = (uint32_t)(key >> shift) & 255u;
+      unsigned long long m = __ballot(valid);
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const bool set = (d >> bit) & 1u;
+        const unsigned long long bb = __ballot(set);
+        m &= set ? bb : ~bb;
+      }
+      const uint32_t rank = (uint32_t)__popcll(m & lt_mask);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wcnt[wave][lane * 4 + k] = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(m);
+      __syncthreads();
+      uint32_t chunk_tot = 0;
+      for (int k = tid; k < 256; k += NT) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const uint32_t c = wcnt[w][k];
+          wcnt[w][k] = run;
+          run += c;
+        }
+        chunk_tot = run;  // NT >= 256: one digit per thread
+      }
+      __syncthreads();
+      if (valid) dst[base[d] + wcnt[wave][d] + rank] = key;
+      __syncthreads();
+      if (tid < 256) base[tid] += chunk_tot;
+      __syncthreads();
+    }
+    unsigned long long* tmp = src;
+    src = dst;
+    dst = tmp;
+  }
+  for (uint32_t i = tid; i < L; i += NT) b.list[s + i] = b.inv_perm[(uint32_t)src[i]];
+}
+
+// Big, medium and small lists in one launch, longest first: workgroups
+// [0, n_big) radix-sort one big list each (> kSortLdsCap); the next n_medium
+// each sort one medium list (512 < L <= 2048: 4 waves x E keys in registers,
+// the strides >= 64 E through LDS); the rest give each of their waves one
+// small list (L <= 512, sorted in one wave's registers).  Keys are unique (the
+// input index is in the low word), so the order is total and deterministic.
 __global__ __launch_bounds__(256) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
   __shared__ unsigned long long keys[kSortLdsCap];
+  __shared__ uint32_t r_hist[256], r_base[256], r_wcnt[4][256];
+  const uint32_t n_big = b.counters[0];
+  if (blockIdx.x < n_big) {  // the longest lists first
+    radix_sort_tile<256>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
+    return;
+  }
   const uint32_t n_med = b.counters[7], n_small = b.counters[9];
-  const uint32_t item = blockIdx.x;
+  const uint32_t item = blockIdx.x - n_big;
   if (item < n_med) {
     uint32_t s, L;
     tile_segment(fp, b, (int)b.medium_tiles[item], s, L);
@@ -769,106 +868,6 @@ __global__ __launch_bounds__(256) void gs_sort_tiles_kernel(FrameParams fp, Buff
     wave_sort_tile<4>(b, s, L, lane);
   else
     wave_sort_tile<8>(b, s, L, lane);
-}
-
-// Large lists: a block-wide stable LSD radix sort (8 passes x 8 bits) over the
-// tile's segment in global memory, pairs <-> pairs_alt.  Ranking inside each
-// 1024-key chunk: wave64 ballot multisplit (8 ballots give each lane the mask
-// of lanes holding the same digit), then a per-digit prefix over the 16 waves.
-// Workgroups pull big tiles from a counter until none is left.
-__global__ __launch_bounds__(1024) void gs_sort_big_kernel(FrameParams fp, Buffers b) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t wcnt[16][256];
-  __shared__ uint32_t s_item;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  const uint32_t n_big = b.counters[0];
-  for (;;) {
-    if (tid == 0) s_item = atomicAdd(&b.counters[1], 1u);
-    __syncthreads();
-    const uint32_t item = s_item;
-    __syncthreads();
-    if (item >= n_big) break;
-    const int t = (int)b.big_tiles[item];
-    uint32_t s, L;
-    tile_segment(fp, b, t, s, L);
-    unsigned long long* src = b.pairs + s;
-    unsigned long long* dst = b.pairs_alt + s;
-    for (int pass = 0; pass < 8; ++pass) {
-      const int shift = pass * 8;
-      if (tid < 256) hist[tid] = 0;
-      __syncthreads();
-      for (uint32_t i = tid; i < L; i += 1024) atomicAdd(&hist[(uint32_t)(src[i] >> shift) & 255u], 1u);
-      __syncthreads();
-      const bool trivial = hist[(uint32_t)(src[0] >> shift) & 255u] == L;
-      if (trivial) {
-        __syncthreads();
-        continue;  // every key has the same digit: order unchanged
-      }
-      if (wave == 0) {  // exclusive scan of 256 bins, 4 per lane
-        uint32_t v[4], tot = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v[k] = hist[lane * 4 + k];
-          tot += v[k];
-        }
-        uint32_t inc = tot;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t o = __shfl_up(inc, d, 64);
-          if (lane >= d) inc += o;
-        }
-        uint32_t run = inc - tot;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          base[lane * 4 + k] = run;
-          run += v[k];
-        }
-      }
-      __syncthreads();
-      for (uint32_t c0 = 0; c0 < L; c0 += 1024) {
-        const uint32_t i = c0 + tid;
-        const bool valid = i < L;
-        const unsigned long long key = valid ? src[i] : 0ull;
-        const uint32_t d = (uint32_t)(key >> shift) & 255u;
-        unsigned long long m = __ballot(valid);
-#pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-          const bool set = (d >> bit) & 1u;
-          const unsigned long long bb = __ballot(set);
-          m &= set ? bb : ~bb;
-        }
-        const uint32_t rank = (uint32_t)__popcll(m & lt_mask);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) wcnt[wave][lane * 4 + k] = 0;
-        __builtin_amdgcn_wave_barrier();
-        if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t chunk_tot = 0;
-        if (tid < 256) {
-          uint32_t run = 0;
-#pragma unroll
-          for (int w = 0; w < 16; ++w) {
-            const uint32_t c = wcnt[w][tid];
-            wcnt[w][tid] = run;
-            run += c;
-          }
-          chunk_tot = run;
-        }
-        __syncthreads();
-        if (valid) dst[base[d] + wcnt[wave][d] + rank] = key;
-        __syncthreads();
-        if (tid < 256) base[tid] += chunk_tot;
-        __syncthreads();
-      }
-      unsigned long long* tmp = src;
-      src = dst;
-      dst = tmp;
-    }
-    for (uint32_t i = tid; i < L; i += 1024) b.list[s + i] = b.inv_perm[(uint32_t)src[i]];
-    __syncthreads();
-  }
 }
 
 // -------------------------------------------------------------------- blend
@@ -1003,7 +1002,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   // the wave's first quad (tile-local pixel coordinates) and quad count
   int q_x, q_y, nq_wave;
   const int qw = (fp.tile_w + 1) >> 1;
-  if (bqw) {
+  if constexpr (BQW != 0) {
     const int bpr = fp.tile_w / (2 * bqw);
     q_x = (chunk % bpr) * (2 * bqw);
     q_y = (chunk / bpr) * (32 / bqw);
@@ -1017,7 +1016,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   }
   // this lane's pixel
   int lqx, lqy;
-  if (bqw) {
+  if constexpr (BQW != 0) {
     lqx = q_x + ((myq % bqw) << 1);
     lqy = q_y + ((myq / bqw) << 1);
   } else {
@@ -1194,8 +1193,8 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
+  // big + medium + ceil(small / 4) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
-  gs_sort_big_kernel<<<64, 1024, 0, s>>>(fp, b);
 }
 
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {

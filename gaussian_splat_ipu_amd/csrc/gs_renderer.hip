@@ -252,7 +252,10 @@ int enqueue_frame(gs_renderer* r) {
     int rc = profile_harvest(r, *slot);
     if (rc != GS_OK) return rc;
   }
-  GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, s));
+  // counters + tile_count: the chunked path rewrites all of them (colscan,
+  // scan); the global-atomic path accumulates tile_count and needs zeros
+  if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
+    GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, s));
   if (slot) GS_HIP(hipEventRecord(slot->ev[0], s));
   gsk::launch_project(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[1], s));
