@@ -104,7 +104,7 @@ def main():
     R, streams = [], []
     for f in range(F):
         r = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=(f == 0),
-                        band_interleaved=world > 1)
+                        band_interleaved=world > 1, band_cull=world > 1)
         r.set_view_wire(view)
         r.set_projection_wire(proj)
         r.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)

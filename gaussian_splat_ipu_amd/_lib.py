@@ -20,6 +20,7 @@ GS_FLAG_PROFILE = 2
 GS_FLAG_BIN_GLOBAL = 4
 GS_FLAG_INPUT_ORDER = 8
 GS_FLAG_BAND_INTERLEAVED = 16
+GS_FLAG_BAND_CULL = 32
 GS_LAYOUT_ROW_MAJOR = 0
 GS_LAYOUT_REF_TILE_MAJOR = 1
 GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_COUNT = range(6)

@@ -200,15 +200,69 @@ __device__ __forceinline__ void alpha_footprint(float mx, float my, float k0, fl
 }
 
 // ------------------------------------------------------------------ project
+// The band rows [yb0, yb1] (band-local) among absolute tile rows [fy0, fy1]
+// (clamped to the frame); empty when yb0 > yb1.
+__device__ __forceinline__ void band_rows_of(const FrameParams& fp, float fy0, float fy1, int& yb0,
+                                             int& yb1) {
+  const float gy1 = (float)(fp.tiles_y - 1);
+  if (fy0 < 0.0f) fy0 = 0.0f;
+  if (fy1 > gy1) fy1 = gy1;
+  yb0 = 0;
+  yb1 = -1;
+  if (fy0 <= fy1) {
+    const int a0 = (int)fy0 - fp.band_ty0, a1 = (int)fy1 - fp.band_ty0, S = fp.band_stride;
+    yb0 = a0 <= 0 ? 0 : (a0 + S - 1) / S;
+    yb1 = a1 < 0 ? -1 : min(a1 / S, fp.band_nrows - 1);
+  }
+}
+
+// GS_FLAG_BAND_CULL: true when Gaussian i provably has no tile row in this
+// band, from an upper bound on its eigen radius that needs only the mean and
+// the scales.  With C the 3D covariance and T the clip-space Jacobian
+// product (ComputeCov2D), the radius is ceil(3 sqrt(l1)) with
+//   l1 <= max(a, c) + sqrt(ac) + 0.32 <= 2 (cov00 + cov11) + 0.92,
+//   cov00 + cov11 <= lambda_max(C) ||T||_F^2 <= max_i exp(s_i)^2 ||W||_F^2 ||J||_F^2,
+//   ||J||_F^2 <= (fx^2 (1 + limx^2) + fy^2 (1 + limy^2)) / tz^2   (tx, ty clamped).
+// The bound is inflated by 5 % + 2 px against fp32 rounding, and the tile-row
+// range is computed with the rectangle's own (monotone) formulas, so it
+// contains the true rows.  Non-finite inputs never cull.
+__device__ __forceinline__ bool band_culled(const FrameParams& fp, float4 mean, float4 sg) {
+  const float* m = fp.mvp;
+  const float cy = mv_row(m, 1, mean.x, mean.y, mean.z, mean.w);
+  const float cw = mv_row(m, 3, mean.x, mean.y, mean.z, mean.w);
+  const float tz = mv_row(m, 2, mean.x, mean.y, mean.z, 1.0f);
+  float vy = cy * (0.5f / cw);
+  vy = vy + 0.5f;
+  vy = vy * fp.H;
+  const float smax = fmaxf(fmaxf(sg.x, sg.y), sg.z) / fp.scale_div;
+  const float lim = 1.3f * fp.tanfov;
+  const float j2 = (fp.focal_x * fp.focal_x + fp.focal_y * fp.focal_y) * (1.0f + lim * lim) / (tz * tz);
+  const float lc = __expf(2.0f * smax) * 1.01f;
+  const float r = 3.0f * __builtin_sqrtf(1.05f * (2.0f * lc * fp.wnorm2 * j2) + 1.0f) + 2.0f;
+  if (!(__builtin_fabsf(vy) < 1e30f) || !(r < 1e30f) || !(__builtin_fabsf(tz) > 1e-30f))
+    return false;
+  const float fy0 = __builtin_floorf(__builtin_floorf(vy - r) / fp.th);
+  const float fy1 = __builtin_floorf(__builtin_ceilf(vy + r) / fp.th);
+  int yb0, yb1;
+  band_rows_of(fp, fy0, fy1, yb0, yb1);
+  return yb0 > yb1;
+}
+
 __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i) {
   bool rendered = false;
   const float4 mean = b.mean[i];
-  const float4 col = b.colour[i];
-  const float4 rot = b.rot[i];
   const float4 sg = b.scale_gid[i];
   float4* rec = b.rec + 4 * (size_t)i;  // 64-B record
   uint2 rect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
+  const bool culled = fp.band_cull && !(sg.w <= 0.0f) && band_culled(fp, mean, sg);
+  if (culled) {  // no tile row in this band: empty rectangle, nothing else used
+    b.rect[i] = rect;
+    b.depth_key[i] = dkey;
+    return false;
+  }
+  const float4 col = b.colour[i];
+  const float4 rot = b.rot[i];
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
     const float* m = fp.mvp;
     // clip = mvp * mean (codelets.cpp:460)
@@ -291,18 +345,12 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       float fx1 = __builtin_floorf(__builtin_ceilf(maxx) / fp.tw);
       float fy0 = __builtin_floorf(__builtin_floorf(miny) / fp.th);
       float fy1 = __builtin_floorf(__builtin_ceilf(maxy) / fp.th);
-      const float gx1 = (float)(fp.tiles_x - 1), gy1 = (float)(fp.tiles_y - 1);
+      const float gx1 = (float)(fp.tiles_x - 1);
       if (fx0 < 0.0f) fx0 = 0.0f;
       if (fx1 > gx1) fx1 = gx1;
-      if (fy0 < 0.0f) fy0 = 0.0f;
-      if (fy1 > gy1) fy1 = gy1;
       // this band's rows among the absolute rows [fy0, fy1]
-      int yb0 = 0, yb1 = -1;
-      if (fy0 <= fy1) {
-        const int a0 = (int)fy0 - fp.band_ty0, a1 = (int)fy1 - fp.band_ty0, S = fp.band_stride;
-        yb0 = a0 <= 0 ? 0 : (a0 + S - 1) / S;
-        yb1 = a1 < 0 ? -1 : min(a1 / S, fp.band_nrows - 1);
-      }
+      int yb0, yb1;
+      band_rows_of(fp, fy0, fy1, yb0, yb1);
       if (fx0 <= fx1 && yb0 <= yb1) {
         const uint32_t x0 = (uint32_t)(int)fx0, x1 = (uint32_t)(int)fx1;
         const uint32_t y0 = (uint32_t)yb0, y1 = (uint32_t)yb1;

@@ -209,6 +209,13 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.band_nrows = r->band_nrows;
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
+  fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
+  {
+    double w2 = 0.0;  // squared Frobenius norm of the upper 3x3 of the mvp, rounded up
+    for (int c = 0; c < 3; ++c)
+      for (int rr = 0; rr < 3; ++rr) w2 += (double)fp.mvp[c * 4 + rr] * (double)fp.mvp[c * 4 + rr];
+    fp.wnorm2 = (float)(w2 * 1.0001);
+  }
   fp.n = (int)r->n;
   fp.n_tiles = r->n_tiles;
   // blend: one wave per 16 pixel quads -- an 8x8 or 16x4 pixel block when the
@@ -697,6 +704,14 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
   if ((rc = finish_frame(r)) != GS_OK) return rc;
   std::vector<float> rec(r->n * 16);
   std::vector<uint32_t> rect(r->n * 2);
+  if (r->n && (r->cfg.flags & GS_FLAG_BAND_CULL)) {
+    // the frame skipped band-culled Gaussians: project all of them again
+    gsk::FrameParams fp = make_params(r);
+    fp.band_cull = 0;
+    gsk::launch_project(fp, r->buf, r->stream);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipStreamSynchronize(r->stream));
+  }
   if (r->n) {
     GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 64, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(rect.data(), r->buf.rect, r->n * 8, hipMemcpyDeviceToHost));

@@ -21,6 +21,7 @@ import numpy as np
 
 from . import camera
 from ._lib import (
+    GS_FLAG_BAND_CULL,
     GS_FLAG_BAND_INTERLEAVED,
     GS_FLAG_BIN_GLOBAL,
     GS_FLAG_INPUT_ORDER,
@@ -64,6 +65,7 @@ class GpuSplatter:
         bin_global: bool = False,
         input_order: bool = False,
         band_interleaved: bool = False,
+        band_cull: bool = False,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -87,6 +89,7 @@ class GpuSplatter:
             | (GS_FLAG_BIN_GLOBAL if bin_global else 0)
             | (GS_FLAG_INPUT_ORDER if input_order else 0)
             | (GS_FLAG_BAND_INTERLEAVED if band_interleaved else 0)
+            | (GS_FLAG_BAND_CULL if band_cull else 0)
         )
         self.cfg = cfg
         h = C.c_void_p()

@@ -76,6 +76,11 @@ typedef struct gs_config {
 #define GS_FLAG_BAND_INTERLEAVED 16u /* band = tile rows band_index,
                                   band_index + band_count, ...: every band gets
                                   an equal share of a scene's dense rows */
+#define GS_FLAG_BAND_CULL 32u  /* skip the full projection of Gaussians whose
+                                  conservative screen extent misses every row
+                                  of this band (frames, lists and histograms
+                                  are unchanged; n_rendered then counts only
+                                  the Gaussians that reach the band) */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */

@@ -231,6 +231,64 @@ def test_edge_cases(built):
     assert not s.get_frame_buffer().any()
 
 
+def _band_render(g, view, proj, fb, scale_div, band_index, band_count, interleaved, cull):
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+
+    s = GpuSplatter(g, fb, device=0, band_index=band_index, band_count=band_count,
+                    band_interleaved=interleaved, band_cull=cull)
+    s.set_view_wire(view)
+    s.set_projection_wire(proj)
+    s.update_focal_lengths(camera.FOV_DEFAULT, scale_div)
+    s.execute()
+    return s
+
+
+@pytest.mark.parametrize("interleaved", [False, True])
+def test_band_cull_changes_nothing(pc12, interleaved):
+    """GS_FLAG_BAND_CULL skips the projection of Gaussians whose conservative
+    extent misses the band.  Every band's frame, RGBA, lists and histogram must
+    equal the unculled band's, on point_cloud_12 and on the edge-case scene
+    (non-finite, behind-camera, huge, degenerate Gaussians); the projection
+    readback must still cover every Gaussian."""
+    from gaussian_splat_ipu_amd import camera, scene
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    ge, bbe = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=5000, seed=3, sh_degree=0)))
+    a = np.ascontiguousarray(ge).view(np.float32).reshape(-1, 16).copy()
+    a[50:100, 15] = -3.0
+    a[100:150, 0:3] = [0.0, 0.0, 40.0]
+    a[150:200, 12:15] = 30.0
+    a[250:300, 12:15] = -200.0
+    a[300:310, 0] = np.nan
+    a[310:320, 0] = np.inf
+    a[320:370, 0] = 30.0
+    g, bb = pc12
+    for scn, box, W, H, sd in [(g, bb, 1920, 1080, 1.0), (g, bb, 1280, 720, 0.1), (a, bbe, 800, 600, 1.0)]:
+        view, proj = camera.headless(box, W, H)
+        fb = TiledFramebuffer(W, H, 16, 16)
+        culled_any = False
+        for bc in (3, 8):
+            for bi in range(bc):
+                ref = _band_render(scn, view, proj, fb, sd, bi, bc, interleaved, False)
+                cul = _band_render(scn, view, proj, fb, sd, bi, bc, interleaved, True)
+                assert_same_bits(cul.get_rgba(), ref.get_rgba(), f"band {bi}/{bc} rgba")
+                np.testing.assert_array_equal(cul.get_frame_buffer(), ref.get_frame_buffer())
+                np.testing.assert_array_equal(cul.get_histogram(), ref.get_histogram())
+                t1, l1 = cul.get_bins()
+                t2, l2 = ref.get_bins()
+                np.testing.assert_array_equal(t1, t2)
+                np.testing.assert_array_equal(l1, l2)
+                assert cul.stats()["n_pairs"] == ref.stats()["n_pairs"]
+                assert cul.stats()["n_rendered"] <= ref.stats()["n_rendered"]
+                culled_any |= cul.stats()["n_rendered"] < ref.stats()["n_rendered"]
+                if bi == 0:
+                    assert_same_bits(cul.get_projected(), ref.get_projected(), "projection readback")
+                cul.close()
+                ref.close()
+        assert culled_any
+
+
 @pytest.mark.parametrize("tw,th", [(16, 16), (32, 20)])
 def test_blend_culling_is_decision_preserving(built, tw, th):
     """Stress the blend's footprint culling (pcut + wave boxes): strongly
