@@ -216,31 +216,27 @@ __device__ __forceinline__ void band_rows_of(const FrameParams& fp, float fy0, f
   }
 }
 
-// GS_FLAG_BAND_CULL: true when Gaussian i provably has no tile row in this
-// band, from an upper bound on its eigen radius that needs only the mean and
-// the scales.  With C the 3D covariance and T the clip-space Jacobian
-// product (ComputeCov2D), the radius is ceil(3 sqrt(l1)) with
-//   l1 <= max(a, c) + sqrt(ac) + 0.32 <= 2 (cov00 + cov11) + 0.92,
-//   cov00 + cov11 <= lambda_max(C) ||T||_F^2 <= max_i exp(s_i)^2 ||W||_F^2 ||J||_F^2,
-//   ||J||_F^2 <= (fx^2 (1 + limx^2) + fy^2 (1 + limy^2)) / tz^2   (tx, ty clamped).
+// GS_FLAG_BAND_CULL: true when a Gaussian provably has no tile row in this
+// band, from an upper bound on its eigen radius that needs only the mean, the
+// scales and T (the clip-space Jacobian product of ComputeCov2D, computed by
+// the same code as the full projection).  With C the 3D covariance:
+//   radius = ceil(3 sqrt(l1)),  l1 <= max(a, c) + sqrt(ac) + 0.32
+//                                  <= 2 (cov00 + cov11) + 0.92,
+//   cov00 + cov11 <= trace(T^T C T) <= lambda_max(C) ||T||_F^2,
+//   lambda_max(C) = max_i exp(s_i / fxy[1])^2   (R orthonormal).
 // The bound is inflated by 5 % + 2 px against fp32 rounding, and the tile-row
-// range is computed with the rectangle's own (monotone) formulas, so it
-// contains the true rows.  Non-finite inputs never cull.
-__device__ __forceinline__ bool band_culled(const FrameParams& fp, float4 mean, float4 sg) {
-  const float* m = fp.mvp;
-  const float cy = mv_row(m, 1, mean.x, mean.y, mean.z, mean.w);
-  const float cw = mv_row(m, 3, mean.x, mean.y, mean.z, mean.w);
-  const float tz = mv_row(m, 2, mean.x, mean.y, mean.z, 1.0f);
-  float vy = cy * (0.5f / cw);
-  vy = vy + 0.5f;
-  vy = vy * fp.H;
+// range is computed with the rectangle's own (monotone) formulas from the same
+// vy, so it contains the true rows.  Non-finite values never cull.
+__device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, const M3& T, float4 sg) {
+  float t2 = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) t2 += T.m[c][r] * T.m[c][r];
   const float smax = fmaxf(fmaxf(sg.x, sg.y), sg.z) / fp.scale_div;
-  const float lim = 1.3f * fp.tanfov;
-  const float j2 = (fp.focal_x * fp.focal_x + fp.focal_y * fp.focal_y) * (1.0f + lim * lim) / (tz * tz);
   const float lc = __expf(2.0f * smax) * 1.01f;
-  const float r = 3.0f * __builtin_sqrtf(1.05f * (2.0f * lc * fp.wnorm2 * j2) + 1.0f) + 2.0f;
-  if (!(__builtin_fabsf(vy) < 1e30f) || !(r < 1e30f) || !(__builtin_fabsf(tz) > 1e-30f))
-    return false;
+  const float r = 3.0f * __builtin_sqrtf(1.05f * (2.0f * lc * t2) + 1.0f) + 2.0f;
+  if (!(__builtin_fabsf(vy) < 1e30f) || !(r < 1e30f)) return false;
   const float fy0 = __builtin_floorf(__builtin_floorf(vy - r) / fp.th);
   const float fy1 = __builtin_floorf(__builtin_ceilf(vy + r) / fp.th);
   int yb0, yb1;
@@ -255,14 +251,6 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   float4* rec = b.rec + 4 * (size_t)i;  // 64-B record
   uint2 rect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
-  const bool culled = fp.band_cull && !(sg.w <= 0.0f) && band_culled(fp, mean, sg);
-  if (culled) {  // no tile row in this band: empty rectangle, nothing else used
-    b.rect[i] = rect;
-    b.depth_key[i] = dkey;
-    return false;
-  }
-  const float4 col = b.colour[i];
-  const float4 rot = b.rot[i];
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
     const float* m = fp.mvp;
     // clip = mvp * mean (codelets.cpp:460)
@@ -305,6 +293,14 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
 #pragma unroll
       for (int r = 0; r < 3; ++r) W.m[c][r] = m[c * 4 + r];
     const M3 T = m3_mul(W, J);
+    if (fp.band_cull && band_culled(fp, vy, T, sg)) {
+      // no tile row in this band: empty rectangle; the record is never read
+      b.rect[i] = rect;
+      b.depth_key[i] = dkey;
+      return false;
+    }
+    const float4 col = b.colour[i];
+    const float4 rot = b.rot[i];
     const M3 C3 = cov3d(rot, sg.x / fp.scale_div, sg.y / fp.scale_div, sg.z / fp.scale_div);
     M3 cov = m3_mul(m3_mul(m3_t(T), m3_t(C3)), T);
     const float a = cov.m[0][0] + 0.3f;
@@ -360,11 +356,10 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
             for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&b.tile_count[y * fp.tiles_x + x], 1u);
       }
     }
-  } else {
+  } else {  // empty slot: never binned; a neutral record for the readback
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    rec[1] = make_float4(0.0f, __builtin_huge_valf(), col.x, col.y);
-    rec[2] = make_float4(col.z, 0.0f, __uint_as_float(kEmptyBox),
-                         __uint_as_float(kEmptyBox));
+    rec[1] = make_float4(0.0f, __builtin_huge_valf(), 0.0f, 0.0f);
+    rec[2] = make_float4(0.0f, 0.0f, __uint_as_float(kEmptyBox), __uint_as_float(kEmptyBox));
     rec[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
   b.rect[i] = rect;
