@@ -570,6 +570,123 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
     }
     if (wave == 15) b.tile_count[t] = run;
   }
+  if (wave == 15) {  // this workgroup's 64 tiles, summarised for gs_scan_multi_kernel
+    const bool ok = t < T;
+    const uint32_t L = ok ? run : 0u;
+    unsigned long long sum = L;
+    uint32_t mx = L;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      sum += __shfl_xor(sum, d, 64);
+      mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+    }
+    const int cl = sort_class(L);
+    const uint32_t ns = (uint32_t)__popcll(__ballot(ok && cl == 0));
+    const uint32_t nm = (uint32_t)__popcll(__ballot(ok && cl == 1));
+    const uint32_t nb = (uint32_t)__popcll(__ballot(ok && cl == 2));
+    if (lane == 0)
+      b.tile_agg[blockIdx.x] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), ns | (nm << 8) | (nb << 16), mx);
+  }
+}
+
+// Chunked path: tile starts and sort queues from the colscan's per-64-tile
+// summaries.  One workgroup per 64 tiles: it scans the summaries of the
+// workgroups before it (all of them are in memory already, no chaining),
+// then its 64 tiles in one wave.  Workgroup 0 also writes the frame counters.
+__global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long s_sum[2][4];
+  __shared__ uint32_t s_q[2][4][3], s_mx[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x, G = gridDim.x, T = fp.n_tiles;
+  unsigned long long ps = 0, ts = 0;
+  uint32_t pq[3] = {0, 0, 0}, tq[3] = {0, 0, 0}, mx = 0;
+  for (int i = tid; i < G; i += 256) {
+    const uint4 a = b.tile_agg[i];
+    const unsigned long long sm = (unsigned long long)a.x | ((unsigned long long)a.y << 32);
+    const uint32_t q[3] = {a.z & 255u, (a.z >> 8) & 255u, (a.z >> 16) & 255u};
+    ts += sm;
+    if (i < g) ps += sm;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      tq[k] += q[k];
+      if (i < g) pq[k] += q[k];
+    }
+    mx = max(mx, a.w);
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    ps += __shfl_xor(ps, d, 64);
+    ts += __shfl_xor(ts, d, 64);
+    mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      pq[k] += __shfl_xor(pq[k], d, 64);
+      tq[k] += __shfl_xor(tq[k], d, 64);
+    }
+  }
+  if (lane == 0) {
+    s_sum[0][wave] = ps;
+    s_sum[1][wave] = ts;
+    s_mx[wave] = mx;
+    for (int k = 0; k < 3; ++k) {
+      s_q[0][wave][k] = pq[k];
+      s_q[1][wave][k] = tq[k];
+    }
+  }
+  __syncthreads();
+  ps = s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3];
+  ts = s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3];
+  for (int k = 0; k < 3; ++k) {
+    pq[k] = s_q[0][0][k] + s_q[0][1][k] + s_q[0][2][k] + s_q[0][3][k];
+    tq[k] = s_q[1][0][k] + s_q[1][1][k] + s_q[1][2][k] + s_q[1][3][k];
+  }
+  mx = max(max(s_mx[0], s_mx[1]), max(s_mx[2], s_mx[3]));
+  if (wave == 0) {
+    const int t = g * 64 + lane;
+    const bool ok = t < T;
+    const uint32_t c = ok ? b.tile_count[t] : 0u;
+    unsigned long long inc = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    const unsigned long long start = ps + inc - c;
+    const int cl = sort_class(c);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned long long m0 = __ballot(ok && cl == 0), m1 = __ballot(ok && cl == 1),
+                             m2 = __ballot(ok && cl == 2);
+    if (ok) {
+      b.tile_start[t] = (uint32_t)(start < 0xFFFFFFFFull ? start : 0xFFFFFFFFull);
+      if (cl == 0) b.small_tiles[pq[0] + (uint32_t)__popcll(m0 & lt)] = (uint32_t)t;
+      if (cl == 1) b.medium_tiles[pq[1] + (uint32_t)__popcll(m1 & lt)] = (uint32_t)t;
+      if (cl == 2) b.big_tiles[pq[2] + (uint32_t)__popcll(m2 & lt)] = (uint32_t)t;
+    }
+  }
+  if (g == 0) {  // frame counters (every counter of the frame is reset here)
+    uint32_t vsum = 0;
+    const int nb = (fp.n + 255) / 256;
+    for (int i = tid; i < nb; i += 256) vsum += b.block_rendered[i];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
+    __syncthreads();
+    if (lane == 0) s_mx[wave] = vsum;
+    __syncthreads();
+    if (tid == 0) {
+      b.counters[0] = tq[2];
+      b.counters[1] = 0;
+      b.counters[2] = s_mx[0] + s_mx[1] + s_mx[2] + s_mx[3];
+      b.counters[3] = ts > fp.pair_cap ? 1u : 0u;
+      b.counters[4] = mx;
+      b.counters[5] = (uint32_t)ts;
+      b.counters[6] = (uint32_t)(ts >> 32);
+      b.counters[7] = tq[1];
+      b.counters[8] = 0;
+      b.counters[9] = tq[0];
+      for (int k = 10; k < 16; ++k) b.counters[k] = 0;
+      b.tile_start[T] = (uint32_t)(ts < 0xFFFFFFFFull ? ts : 0xFFFFFFFFull);
+    }
+  }
 }
 
 __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buffers b) {
@@ -1220,6 +1337,8 @@ void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     const size_t lds = bin_lds_bytes(fp.n_tiles);
     gs_count_kernel<<<fp.n_chunks, 1024, lds, s>>>(fp, b);
     gs_colscan_kernel<<<(fp.n_tiles + 63) / 64, 1024, 0, s>>>(fp, b);
+    gs_scan_multi_kernel<<<(fp.n_tiles + 63) / 64, 256, 0, s>>>(fp, b);
+    return;
   }
   gs_scan_kernel<<<1, 1024, 0, s>>>(fp, b);
 }

@@ -65,6 +65,8 @@ struct Buffers {
   uint32_t* medium_tiles;   // [n_tiles]  lists in (kSortRegCap, kSortLdsCap] (block sort queue)
   uint32_t* small_tiles;    // [n_tiles]  lists in [1, kSortRegCap] (one-wave sort queue)
   uint32_t* chunk_off;      // [n_chunks][n_tiles] chunk histograms -> offsets
+  uint4* tile_agg;          // [ceil(n_tiles / 64)] per 64 tiles: list-length sum (lo, hi),
+                            //   small | medium << 8 | big << 16 counts, max length
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
   uint32_t* counters;       // [16]: 0 n_big, 1 big_next, 2 n_rendered, 3 overflow,
                             //  4 max_list, 5 n_pairs (low), 6 n_pairs (high),

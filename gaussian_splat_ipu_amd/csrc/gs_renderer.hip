@@ -469,13 +469,15 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   if ((e = hipMalloc(&r->d_zero, r->zero_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(zero)"));
   r->buf.counters = (uint32_t*)r->d_zero;
   r->buf.tile_count = (uint32_t*)r->d_zero + 16;
-  if ((e = hipMalloc(&r->d_tiles, (T + 1 + 4 * T) * 4)) != hipSuccess)
+  const size_t n_agg = (T + 63) / 64;
+  if ((e = hipMalloc(&r->d_tiles, (T + 1 + 4 * T) * 4 + n_agg * 16 + 16)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(tiles)"));
   r->buf.tile_start = (uint32_t*)r->d_tiles;
   r->buf.tile_cursor = r->buf.tile_start + T + 1;
   r->buf.big_tiles = r->buf.tile_cursor + T;
   r->buf.medium_tiles = r->buf.big_tiles + T;
   r->buf.small_tiles = r->buf.medium_tiles + T;
+  r->buf.tile_agg = (uint4*)(((uintptr_t)(r->buf.small_tiles + T) + 15) & ~(uintptr_t)15);
   if ((e = hipMemset(r->d_tiles, 0, (T + 1 + 4 * T) * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(tiles)"));
 
