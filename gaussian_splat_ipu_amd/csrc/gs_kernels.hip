@@ -527,14 +527,24 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
   const int c = blockIdx.x;
   const int g0 = c * fp.chunk_size;
   const int g1 = min(fp.n, g0 + fp.chunk_size);
-  for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
-    const uint2 r = b.rect[i];
+  // Consecutive Gaussians (Morton order) often share their whole rectangle:
+  // the first lane of each run of equal rectangles adds the run length, so
+  // the LDS atomics on the same counters are not serialised lane by lane.
+  const int lane = threadIdx.x & 63;
+  for (int i0 = g0; i0 < g1; i0 += 1024) {
+    const int i = i0 + (int)threadIdx.x;
+    const uint2 r = i < g1 ? b.rect[i] : kEmptyRect;
+    const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
+    const bool start = lane == 0 || r.x != px || r.y != py;
+    const unsigned long long st = __ballot(start);
+    const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
+    const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
     const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
-    if (x0 > x1) continue;
+    if (!start || x0 > x1) continue;
     for (uint32_t y = y0; y <= y1; ++y)
       for (uint32_t x = x0; x <= x1; ++x) {
         const uint32_t t = y * fp.tiles_x + x;
-        atomicAdd(&cnt[t >> 1], 1u << ((t & 1u) * 16u));
+        atomicAdd(&cnt[t >> 1], len << ((t & 1u) * 16u));
       }
   }
   __syncthreads();
