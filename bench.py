@@ -57,6 +57,24 @@ STAGE_KERNELS = {
 }
 
 
+def measured_copy_peak(torch) -> float:
+    """Achievable HBM GB/s on this box: a 2 GiB device-to-device copy (read +
+    write bytes), best of 5 (SURVEY §8 d asks for it beside the spec peak)."""
+    n = 1 << 31
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    best = None
+    for _ in range(6):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dst.copy_(src)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None or dt < best else best
+    del src, dst
+    return round(2 * n / best / 1e9, 1)
+
+
 def alg_bytes(kernel: str, st: dict, n: int, px: int) -> float:
     """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md)."""
     T, P = st["n_tiles"], st["n_pairs"]
@@ -185,6 +203,7 @@ def main():
     # HBM bytes per launch of the same stage, from the committed PMC summary of
     # this workload (tools/profile.sh + tools/pmc_summary.py), when it matches
     pmc = None
+    valu = None
     if os.path.exists(a.pmc_json):
         try:
             pm = json.load(open(a.pmc_json))
@@ -192,6 +211,11 @@ def main():
             names = [k for k in STAGE_KERNELS[dom] if k in ks]
             if pm.get("config") == f"{a.n}@{W}x{H}/t{TW}/w{world}" and names:
                 pmc = int(sum(ks[k]["hbm_bytes_per_launch"] for k in names))
+                # VALU issue-slot fraction beside the HBM fraction (SURVEY §8 d):
+                # wave64 VALU instructions x 2 cycles over 1024 SIMDs x 2.4 GHz
+                vi = sum(ks[k].get("SQ_INSTS_VALU", 0.0) for k in names)
+                if vi:
+                    valu = round(vi * 2.0 / (1024 * 2.4e9 * kern[dom]["avg_ms"] * 1e-3), 3)
         except Exception:
             pmc = None
     dk = kern[dom]
@@ -206,6 +230,8 @@ def main():
         "traffic": pmc,
         "alg_bytes_per_launch": dk["alg_bytes"],
         "avg_launch_ms": dk["avg_ms"],
+        "valu_issue_frac": valu,
+        "peak_measured": measured_copy_peak(torch),
     }
 
     # single-frame latency (one frame in flight, blocking), for reference
@@ -236,6 +262,21 @@ def main():
             "sample": f"{a.cpu_frames} full frames of the same {a.n}-Gaussian {W}x{H} workload through the "
             f"CPU oracle Gaussian rasteriser (OpenMP, {threads} threads)",
             "gaussians_per_sec": round(a.n / tc, 1),
+        }
+        # the reference's own CPU path is a point splatter (cpu_rasteriser.cpp:
+        # 9-92), restated in the oracle: reported beside, not comparable
+        xyz = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16)[:, 0:3]
+        O.point_splat(xyz, view, proj, W, H, TW, TW, nthreads=threads)
+        tp0 = time.perf_counter()
+        for _ in range(5):
+            O.point_splat(xyz, view, proj, W, H, TW, TW, nthreads=threads)
+        tp = (time.perf_counter() - tp0) / 5
+        cpu["reference_cpu_path"] = {
+            "value": round(1.0 / tp, 2),
+            "unit": "frames/s",
+            "kind": "port",
+            "sample": f"5 frames of the reference's CPU point splatter (projectPoints + splatPoints + "
+            f"buildTileHistogram) on the same {a.n} points, {threads} threads",
         }
 
     if rank == 0:
