@@ -1078,7 +1078,7 @@ __device__ __forceinline__ float gs_expf_inrange(float x) {
   const float r2 = r * r;
   p = __builtin_fmaf(p, r2, r);
   p = p + 1.0f;
-  return p * __uint_as_float((uint32_t)((int)k + 127) << 23);
+  return __builtin_amdgcn_ldexpf(p, (int)k);  // == p * 2^k: k in [-115, 0], p in [0.7, 1.5]
 }
 
 // One staged record (48 B, see the project kernel):
@@ -1111,15 +1111,13 @@ __device__ __forceinline__ void blend_composite(Px& q, float power, float e, con
       ok && !q.done && !(power > 0.0f) && !(power < pcut) && !(alpha < 1.0f / 255.0f);
   const bool brk = hit && test_T < 0.0001f;  // break (codelets.cpp:406-408)
   const bool upd = hit && !brk;
-  const float n0 = q.c01.x + (r1.z * alpha) * q.T;  // colour += gCont * alpha * T
-  const float n1 = q.c01.y + (r1.w * alpha) * q.T;
-  const float n2 = q.c23.x + (r2.x * alpha) * q.T;
-  const float n3 = q.c23.y + (op * alpha) * q.T;
-  q.c01.x = upd ? n0 : q.c01.x;
-  q.c01.y = upd ? n1 : q.c01.y;
-  q.c23.x = upd ? n2 : q.c23.x;
-  q.c23.y = upd ? n3 : q.c23.y;
-  q.T = upd ? test_T : q.T;
+  if (__builtin_expect(upd, 0)) {
+    q.c01.x = q.c01.x + (r1.z * alpha) * q.T;  // colour += gCont * alpha * T
+    q.c01.y = q.c01.y + (r1.w * alpha) * q.T;
+    q.c23.x = q.c23.x + (r2.x * alpha) * q.T;
+    q.c23.y = q.c23.y + (op * alpha) * q.T;
+    q.T = test_T;
+  }
   q.done = q.done || brk;
 }
 
