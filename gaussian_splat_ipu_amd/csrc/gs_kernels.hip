@@ -702,12 +702,30 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
 __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buffers b) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
   const int T = fp.n_tiles;
-  lds_zero(cnt, (T + 1) >> 1);
-  __syncthreads();
   const int c = blockIdx.x;
   const int g0 = c * fp.chunk_size;
   const int g1 = min(fp.n, g0 + fp.chunk_size);
   const uint32_t* row = b.chunk_off + (size_t)c * T;
+  if (fp.emit_wide) {
+    // one u32 cursor per tile, seeded with the chunk's first slot of the
+    // tile: a single LDS atomic returns the pair's final position
+    for (int t = threadIdx.x; t < T; t += 1024) cnt[t] = b.tile_start[t] + row[t];
+    __syncthreads();
+    for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
+      const uint2 r = b.rect[i];
+      const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+      if (x0 > x1) continue;
+      const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
+      for (uint32_t y = y0; y <= y1; ++y)
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
+          if (pos < fp.pair_cap) b.pairs[pos] = key;
+        }
+    }
+    return;
+  }
+  lds_zero(cnt, (T + 1) >> 1);
+  __syncthreads();
   for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
     const uint2 r = b.rect[i];
     const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
@@ -1355,7 +1373,8 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
   if (!fp.bin_global) {
     if (fp.n_chunks > 0 && fp.n_tiles > 0)
-      gs_emit_chunk_kernel<<<fp.n_chunks, 1024, bin_lds_bytes(fp.n_tiles), s>>>(fp, b);
+      gs_emit_chunk_kernel<<<fp.n_chunks, 1024,
+                             fp.emit_wide ? (size_t)fp.n_tiles * 4 : bin_lds_bytes(fp.n_tiles), s>>>(fp, b);
     return;
   }
   gs_emit_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);

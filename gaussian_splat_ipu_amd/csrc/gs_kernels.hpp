@@ -37,6 +37,7 @@ struct FrameParams {
   int bin_global;     // 1: fallback binning with global atomics
   int chunk_size;     // Gaussians per binning chunk (<= 65535)
   int n_chunks;
+  int emit_wide;      // emit with one u32 LDS cursor per tile (n_tiles * 4 <= kBinLdsMax)
 };
 
 // Device workspace of one renderer.

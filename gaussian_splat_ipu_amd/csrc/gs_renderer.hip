@@ -231,6 +231,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.bin_global = r->bin_global;
   fp.chunk_size = r->chunk_size;
   fp.n_chunks = r->n_chunks;
+  fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
   return fp;
 }
 
