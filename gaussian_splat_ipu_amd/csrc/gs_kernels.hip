@@ -866,50 +866,6 @@ __device__ __forceinline__ void wave_bitonic(unsigned long long (&v)[E], int lan
   for (int k = 2; k <= n; k <<= 1) wave_merge<E>(v, lane, 0, k, k >> 1);
 }
 
-// W waves x 64 lanes x E keys = up to W*64*E keys per workgroup: every wave
-// sorts its slice in registers; the strides >= 64*E (3 of them for 2048 keys)
-// exchange through LDS between barriers.
-template <int E, int W>
-__device__ __forceinline__ void block_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
-                                                unsigned long long* lds) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  constexpr int WN = 64 * E;
-  const int ibase = wave * WN;
-  uint32_t n2 = WN;
-  while (n2 < L) n2 <<= 1;
-  unsigned long long v[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const uint32_t i = (uint32_t)(ibase + lane * E + e);
-    v[e] = i < L ? b.pairs[s + i] : ~0ull;
-  }
-  for (int k = 2; k <= (int)n2; k <<= 1) {
-    int j = k >> 1;
-    for (; j >= WN; j >>= 1) {  // cross-wave stage through LDS
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < E; ++e) lds[ibase + lane * E + e] = v[e];
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = ibase + lane * E + e;
-        const unsigned long long o = lds[i ^ j];
-        const bool asc = (i & k) == 0;
-        const bool take_min = ((i & j) == 0) == asc;
-        const bool gt = v[e] > o;
-        v[e] = (take_min == gt) ? o : v[e];
-      }
-    }
-    if (ibase < (int)n2) wave_merge<E>(v, lane, ibase, k, j);
-  }
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const uint32_t i = (uint32_t)(ibase + lane * E + e);
-    if (i < L) b.list[s + i] = b.inv_perm[(uint32_t)v[e]];
-  }
-}
-
 template <int E>
 __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uint32_t L, int lane) {
   unsigned long long v[E];
@@ -923,6 +879,85 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
   for (int e = 0; e < E; ++e) {
     const uint32_t i = (uint32_t)(lane * E + e);
     if (i < L) b.list[s + i] = b.inv_perm[(uint32_t)v[e]];
+  }
+}
+
+// Medium lists (kSortRegCap < L <= kSortLdsCap): the 4 waves sort 256-key
+// runs in registers (wave_bitonic<4>), then log2(runs) merge-path levels run
+// in LDS.  At every level each thread produces K = runs consecutive outputs:
+// a co-rank binary search finds where its first output comes from, then it
+// merges sequentially, holding the outputs in registers across the barrier
+// (the merge is in place).  The last level writes the list.  Work is
+// O(L log L) over L rounded up to 256, against O(L log^2 L) over L rounded up
+// to a power of two for a bitonic network.
+__device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
+                                                unsigned long long* lds) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int runs = (int)((L + 255u) >> 8);  // 3 .. 8 for medium lists
+  const int npad = runs << 8;
+  for (int r = wave; r < runs; r += 4) {
+    unsigned long long v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t i = (uint32_t)(r * 256 + lane * 4 + e);
+      v[e] = i < L ? b.pairs[s + i] : ~0ull;
+    }
+    wave_bitonic<4>(v, lane);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lds[r * 256 + lane * 4 + e] = v[e];
+  }
+  __syncthreads();
+  const int K = runs;
+  const int d0 = (int)threadIdx.x * K;
+  for (int w = 256;; w <<= 1) {  // runs == 1 degenerates to a copy
+    unsigned long long out[8];
+    int i = 0, j = 0, la = 0, lb = 0, abase = 0, bbase = 0;
+    unsigned long long av = 0ull, bv = 0ull;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < K) {
+        const int d = d0 + k;
+        if (k == 0 || (d & (2 * w - 1)) == 0) {  // (re)locate: first output or a new pair
+          abase = d & ~(2 * w - 1);
+          bbase = abase + w;
+          la = min(w, npad - abase);
+          lb = max(0, min(w, npad - bbase));
+          const int dd = d - abase;
+          int lo = max(0, dd - lb), hi = min(dd, la);
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (lds[abase + mid] <= lds[bbase + dd - 1 - mid]) lo = mid + 1;
+            else hi = mid;
+          }
+          i = lo;
+          j = dd - lo;
+          av = i < la ? lds[abase + i] : ~0ull;
+          bv = j < lb ? lds[bbase + j] : ~0ull;
+        }
+        const bool ta = j >= lb || (i < la && av <= bv);
+        out[k] = ta ? av : bv;
+        if (ta) {
+          ++i;
+          av = i < la ? lds[abase + i] : ~0ull;
+        } else {
+          ++j;
+          bv = j < lb ? lds[bbase + j] : ~0ull;
+        }
+      }
+    }
+    __syncthreads();
+    if (2 * w < npad) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < K) lds[d0 + k] = out[k];
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < K && d0 + k < (int)L) b.list[s + d0 + k] = b.inv_perm[(uint32_t)out[k]];
+      break;
+    }
   }
 }
 
@@ -1036,10 +1071,7 @@ __global__ __launch_bounds__(256) void gs_sort_tiles_kernel(FrameParams fp, Buff
   if (item < n_med) {
     uint32_t s, L;
     tile_segment(fp, b, (int)b.medium_tiles[item], s, L);
-    if (L <= 1024u)
-      block_sort_tile<4, 4>(b, s, L, keys);
-    else
-      block_sort_tile<8, 4>(b, s, L, keys);
+    merge_sort_tile(b, s, L, keys);
     return;
   }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
