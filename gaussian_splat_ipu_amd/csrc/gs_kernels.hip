@@ -790,18 +790,21 @@ __device__ __forceinline__ void reg_stage(unsigned long long (&v)[E], int i0, in
 }
 
 // Value of lane ^ lj (lj = 1 .. 32, wave-uniform) without an LDS round trip:
-// DPP quad_perm for 1 / 2, row_shl / row_shr for 4 / 8 (lane i reads i + n /
-// i - n inside its row of 16), v_permlane16_swap / v_permlane32_swap for 16 / 32.
+// DPP quad_perm for 1 / 2, bank-masked row_shl / row_shr for 4, row_ror for 8,
+// v_permlane16_swap / v_permlane32_swap for 16 / 32.
 template <int LJ>
 __device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x, int lane) {
   if constexpr (LJ == 1) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
   } else if constexpr (LJ == 2) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
-  } else if constexpr (LJ == 4 || LJ == 8) {
-    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x100 | LJ, 0xF, 0xF, false);
-    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x110 | LJ, 0xF, 0xF, false);
-    return (lane & LJ) ? dn : up;
+  } else if constexpr (LJ == 4) {
+    // row_shl:4 into banks 0 / 2 (lanes 0-3, 8-11 of a row), row_shr:4 into
+    // banks 1 / 3: two DPP moves, no select
+    const int up = __builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0x5, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(up, (int)x, 0x114, 0xF, 0xA, false);
+  } else if constexpr (LJ == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
   } else if constexpr (LJ == 16) {
     const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
     return (lane & 16) ? p[0] : p[1];
