@@ -131,6 +131,9 @@ def main():
         R.append(r)
         streams.append(st)
     s = R[0]
+    # stage events on every 8th frame: each event costs device time, so the
+    # throughput run samples (the averages still come from the timed frames)
+    s.set_profile_interval(8)
 
     # N > 1: frame k's band is copied out and all-gathered (RCCL) on a comm
     # stream while later frames render; one band / frame buffer per renderer.

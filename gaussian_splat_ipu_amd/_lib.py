@@ -140,6 +140,7 @@ _SIGS = {
     "gs_copy_bgr8_device": (C.c_int, [_P, _P, C.c_size_t]),
     "gs_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
     "gs_reset_kernel_times": (C.c_int, [_P]),
+    "gs_set_profile_interval": (C.c_int, [_P, C.c_uint32]),
     "gs_ply_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "gs_ply_save": (C.c_int, [_P, C.c_char_p]),
     "gs_ply_free": (None, [_P]),

@@ -603,6 +603,8 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
 // summaries.  One workgroup per 64 tiles: it scans the summaries of the
 // workgroups before it (all of them are in memory already, no chaining),
 // then its 64 tiles in one wave.  Workgroup 0 also writes the frame counters.
+// Counters and list lengths also go straight to the mapped host mirror, so a
+// frame needs no device-to-host copy.
 __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buffers b) {
   __shared__ unsigned long long s_sum[2][4];
   __shared__ uint32_t s_q[2][4][3], s_mx[4];
@@ -667,6 +669,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
     const unsigned long long m0 = __ballot(ok && cl == 0), m1 = __ballot(ok && cl == 1),
                              m2 = __ballot(ok && cl == 2);
     if (ok) {
+      b.host_counters[16 + t] = c;  // the histogram, straight to host memory
       b.tile_start[t] = (uint32_t)(start < 0xFFFFFFFFull ? start : 0xFFFFFFFFull);
       if (cl == 0) b.small_tiles[pq[0] + (uint32_t)__popcll(m0 & lt)] = (uint32_t)t;
       if (cl == 1) b.medium_tiles[pq[1] + (uint32_t)__popcll(m1 & lt)] = (uint32_t)t;
@@ -695,6 +698,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
       b.counters[9] = tq[0];
       for (int k = 10; k < 16; ++k) b.counters[k] = 0;
       b.tile_start[T] = (uint32_t)(ts < 0xFFFFFFFFull ? ts : 0xFFFFFFFFull);
+      for (int k = 0; k < 16; ++k) b.host_counters[k] = b.counters[k];
     }
   }
 }

@@ -67,7 +67,7 @@ struct gs_renderer {
   gsk::Buffers buf{};
 
   // host mirrors
-  uint32_t* h_counters = nullptr;  // pinned mirror of d_zero: counters[16] + tile_count[T]
+  uint32_t* h_counters = nullptr;  // mapped pinned mirror of d_zero: counters[16] + tile_count[T]
   std::vector<uint32_t> hist_snapshot;
   std::mutex hist_mu;
   bool frame_pending = false;
@@ -76,6 +76,8 @@ struct gs_renderer {
 
   // profiling
   bool profile = false;
+  uint32_t profile_every = 1;  // stage events on every n-th frame
+  uint64_t frame_seq = 0;
   ProfileSlot ring[kProfileRing];
   int ring_head = 0;
   double k_ms[GS_K_COUNT] = {0};
@@ -254,7 +256,7 @@ int enqueue_frame(gs_renderer* r) {
   const gsk::FrameParams fp = make_params(r);
   hipStream_t s = r->stream;
   ProfileSlot* slot = nullptr;
-  if (r->profile) {
+  if (r->profile && r->frame_seq++ % r->profile_every == 0) {
     slot = &r->ring[r->ring_head];
     r->ring_head = (r->ring_head + 1) % kProfileRing;
     int rc = profile_harvest(r, *slot);
@@ -279,9 +281,11 @@ int enqueue_frame(gs_renderer* r) {
     slot->pending = true;
   }
   GS_HIP(hipGetLastError());
-  // counters and per-tile list lengths are adjacent: one small D2H copy
-  GS_HIP(hipMemcpyAsync(r->h_counters, r->d_zero, (16 + (size_t)r->n_tiles) * 4,
-                        hipMemcpyDeviceToHost, s));
+  // the chunked scan writes the counters and list lengths into the mapped host
+  // mirror itself; the other paths copy them (adjacent: one small D2H copy)
+  if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
+    GS_HIP(hipMemcpyAsync(r->h_counters, r->d_zero, (16 + (size_t)r->n_tiles) * 4,
+                          hipMemcpyDeviceToHost, s));
   r->frame_pending = true;
   return GS_OK;
 }
@@ -511,9 +515,12 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   if ((e = hipMemset(r->d_out, 0, px * 16 + r->bgr_bytes)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(framebuffer)"));
 
-  if ((e = hipHostMalloc((void**)&r->h_counters, r->zero_bytes, hipHostMallocDefault)) != hipSuccess)
+  if ((e = hipHostMalloc((void**)&r->h_counters, r->zero_bytes,
+                         hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
     return fail(hip_fail(e, "hipHostMalloc"));
   std::memset(r->h_counters, 0, r->zero_bytes);
+  if ((e = hipHostGetDevicePointer((void**)&r->buf.host_counters, r->h_counters, 0)) != hipSuccess)
+    return fail(hip_fail(e, "hipHostGetDevicePointer"));
   r->hist_snapshot.assign((size_t)r->n_tiles, 0u);
   if (r->profile) {
     for (auto& s : r->ring)
@@ -768,6 +775,13 @@ int gs_kernel_times(gs_renderer* r, double* avg_ms, uint64_t* launches, int n) {
     avg_ms[k] = r->k_launches[k] ? r->k_ms[k] / (double)r->k_launches[k] : 0.0;
     if (launches) launches[k] = r->k_launches[k];
   }
+  return GS_OK;
+}
+
+int gs_set_profile_interval(gs_renderer* r, uint32_t every) {
+  if (!r || every == 0) return GS_EINVAL;
+  r->profile_every = every;
+  r->frame_seq = 0;
   return GS_OK;
 }
 

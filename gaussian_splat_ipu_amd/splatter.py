@@ -229,6 +229,10 @@ class GpuSplatter:
     def reset_kernel_times(self) -> None:
         check(lib().gs_reset_kernel_times(self._h))
 
+    def set_profile_interval(self, every: int) -> None:
+        """Stage events on every `every`-th frame only (each event costs device time)."""
+        check(lib().gs_set_profile_interval(self._h, every))
+
     # reference-spelled aliases (ipu_rasteriser.hpp:20-55)
     updateModelView = update_model_view
     updateProjection = update_projection

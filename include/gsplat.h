@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 2
+#define GSPLAT_ABI_VERSION 3
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -184,6 +184,9 @@ int gs_copy_bgr8_device(gs_renderer* r, void* dst_dev, size_t bytes);
  * frames since the last reset (requires GS_FLAG_PROFILE). */
 int gs_kernel_times(gs_renderer* r, double* avg_ms, uint64_t* launches, int n);
 int gs_reset_kernel_times(gs_renderer* r);
+/* Record the stage events on every `every`-th frame only (default 1): each
+ * event costs device time, so throughput runs sample. */
+int gs_set_profile_interval(gs_renderer* r, uint32_t every);
 
 /* ------------------------------------------------------------ host-side data path */
 /* PLY / XYZ ingest (src/splat/file_io.cpp:11-77): all 14 3DGS properties are
