@@ -76,8 +76,10 @@ def measured_copy_peak(torch) -> float:
 
 
 def alg_bytes(kernel: str, st: dict, n: int, px: int) -> float:
-    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md)."""
-    T, P = st["n_tiles"], st["n_pairs"]
+    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md).
+    P = the pairs actually binned, sorted and blended (n_pairs_binned: the
+    reference rectangle's pairs minus those the alpha box culls)."""
+    T, P = st["n_tiles"], st["n_pairs_binned"]
     return {
         "project": n * (56 + 52),
         "scan": T * 12,
@@ -307,7 +309,8 @@ def main():
                 "frames_in_flight": F,
                 "parallelism": f"row-band x{world}" + (" (interleaved tile rows) + RCCL all-gather" if world > 1 else ""),
             },
-            "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "max_list", "n_tiles", "n_big_tiles")},
+            "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "n_pairs_binned", "max_list", "n_tiles",
+                                         "n_big_tiles")},
             "kernels": kern,
             "roofline": roofline,
             "cpu_baseline": cpu,

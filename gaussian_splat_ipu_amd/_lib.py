@@ -21,6 +21,7 @@ GS_FLAG_BIN_GLOBAL = 4
 GS_FLAG_INPUT_ORDER = 8
 GS_FLAG_BAND_INTERLEAVED = 16
 GS_FLAG_BAND_CULL = 32
+GS_FLAG_NO_PAIR_CULL = 64
 GS_LAYOUT_ROW_MAJOR = 0
 GS_LAYOUT_REF_TILE_MAJOR = 1
 GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_COUNT = range(6)
@@ -91,6 +92,7 @@ class FrameStats(C.Structure):
         ("band_rows", C.c_uint32),
         ("n_big_tiles", C.c_uint32),
         ("band_stride", C.c_uint32),
+        ("n_pairs_binned", C.c_uint64),
     ]
 
     def as_dict(self):

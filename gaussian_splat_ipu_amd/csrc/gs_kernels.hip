@@ -249,7 +249,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   const float4 mean = b.mean[i];
   const float4 sg = b.scale_gid[i];
   float4* rec = b.rec + 4 * (size_t)i;  // 64-B record
-  uint2 rect = kEmptyRect;
+  uint2 rect = kEmptyRect, crect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
     const float* m = fp.mvp;
@@ -296,6 +296,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     if (fp.band_cull && band_culled(fp, vy, T, sg)) {
       // no tile row in this band: empty rectangle; the record is never read
       b.rect[i] = rect;
+      if (fp.pair_cull) b.crect[i] = crect;
       b.depth_key[i] = dkey;
       return false;
     }
@@ -351,6 +352,23 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
         const uint32_t x0 = (uint32_t)(int)fx0, x1 = (uint32_t)(int)fx1;
         const uint32_t y0 = (uint32_t)yb0, y1 = (uint32_t)yb1;
         rect = make_uint2(x0 | (x1 << 16), y0 | (y1 << 16));
+        if (fp.pair_cull) {
+          // the tiles whose pixels the alpha box meets: a tile outside it has
+          // no pixel where the Gaussian passes alpha >= 1/255 (blend culling),
+          // so leaving it out of that tile's list changes no pixel
+          const int bx0 = (int)(b01 << 16) >> 16, bx1 = (int)b01 >> 16;
+          const int by0 = (int)(b23 << 16) >> 16, by1 = (int)b23 >> 16;
+          const int cx0 = max((int)x0, max(bx0, 0) / fp.tile_w);
+          const int cx1 = min((int)x1, bx1 < 0 ? -1 : bx1 / fp.tile_w);
+          const float gy0 = smax(fy0, (float)(max(by0, 0) / fp.tile_h));
+          const float gy1 = smin(fy1, by1 < 0 ? -1.0f : (float)(by1 / fp.tile_h));
+          int cy0, cy1;
+          band_rows_of(fp, gy0, gy1, cy0, cy1);
+          crect = (cx0 <= cx1 && cy0 <= cy1 && bx0 <= bx1 && by0 <= by1)
+                      ? make_uint2((uint32_t)cx0 | ((uint32_t)cx1 << 16),
+                                   (uint32_t)cy0 | ((uint32_t)cy1 << 16))
+                      : kEmptyRect;
+        }
         if (fp.bin_global)  // fallback binning: per-tile lengths by global atomics
           for (uint32_t y = y0; y <= y1; ++y)
             for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&b.tile_count[y * fp.tiles_x + x], 1u);
@@ -363,6 +381,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     rec[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
   b.rect[i] = rect;
+  if (fp.pair_cull) b.crect[i] = crect;
   b.depth_key[i] = dkey;
   return rendered;
 }
@@ -522,8 +541,6 @@ __device__ __forceinline__ void lds_zero(uint32_t* cnt, int words) {
 __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers b) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
   const int T = fp.n_tiles;
-  lds_zero(cnt, (T + 1) >> 1);
-  __syncthreads();
   const int c = blockIdx.x;
   const int g0 = c * fp.chunk_size;
   const int g1 = min(fp.n, g0 + fp.chunk_size);
@@ -531,6 +548,39 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
   // the first lane of each run of equal rectangles adds the run length, so
   // the LDS atomics on the same counters are not serialised lane by lane.
   const int lane = threadIdx.x & 63;
+  if (fp.pair_cull) {
+    // one u32 per tile: binned (culled) pairs in the low half, the reference
+    // list length in the high half (chunk_size <= 65535 keeps both in 16 bits)
+    lds_zero(cnt, T);
+    __syncthreads();
+    for (int i0 = g0; i0 < g1; i0 += 1024) {
+      const int i = i0 + (int)threadIdx.x;
+      const uint2 r = i < g1 ? b.rect[i] : kEmptyRect;
+      const uint2 q = i < g1 ? b.crect[i] : kEmptyRect;
+      const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
+      const uint32_t qx = (uint32_t)__shfl_up((int)q.x, 1, 64), qy = (uint32_t)__shfl_up((int)q.y, 1, 64);
+      const bool start = lane == 0 || r.x != px || r.y != py || q.x != qx || q.y != qy;
+      const unsigned long long st = __ballot(start);
+      const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
+      const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
+      const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+      const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
+      if (!start || x0 > x1) continue;
+      for (uint32_t y = y0; y <= y1; ++y) {
+        const bool yin = v0 <= y && y <= v1;
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const uint32_t inc = (len << 16) | ((yin && u0 <= x && x <= u1) ? len : 0u);
+          atomicAdd(&cnt[y * fp.tiles_x + x], inc);
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t* row = b.chunk_off + (size_t)c * T;
+    for (int t = threadIdx.x; t < T; t += 1024) row[t] = cnt[t];
+    return;
+  }
+  lds_zero(cnt, (T + 1) >> 1);
+  __syncthreads();
   for (int i0 = g0; i0 < g1; i0 += 1024) {
     const int i = i0 + (int)threadIdx.x;
     const uint2 r = i < g1 ? b.rect[i] : kEmptyRect;
@@ -555,20 +605,26 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
 // 64 tiles per workgroup (one per lane), the chunk rows split over 16 waves
 // (n_chunks <= 256: at most 16 rows per wave, held in registers).
 __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffers b) {
-  __shared__ uint32_t wsum[16][64];
+  __shared__ uint32_t wsum[16][64], whsum[16][64];
   const int T = fp.n_tiles, NC = fp.n_chunks;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int t = blockIdx.x * 64 + lane;
   const int rows = (NC + 15) / 16;
   const int c0 = wave * rows, c1 = min(NC, c0 + rows);
+  // pair_cull: entries hold binned | reference << 16; the offsets scan the
+  // binned counts, the reference counts are only summed (the histogram)
+  const uint32_t lo_mask = fp.pair_cull ? 0xFFFFu : 0xFFFFFFFFu;
   uint32_t v[16];
-  uint32_t sum = 0;
+  uint32_t sum = 0, hsum = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    v[k] = (t < T && c0 + k < c1) ? b.chunk_off[(size_t)(c0 + k) * T + t] : 0u;
+    const uint32_t e = (t < T && c0 + k < c1) ? b.chunk_off[(size_t)(c0 + k) * T + t] : 0u;
+    v[k] = e & lo_mask;
     sum += v[k];
+    hsum += fp.pair_cull ? e >> 16 : e;
   }
   wsum[wave][lane] = sum;
+  whsum[wave][lane] = hsum;
   __syncthreads();
   uint32_t run = 0;
   for (int w = 0; w < wave; ++w) run += wsum[w][lane];
@@ -582,6 +638,13 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
   }
   if (wave == 15) {  // this workgroup's 64 tiles, summarised for gs_scan_multi_kernel
     const bool ok = t < T;
+    uint32_t href = 0;  // the reference list length: the histogram, straight to host memory
+    for (int w = 0; w < 16; ++w) href += whsum[w][lane];
+    if (ok) b.host_counters[16 + t] = href;
+    unsigned long long rsum = ok ? href : 0u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) rsum += __shfl_xor(rsum, d, 64);
+    if (lane == 0) b.tile_agg[2 * blockIdx.x + 1] = make_uint4((uint32_t)rsum, (uint32_t)(rsum >> 32), 0u, 0u);
     const uint32_t L = ok ? run : 0u;
     unsigned long long sum = L;
     uint32_t mx = L;
@@ -595,7 +658,7 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
     const uint32_t nm = (uint32_t)__popcll(__ballot(ok && cl == 1));
     const uint32_t nb = (uint32_t)__popcll(__ballot(ok && cl == 2));
     if (lane == 0)
-      b.tile_agg[blockIdx.x] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), ns | (nm << 8) | (nb << 16), mx);
+      b.tile_agg[2 * blockIdx.x] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), ns | (nm << 8) | (nb << 16), mx);
   }
 }
 
@@ -606,14 +669,16 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
 // Counters and list lengths also go straight to the mapped host mirror, so a
 // frame needs no device-to-host copy.
 __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buffers b) {
-  __shared__ unsigned long long s_sum[2][4];
+  __shared__ unsigned long long s_sum[3][4];
   __shared__ uint32_t s_q[2][4][3], s_mx[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = blockIdx.x, G = gridDim.x, T = fp.n_tiles;
-  unsigned long long ps = 0, ts = 0;
+  unsigned long long ps = 0, ts = 0, rs = 0;
   uint32_t pq[3] = {0, 0, 0}, tq[3] = {0, 0, 0}, mx = 0;
   for (int i = tid; i < G; i += 256) {
-    const uint4 a = b.tile_agg[i];
+    const uint4 a = b.tile_agg[2 * i];
+    const uint4 ar = b.tile_agg[2 * i + 1];
+    rs += (unsigned long long)ar.x | ((unsigned long long)ar.y << 32);
     const unsigned long long sm = (unsigned long long)a.x | ((unsigned long long)a.y << 32);
     const uint32_t q[3] = {a.z & 255u, (a.z >> 8) & 255u, (a.z >> 16) & 255u};
     ts += sm;
@@ -629,6 +694,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
   for (int d = 32; d > 0; d >>= 1) {
     ps += __shfl_xor(ps, d, 64);
     ts += __shfl_xor(ts, d, 64);
+    rs += __shfl_xor(rs, d, 64);
     mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -639,6 +705,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
   if (lane == 0) {
     s_sum[0][wave] = ps;
     s_sum[1][wave] = ts;
+    s_sum[2][wave] = rs;
     s_mx[wave] = mx;
     for (int k = 0; k < 3; ++k) {
       s_q[0][wave][k] = pq[k];
@@ -648,6 +715,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
   __syncthreads();
   ps = s_sum[0][0] + s_sum[0][1] + s_sum[0][2] + s_sum[0][3];
   ts = s_sum[1][0] + s_sum[1][1] + s_sum[1][2] + s_sum[1][3];
+  rs = s_sum[2][0] + s_sum[2][1] + s_sum[2][2] + s_sum[2][3];
   for (int k = 0; k < 3; ++k) {
     pq[k] = s_q[0][0][k] + s_q[0][1][k] + s_q[0][2][k] + s_q[0][3][k];
     tq[k] = s_q[1][0][k] + s_q[1][1][k] + s_q[1][2][k] + s_q[1][3][k];
@@ -669,7 +737,6 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
     const unsigned long long m0 = __ballot(ok && cl == 0), m1 = __ballot(ok && cl == 1),
                              m2 = __ballot(ok && cl == 2);
     if (ok) {
-      b.host_counters[16 + t] = c;  // the histogram, straight to host memory
       b.tile_start[t] = (uint32_t)(start < 0xFFFFFFFFull ? start : 0xFFFFFFFFull);
       if (cl == 0) b.small_tiles[pq[0] + (uint32_t)__popcll(m0 & lt)] = (uint32_t)t;
       if (cl == 1) b.medium_tiles[pq[1] + (uint32_t)__popcll(m1 & lt)] = (uint32_t)t;
@@ -696,7 +763,9 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
       b.counters[7] = tq[1];
       b.counters[8] = 0;
       b.counters[9] = tq[0];
-      for (int k = 10; k < 16; ++k) b.counters[k] = 0;
+      b.counters[10] = (uint32_t)rs;
+      b.counters[11] = (uint32_t)(rs >> 32);
+      for (int k = 12; k < 16; ++k) b.counters[k] = 0;
       b.tile_start[T] = (uint32_t)(ts < 0xFFFFFFFFull ? ts : 0xFFFFFFFFull);
       for (int k = 0; k < 16; ++k) b.host_counters[k] = b.counters[k];
     }
@@ -715,8 +784,9 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
     // tile: a single LDS atomic returns the pair's final position
     for (int t = threadIdx.x; t < T; t += 1024) cnt[t] = b.tile_start[t] + row[t];
     __syncthreads();
+    const uint2* __restrict__ rects = fp.pair_cull ? b.crect : b.rect;
     for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
-      const uint2 r = b.rect[i];
+      const uint2 r = rects[i];
       const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
       if (x0 > x1) continue;
       const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
@@ -731,7 +801,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
   lds_zero(cnt, (T + 1) >> 1);
   __syncthreads();
   for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
-    const uint2 r = b.rect[i];
+    const uint2 r = fp.pair_cull ? b.crect[i] : b.rect[i];
     const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
     if (x0 > x1) continue;
     const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
@@ -1399,7 +1469,7 @@ hipError_t init_kernel_attributes() {
 
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (!fp.bin_global && fp.n_chunks > 0 && fp.n_tiles > 0) {
-    const size_t lds = bin_lds_bytes(fp.n_tiles);
+    const size_t lds = fp.pair_cull ? (size_t)fp.n_tiles * 4 : bin_lds_bytes(fp.n_tiles);
     gs_count_kernel<<<fp.n_chunks, 1024, lds, s>>>(fp, b);
     gs_colscan_kernel<<<(fp.n_tiles + 63) / 64, 1024, 0, s>>>(fp, b);
     gs_scan_multi_kernel<<<(fp.n_tiles + 63) / 64, 256, 0, s>>>(fp, b);

@@ -38,6 +38,8 @@ struct FrameParams {
   int chunk_size;     // Gaussians per binning chunk (<= 65535)
   int n_chunks;
   int emit_wide;      // emit with one u32 LDS cursor per tile (n_tiles * 4 <= kBinLdsMax)
+  int pair_cull;      // bin only the tiles the alpha box meets (crect); the
+                      // reference list lengths are counted alongside
 };
 
 // Device workspace of one renderer.
@@ -55,6 +57,7 @@ struct Buffers {
   float4* rec;              // 4 x float4 (64 B): mx my k0 k1 | k2 k3 r g | b pcut boxx boxy | radius clipz 0 0
   uint32_t* depth_key;      // order-preserving key of clip z
   uint2* rect;              // (tx0 | tx1 << 16, ty0 | ty1 << 16), band-relative rows
+  uint2* crect;             // rect cut to the tiles the alpha box meets (pair_cull)
   // binning
   uint32_t* tile_count;     // [n_tiles]      (memset 0 each frame)
   uint32_t* tile_start;     // [n_tiles + 1]
@@ -66,14 +69,16 @@ struct Buffers {
   uint32_t* medium_tiles;   // [n_tiles]  lists in (kSortRegCap, kSortLdsCap] (block sort queue)
   uint32_t* small_tiles;    // [n_tiles]  lists in [1, kSortRegCap] (one-wave sort queue)
   uint32_t* chunk_off;      // [n_chunks][n_tiles] chunk histograms -> offsets
-  uint4* tile_agg;          // [ceil(n_tiles / 64)] per 64 tiles: list-length sum (lo, hi),
-                            //   small | medium << 8 | big << 16 counts, max length
+  uint4* tile_agg;          // [2 * ceil(n_tiles / 64)] per 64 tiles: list-length sum (lo, hi),
+                            //   small | medium << 8 | big << 16 counts, max length;
+                            //   then the reference list-length sum (lo, hi), 0, 0
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
   uint32_t* host_counters;  // mapped pinned mirror of counters[16] + tile_count[n_tiles],
                             //   written by the chunked scan (no D2H copy per frame)
   uint32_t* counters;       // [16]: 0 n_big, 1 big_next, 2 n_rendered, 3 overflow,
                             //  4 max_list, 5 n_pairs (low), 6 n_pairs (high),
-                            //  7 n_medium, 8 medium_next, 9 n_small
+                            //  7 n_medium, 8 medium_next, 9 n_small,
+                            //  10 / 11 reference pairs (low / high: unculled lists)
   // outputs
   float4* rgba;             // band_rows x width, row-major
   uint8_t* bgr;             // band rows (padded) x width x 3

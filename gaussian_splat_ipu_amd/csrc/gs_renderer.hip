@@ -55,13 +55,14 @@ struct gs_renderer {
 
   // device memory
   void* d_scene = nullptr;      // 4 x float4 x n
-  void* d_gauss = nullptr;      // rec (48 B) + depth key (4 B) + rect (8 B) per Gaussian
+  void* d_gauss = nullptr;      // rec (64 B) + rect, crect (8 B each) + depth key (4 B) per Gaussian
   void* d_zero = nullptr;       // counters[16] + tile_count[n_tiles] (memset every frame)
   void* d_tiles = nullptr;      // tile_start[n_tiles+1], tile_cursor, big_tiles
   void* d_pairs = nullptr;      // pairs, pairs_alt, list
   void* d_out = nullptr;        // rgba f32 + bgr8
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
   int bin_global = 0, chunk_size = 0, n_chunks = 0;
+  bool pair_cull = false;       // chunked binning into the alpha-box tiles only
   size_t zero_bytes = 0;
   size_t bgr_bytes = 0;
   gsk::Buffers buf{};
@@ -234,6 +235,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.chunk_size = r->chunk_size;
   fp.n_chunks = r->n_chunks;
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
+  fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
   return fp;
 }
 
@@ -296,10 +298,17 @@ int finish_frame(gs_renderer* r) {
   r->frame_pending = false;
   const uint32_t* c = r->h_counters;
   const uint64_t P = (uint64_t)c[5] | ((uint64_t)c[6] << 32);
+  // the chunked scan also sums the reference (unculled) list lengths
+  const bool chunked = !r->bin_global && r->n_chunks > 0 && r->n_tiles > 0;
+  const uint64_t P_ref = chunked ? ((uint64_t)c[10] | ((uint64_t)c[11] << 32)) : P;
   r->stats.n_gaussians = r->n;
   r->stats.n_rendered = c[2];
-  r->stats.n_pairs = P;
-  r->stats.max_list = c[4];
+  r->stats.n_pairs = P_ref;
+  r->stats.n_pairs_binned = P;
+  // the longest reference list (the binned lists can be shorter)
+  uint32_t mx = 0;
+  for (int t = 0; t < r->n_tiles; ++t) mx = std::max(mx, c[16 + t]);
+  r->stats.max_list = mx;
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
   if (c[3]) {
@@ -366,6 +375,7 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   r->cfg = *cfg;
   r->n = n;
   r->profile = (cfg->flags & GS_FLAG_PROFILE) != 0;
+  r->pair_cull = (cfg->flags & GS_FLAG_NO_PAIR_CULL) == 0;
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
@@ -459,15 +469,16 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
   r->buf.inv_perm = r->buf.perm + nn;
 
-  // per Gaussian: 64-B record, 8-B tile rectangle, 4-B depth key; plus V per
-  // project workgroup
+  // per Gaussian: 64-B record, 8-B tile rectangle and its alpha-box cut, 4-B
+  // depth key; plus V per project workgroup
   const size_t nblk = (nn + 255) / 256;
-  if ((e = hipMalloc(&r->d_gauss, nn * (64 + 8 + 4) + nblk * 4)) != hipSuccess)
+  if ((e = hipMalloc(&r->d_gauss, nn * (64 + 8 + 8 + 4) + nblk * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(per-Gaussian)"));
   r->buf.rec = (float4*)r->d_gauss;
   r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 64);
-  r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
-  r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 76);
+  r->buf.crect = (uint2*)((char*)r->d_gauss + nn * 72);
+  r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 80);
+  r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 84);
 
   const size_t T = (size_t)std::max(r->n_tiles, 1);
   r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
@@ -475,7 +486,7 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   r->buf.counters = (uint32_t*)r->d_zero;
   r->buf.tile_count = (uint32_t*)r->d_zero + 16;
   const size_t n_agg = (T + 63) / 64;
-  if ((e = hipMalloc(&r->d_tiles, (T + 1 + 4 * T) * 4 + n_agg * 16 + 16)) != hipSuccess)
+  if ((e = hipMalloc(&r->d_tiles, (T + 1 + 4 * T) * 4 + n_agg * 32 + 16)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(tiles)"));
   r->buf.tile_start = (uint32_t*)r->d_tiles;
   r->buf.tile_cursor = r->buf.tile_start + T + 1;
@@ -590,7 +601,7 @@ int gs_render(gs_renderer* r) {
     rc = finish_frame(r);
     if (rc != GS_EOVERFLOW) return rc;
     // grow the pair capacity (the reference silently drops on overflow)
-    const uint64_t need = r->stats.n_pairs + r->stats.n_pairs / 4 + 1024;
+    const uint64_t need = r->stats.n_pairs_binned + r->stats.n_pairs_binned / 4 + 1024;
     const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(need, 2 * r->pair_cap), 0xFFFFFFF0ull);
     if (need > 0xFFFFFFF0ull) {
       set_error("gs_render: pair count exceeds 2^32");
@@ -687,6 +698,14 @@ int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t*
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
+  if (make_params(r).pair_cull) {
+    // the frame's lists hold only the tiles each alpha box meets: bin the
+    // reference lists again (the frame itself comes out identical)
+    r->pair_cull = false;
+    rc = gs_render(r);
+    r->pair_cull = true;
+    if (rc != GS_OK) return rc;
+  }
   const size_t T = (size_t)r->n_tiles;
   if (n_start < T + 1 || n_list < r->stats.n_pairs) {
     set_error("gs_read_bins: destination too small");

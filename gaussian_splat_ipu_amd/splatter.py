@@ -22,6 +22,7 @@ import numpy as np
 from . import camera
 from ._lib import (
     GS_FLAG_BAND_CULL,
+    GS_FLAG_NO_PAIR_CULL,
     GS_FLAG_BAND_INTERLEAVED,
     GS_FLAG_BIN_GLOBAL,
     GS_FLAG_INPUT_ORDER,
@@ -66,6 +67,7 @@ class GpuSplatter:
         input_order: bool = False,
         band_interleaved: bool = False,
         band_cull: bool = False,
+        pair_cull: bool = True,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -90,6 +92,7 @@ class GpuSplatter:
             | (GS_FLAG_INPUT_ORDER if input_order else 0)
             | (GS_FLAG_BAND_INTERLEAVED if band_interleaved else 0)
             | (GS_FLAG_BAND_CULL if band_cull else 0)
+            | (0 if pair_cull else GS_FLAG_NO_PAIR_CULL)
         )
         self.cfg = cfg
         h = C.c_void_p()

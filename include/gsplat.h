@@ -81,6 +81,11 @@ typedef struct gs_config {
                                   of this band (frames, lists and histograms
                                   are unchanged; n_rendered then counts only
                                   the Gaussians that reach the band) */
+#define GS_FLAG_NO_PAIR_CULL 64u /* bin every tile of the reference rectangle.
+                                  By default a Gaussian is binned only into the
+                                  tiles its alpha >= 1/255 box meets (the
+                                  frame is bit-identical; the histogram and
+                                  gs_read_bins keep the reference lists) */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */
@@ -92,8 +97,9 @@ typedef enum gs_layout {
 typedef struct gs_frame_stats {
   uint64_t n_gaussians;   /* N                                  */
   uint64_t n_rendered;    /* V: pass guard band and z < 0       */
-  uint64_t n_pairs;       /* P: sum over tiles of list lengths  */
-  uint64_t max_list;      /* max tile list length               */
+  uint64_t n_pairs;       /* P: sum over tiles of the reference list
+                             lengths (the histogram)            */
+  uint64_t max_list;      /* max reference tile list length     */
   uint64_t pair_capacity;
   uint32_t n_tiles;       /* tiles in this renderer's band      */
   uint32_t tiles_x, tiles_y;
@@ -103,6 +109,9 @@ typedef struct gs_frame_stats {
                                    to whole tiles                   */
   uint32_t n_big_tiles;   /* tiles sorted by the large-list path */
   uint32_t band_stride;   /* tile-row stride of the band (1: contiguous) */
+  uint64_t n_pairs_binned; /* pairs binned, sorted and blended: P minus
+                              the pairs culled by the alpha box (= P with
+                              GS_FLAG_NO_PAIR_CULL)                   */
 } gs_frame_stats;
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */

@@ -244,6 +244,54 @@ def _band_render(g, view, proj, fb, scale_div, band_index, band_count, interleav
     return s
 
 
+def test_pair_cull_changes_nothing(pc12):
+    """By default a Gaussian is binned only into the tiles its alpha >= 1/255
+    box meets.  Frame, RGBA, histogram, reference lists (gs_read_bins re-bins
+    them) and pair count must equal GS_FLAG_NO_PAIR_CULL's, on point_cloud_12
+    (reference geometry and 1080p), the edge-case scene and interleaved bands;
+    and the culled frames must bin fewer pairs."""
+    from gaussian_splat_ipu_amd import camera, scene
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    ge, bbe = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=5000, seed=3, sh_degree=0)))
+    a = np.ascontiguousarray(ge).view(np.float32).reshape(-1, 16).copy()
+    a[50:100, 15] = -3.0
+    a[100:150, 0:3] = [0.0, 0.0, 40.0]
+    a[150:200, 12:15] = 30.0
+    a[250:300, 12:15] = -200.0
+    a[300:310, 0] = np.nan
+    a[310:320, 0] = np.inf
+    a[320:370, 7] = 1.0 / 255.0  # opacities at the cut
+    a[370:420, 7] = 0.5 / 255.0
+    g, bb = pc12
+    cases = [(g, bb, 1920, 1080, 16, 16, 1.0, 1, 0), (g, bb, 1280, 720, 32, 20, 0.1, 1, 0),
+             (g, bb, 1280, 720, 16, 16, 1.0, 3, 1), (a, bbe, 800, 600, 16, 16, 1.0, 1, 0)]
+    for scn, box, W, H, TW, TH, sd, bc, bi in cases:
+        view, proj = camera.headless(box, W, H)
+        fb = TiledFramebuffer(W, H, TW, TH)
+        out = []
+        for pc in (True, False):
+            s = GpuSplatter(scn, fb, device=0, band_index=bi, band_count=bc, band_interleaved=bc > 1,
+                            pair_cull=pc)
+            s.set_view_wire(view)
+            s.set_projection_wire(proj)
+            s.update_focal_lengths(camera.FOV_DEFAULT, sd)
+            s.execute()
+            st = s.stats()
+            out.append((s.get_rgba(), s.get_frame_buffer(), s.get_histogram(), st, s.get_bins()))
+            s.close()
+        (r1, b1, h1, s1, (t1, l1)), (r2, b2, h2, s2, (t2, l2)) = out
+        assert_same_bits(r1, r2, f"{W}x{H} rgba")
+        np.testing.assert_array_equal(b1, b2)
+        np.testing.assert_array_equal(h1, h2)
+        np.testing.assert_array_equal(t1, t2)
+        np.testing.assert_array_equal(l1, l2)
+        assert s1["n_pairs"] == s2["n_pairs"] == s2["n_pairs_binned"]
+        assert s1["max_list"] == s2["max_list"]
+        assert s1["n_pairs_binned"] < s1["n_pairs"]
+
+
 @pytest.mark.parametrize("interleaved", [False, True])
 def test_band_cull_changes_nothing(pc12, interleaved):
     """GS_FLAG_BAND_CULL skips the projection of Gaussians whose conservative
@@ -334,7 +382,7 @@ def test_overflow_grows_capacity(pc12):
     g, bb = pc12
     view, proj = camera.headless(bb, 1280, 720)
     s, f = _frame_pair(g, view, proj, 1280, 720, 16, 16, 1.0, pair_capacity=1000)
-    assert s.stats()["pair_capacity"] >= s.stats()["n_pairs"] > 1000
+    assert s.stats()["pair_capacity"] >= s.stats()["n_pairs_binned"] > 1000
     _assert_parity(s, f, g, check_proj=False)
 
 
