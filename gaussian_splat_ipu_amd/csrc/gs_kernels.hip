@@ -248,7 +248,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   bool rendered = false;
   const float4 mean = b.mean[i];
   const float4 sg = b.scale_gid[i];
-  float4* rec = b.rec + 4 * (size_t)i;  // 64-B record
+  float4* rec = b.rec + 3 * (size_t)i;  // 48-B record
   uint2 rect = kEmptyRect, crect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
@@ -333,7 +333,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     rec[0] = make_float4(vx, vy, k0, k2);
     rec[1] = make_float4(k1, pcut, col.x, col.y);
     rec[2] = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
-    rec[3] = make_float4(radius, cz, 0.0f, 0.0f);
+    if (fp.full_record) b.rec_tail[i] = make_float2(radius, cz);  // readback only
     if (within && cz < 0.0f) {  // codelets.cpp:493
       rendered = true;
       dkey = depth_key_of(cz);
@@ -378,7 +378,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     rec[1] = make_float4(0.0f, __builtin_huge_valf(), 0.0f, 0.0f);
     rec[2] = make_float4(0.0f, 0.0f, __uint_as_float(kEmptyBox), __uint_as_float(kEmptyBox));
-    rec[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (fp.full_record) b.rec_tail[i] = make_float2(0.0f, 0.0f);
   }
   b.rect[i] = rect;
   if (fp.pair_cull) b.crect[i] = crect;
@@ -1347,7 +1347,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
   uint32_t g_cur = load_idx(lane);
   if (g_cur != 0xFFFFFFFFu) {
-    const float4* qq = b.rec + 4 * (size_t)g_cur;
+    const float4* qq = b.rec + 3 * (size_t)g_cur;
     a0 = qq[0];
     a1 = qq[1];
     a2 = qq[2];
@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     g_cur = g_next;
     a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (g_cur != 0xFFFFFFFFu) {
-      const float4* qq = b.rec + 4 * (size_t)g_cur;
+      const float4* qq = b.rec + 3 * (size_t)g_cur;
       a0 = qq[0];
       a1 = qq[1];
       a2 = qq[2];

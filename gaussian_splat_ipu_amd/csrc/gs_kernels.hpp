@@ -38,6 +38,7 @@ struct FrameParams {
   int chunk_size;     // Gaussians per binning chunk (<= 65535)
   int n_chunks;
   int emit_wide;      // emit with one u32 LDS cursor per tile (n_tiles * 4 <= kBinLdsMax)
+  int full_record;    // also write the readback-only record tail (radius, clip z)
   int pair_cull;      // bin only the tiles the alpha box meets (crect); the
                       // reference list lengths are counted alongside
 };
@@ -54,7 +55,8 @@ struct Buffers {
   const uint32_t* perm;     // [n] device index -> input index
   const uint32_t* inv_perm; // [n] input index -> device index
   // per-Gaussian projection outputs
-  float4* rec;              // 4 x float4 (64 B): mx my k0 k1 | k2 k3 r g | b pcut boxx boxy | radius clipz 0 0
+  float4* rec;              // 3 x float4 (48 B): mx my k0 k2 | k1 pcut r g | b op boxx boxy
+  float2* rec_tail;         // radius, clip z: readback only (written with full_record)
   uint32_t* depth_key;      // order-preserving key of clip z
   uint2* rect;              // (tx0 | tx1 << 16, ty0 | ty1 << 16), band-relative rows
   uint2* crect;             // rect cut to the tiles the alpha box meets (pair_cull)

@@ -55,7 +55,7 @@ struct gs_renderer {
 
   // device memory
   void* d_scene = nullptr;      // 4 x float4 x n
-  void* d_gauss = nullptr;      // rec (64 B) + rect, crect (8 B each) + depth key (4 B) per Gaussian
+  void* d_gauss = nullptr;      // rec (48 B) + tail, rect, crect (8 B each) + depth key (4 B) per Gaussian
   void* d_zero = nullptr;       // counters[16] + tile_count[n_tiles] (memset every frame)
   void* d_tiles = nullptr;      // tile_start[n_tiles+1], tile_cursor, big_tiles
   void* d_pairs = nullptr;      // pairs, pairs_alt, list
@@ -469,16 +469,18 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
   r->buf.inv_perm = r->buf.perm + nn;
 
-  // per Gaussian: 64-B record, 8-B tile rectangle and its alpha-box cut, 4-B
-  // depth key; plus V per project workgroup
+  // per Gaussian: 48-B record (what the blend reads), its 8-B readback tail,
+  // 8-B tile rectangle and its alpha-box cut, 4-B depth key; plus V per
+  // project workgroup
   const size_t nblk = (nn + 255) / 256;
-  if ((e = hipMalloc(&r->d_gauss, nn * (64 + 8 + 8 + 4) + nblk * 4)) != hipSuccess)
+  if ((e = hipMalloc(&r->d_gauss, nn * (48 + 8 + 8 + 8 + 4) + nblk * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(per-Gaussian)"));
   r->buf.rec = (float4*)r->d_gauss;
-  r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 64);
-  r->buf.crect = (uint2*)((char*)r->d_gauss + nn * 72);
-  r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 80);
-  r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 84);
+  r->buf.rec_tail = (float2*)((char*)r->d_gauss + nn * 48);
+  r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 56);
+  r->buf.crect = (uint2*)((char*)r->d_gauss + nn * 64);
+  r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
+  r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 76);
 
   const size_t T = (size_t)std::max(r->n_tiles, 1);
   r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
@@ -731,22 +733,25 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
-  std::vector<float> rec(r->n * 16);
+  std::vector<float> rec(r->n * 12), tail(r->n * 2);
   std::vector<uint32_t> rect(r->n * 2);
-  if (r->n && (r->cfg.flags & GS_FLAG_BAND_CULL)) {
-    // the frame skipped band-culled Gaussians: project all of them again
+  if (r->n) {
+    // project again with the readback tail of the record (radius, clip z),
+    // which frames skip, and without the band cull (same values otherwise)
     gsk::FrameParams fp = make_params(r);
     fp.band_cull = 0;
+    fp.full_record = 1;
     gsk::launch_project(fp, r->buf, r->stream);
     GS_HIP(hipGetLastError());
     GS_HIP(hipStreamSynchronize(r->stream));
   }
   if (r->n) {
-    GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 64, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 48, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(tail.data(), r->buf.rec_tail, r->n * 8, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(rect.data(), r->buf.rect, r->n * 8, hipMemcpyDeviceToHost));
   }
   for (size_t i = 0; i < r->n; ++i) {
-    const float* q = &rec[i * 16];
+    const float* q = &rec[i * 12];
     float* o = dst + (size_t)r->perm[i] * 12;  // in input order
     o[0] = q[0];  // mean2d
     o[1] = q[1];
@@ -754,8 +759,8 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     o[3] = q[4];
     o[4] = q[3];
     o[5] = q[9];
-    o[6] = q[13];  // clip z
-    o[7] = q[12];  // radius
+    o[6] = tail[i * 2 + 1];  // clip z
+    o[7] = tail[i * 2];      // radius
     const uint32_t rx = rect[i * 2], ry = rect[i * 2 + 1];
     o[8] = (float)(rx & 0xFFFF);
     o[9] = (float)(ry & 0xFFFF);
