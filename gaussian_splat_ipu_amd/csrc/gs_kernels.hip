@@ -144,22 +144,23 @@ constexpr uint2 kEmptyRect = {1u, 1u};  // tx0 = 1 > tx1 = 0
 constexpr uint32_t kEmptyBox = 0x80007FFFu;  // lo = +32767 > hi = -32768
 constexpr uint32_t kFullBox = 0x7FFF8000u;   // lo = -32768, hi = +32767
 
-__device__ __forceinline__ uint32_t pack_i16x2(double lo, double hi) {
-  lo = fmax(-32768.0, fmin(32767.0, lo));
-  hi = fmax(-32768.0, fmin(32767.0, hi));
+__device__ __forceinline__ uint32_t pack_i16x2(float lo, float hi) {
+  lo = fmaxf(-32768.0f, fminf(32767.0f, lo));
+  hi = fmaxf(-32768.0f, fminf(32767.0f, hi));
   return ((uint32_t)(int)lo & 0xFFFFu) | ((uint32_t)(int)hi << 16);
 }
 
-// Conservative alpha footprint of one 2D Gaussian, used by the blend to skip
-// work that cannot change a pixel ("blend culling"):
+// Conservative alpha footprint of one 2D Gaussian, used to skip work that
+// cannot change a pixel ("blend culling"):
 //   pcut: a lane with power < pcut has op * expf(power) < 1/255, i.e. the
 //         reference would `continue` (codelets.cpp:401-403);
 //   box:  integer pixel box (x0,x1 | y0,y1) outside of which every pixel has
 //         power < pcut (the bounding box of the ellipse { d^T Q d <= -2 pcut }
-//         of the conic Q, half-widths widened by 0.1%, computed in fp64; pixel
+//         of the conic Q, widened to cover its own fp32 rounding; pixel
 //         centres are the integer coordinates the blend evaluates).
 // Both only ever remove evaluations whose outcome is "skip", so the blended
-// result is bit-identical to evaluating every list entry.
+// result is bit-identical to evaluating every list entry.  fp32 throughout,
+// each rounding covered by an explicit margin (the bounds are in DESIGN.md).
 __device__ __forceinline__ void alpha_footprint(float mx, float my, float k0, float k1, float k2,
                                                 float op, const FrameParams& fp, float& pcut,
                                                 uint32_t& box_x, uint32_t& box_y) {
@@ -176,26 +177,27 @@ __device__ __forceinline__ void alpha_footprint(float mx, float my, float k0, fl
     box_y = kEmptyBox;
     return;
   }
-  const double pc = -log(255.0 * (double)op) - 0.05;  // power below this: alpha < 0.96 / 255
-  float pf = (float)pc;
-  // round toward -inf (pc <= -0.05 < 0: one ulp more negative is bits + 1)
-  if ((double)pf > pc) pf = __uint_as_float(__float_as_uint(pf) + 1u);
-  pcut = pf;
-  const double a = k0, b = k1, c = k2;
-  const double det = a * c - b * b;
+  // pc = ln(1 / (255 op)) - 0.05 (power below it: alpha < 0.96 / 255), pushed
+  // down by far more than the error of v_log_f32 and the product 255 * op
+  const float ln = __builtin_amdgcn_logf(255.0f * op) * 0.693147182f;  // >= 0
+  if (!(ln < 1e30f)) return;                                          // op = +inf
+  const float pc = -ln - 0.05f;
+  pcut = pc - (ln * 1e-5f + 1e-5f);
+  const float a = k0, b = k1, c = k2;
+  const float det = __builtin_fmaf(a, c, -(b * b));  // relative error < 6e-5 when kept
   // Well-conditioned conics only (1 - rho^2 > 1e-3): then the fp32 rounding of
-  // the reference's power expression is < 7e-4 relative, far inside the 0.05
-  // margin of pcut ("blend culling").
-  if (a > 0.0 && c > 0.0 && det > 1e-3 * a * c) {
-    const double R = -2.0 * pc;
-    // The integer pixels within the widened half-widths: a pixel outside has
-    // |d| beyond 1.001x the ellipse's extent, so d^T Q d > 1.002 R exactly and
-    // the fp32 power (relative error < 7.2e-4) is < 1.0012 pc < pcut.  The
-    // 1e-6 absorbs the fp64 rounding of mx -/+ ex for vanishing ellipses.
-    const double ex = sqrt(R * c / det) * 1.001 + 1e-6;
-    const double ey = sqrt(R * a / det) * 1.001 + 1e-6;
-    box_x = pack_i16x2(ceil((double)mx - ex), floor((double)mx + ex));
-    box_y = pack_i16x2(ceil((double)my - ey), floor((double)my + ey));
+  // the reference's power expression is < 7.2e-4 relative.  A pixel outside
+  // the box has |d| > 1.00096 x the ellipse's extent (1.001 minus the < 4e-5
+  // error of ex), so d^T Q d > 1.0019 R and its fp32 power < 1.0011 pcut < pcut.
+  if (a > 0.0f && c > 0.0f && det > 1e-3f * a * c) {
+    const float R = -2.0f * pcut;
+    const float ex = __builtin_sqrtf(R * c / det) * 1.001f;
+    const float ey = __builtin_sqrtf(R * a / det) * 1.001f;
+    // slack for the rounding of m -/+ e (< 2^-24 of their magnitude)
+    const float sx = (__builtin_fabsf(mx) + ex) * 4.8e-7f + 1e-6f;
+    const float sy = (__builtin_fabsf(my) + ey) * 4.8e-7f + 1e-6f;
+    box_x = pack_i16x2(__builtin_ceilf(mx - ex - sx), __builtin_floorf(mx + ex + sx));
+    box_y = pack_i16x2(__builtin_ceilf(my - ey - sy), __builtin_floorf(my + ey + sy));
   }
 }
 
