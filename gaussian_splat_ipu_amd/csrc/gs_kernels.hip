@@ -555,24 +555,32 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
     // list length in the high half (chunk_size <= 65535 keeps both in 16 bits)
     lds_zero(cnt, T);
     __syncthreads();
-    for (int i0 = g0; i0 < g1; i0 += 1024) {
-      const int i = i0 + (int)threadIdx.x;
-      const uint2 r = i < g1 ? b.rect[i] : kEmptyRect;
-      const uint2 q = i < g1 ? b.crect[i] : kEmptyRect;
-      const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
-      const uint32_t qx = (uint32_t)__shfl_up((int)q.x, 1, 64), qy = (uint32_t)__shfl_up((int)q.y, 1, 64);
-      const bool start = lane == 0 || r.x != px || r.y != py || q.x != qx || q.y != qy;
-      const unsigned long long st = __ballot(start);
-      const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
-      const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
-      const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
-      const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
-      if (!start || x0 > x1) continue;
-      for (uint32_t y = y0; y <= y1; ++y) {
-        const bool yin = v0 <= y && y <= v1;
-        for (uint32_t x = x0; x <= x1; ++x) {
-          const uint32_t inc = (len << 16) | ((yin && u0 <= x && x <= u1) ? len : 0u);
-          atomicAdd(&cnt[y * fp.tiles_x + x], inc);
+    for (int i00 = g0; i00 < g1; i00 += 4096) {  // 4 Gaussians per thread, loaded up front
+      uint2 rr[4], qq[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i00 + k * 1024 + (int)threadIdx.x;
+        rr[k] = i < g1 ? b.rect[i] : kEmptyRect;
+        qq[k] = i < g1 ? b.crect[i] : kEmptyRect;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint2 r = rr[k], q = qq[k];
+        const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
+        const uint32_t qx = (uint32_t)__shfl_up((int)q.x, 1, 64), qy = (uint32_t)__shfl_up((int)q.y, 1, 64);
+        const bool start = lane == 0 || r.x != px || r.y != py || q.x != qx || q.y != qy;
+        const unsigned long long st = __ballot(start);
+        const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
+        const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
+        const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+        const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
+        if (!start || x0 > x1) continue;
+        for (uint32_t y = y0; y <= y1; ++y) {
+          const bool yin = v0 <= y && y <= v1;
+          for (uint32_t x = x0; x <= x1; ++x) {
+            const uint32_t inc = (len << 16) | ((yin && u0 <= x && x <= u1) ? len : 0u);
+            atomicAdd(&cnt[y * fp.tiles_x + x], inc);
+          }
         }
       }
     }
@@ -748,7 +756,16 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
   if (g == 0) {  // frame counters (every counter of the frame is reset here)
     uint32_t vsum = 0;
     const int nb = (fp.n + 255) / 256;
-    for (int i = tid; i < nb; i += 256) vsum += b.block_rendered[i];
+    for (int i0 = 0; i0 < nb; i0 += 256 * 8) {  // 8 independent loads in flight per thread
+      uint32_t vr[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + k * 256 + tid;
+        vr[k] = i < nb ? b.block_rendered[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) vsum += vr[k];
+    }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
     __syncthreads();
@@ -784,19 +801,43 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
   if (fp.emit_wide) {
     // one u32 cursor per tile, seeded with the chunk's first slot of the
     // tile: a single LDS atomic returns the pair's final position
-    for (int t = threadIdx.x; t < T; t += 1024) cnt[t] = b.tile_start[t] + row[t];
+    for (int t0 = 0; t0 < T; t0 += 1024 * 8) {  // loads first: 16 in flight per thread
+      uint32_t st[8], ro[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int t = t0 + k * 1024 + (int)threadIdx.x;
+        st[k] = t < T ? b.tile_start[t] : 0u;
+        ro[k] = t < T ? row[t] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int t = t0 + k * 1024 + (int)threadIdx.x;
+        if (t < T) cnt[t] = st[k] + ro[k];
+      }
+    }
     __syncthreads();
     const uint2* __restrict__ rects = fp.pair_cull ? b.crect : b.rect;
-    for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
-      const uint2 r = rects[i];
-      const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
-      if (x0 > x1) continue;
-      const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
-      for (uint32_t y = y0; y <= y1; ++y)
-        for (uint32_t x = x0; x <= x1; ++x) {
-          const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
-          if (pos < fp.pair_cap) b.pairs[pos] = key;
-        }
+    for (int i0 = g0; i0 < g1; i0 += 4096) {  // 4 Gaussians per thread, loaded up front
+      uint2 r[4];
+      uint32_t dk[4], pm[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + k * 1024 + (int)threadIdx.x;
+        r[k] = i < g1 ? rects[i] : kEmptyRect;
+        dk[k] = i < g1 ? b.depth_key[i] : 0u;
+        pm[k] = i < g1 ? b.perm[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x0 = r[k].x & 0xFFFFu, x1 = r[k].x >> 16, y0 = r[k].y & 0xFFFFu, y1 = r[k].y >> 16;
+        if (x0 > x1) continue;
+        const unsigned long long key = ((unsigned long long)dk[k] << 32) | pm[k];
+        for (uint32_t y = y0; y <= y1; ++y)
+          for (uint32_t x = x0; x <= x1; ++x) {
+            const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
+            if (pos < fp.pair_cap) b.pairs[pos] = key;
+          }
+      }
     }
     return;
   }
