@@ -36,7 +36,8 @@ class GpuSplatter {
  public:
   // IpuSplatter(const Gaussians&, TiledFramebuffer&, bool noAMP)
   GpuSplatter(const std::vector<gs_gaussian3d>& gaussians, const GpuFramebuffer& fb,
-              int device = -1, uint32_t bandIndex = 0, uint32_t bandCount = 1)
+              int device = -1, uint32_t bandIndex = 0, uint32_t bandCount = 1,
+              uint32_t flags = 0 /* GS_FLAG_* */)
       : fb_(fb) {
     gs_config cfg;
     gs_check(gs_config_init(&cfg), "gs_config_init");
@@ -47,6 +48,7 @@ class GpuSplatter {
     cfg.device = device;
     cfg.band_index = bandIndex;
     cfg.band_count = bandCount;
+    cfg.flags = flags;
     gs_check(gs_create(gaussians.data(), gaussians.size(), &cfg, &r_), "gs_create");
   }
   ~GpuSplatter() { gs_destroy(r_); }
