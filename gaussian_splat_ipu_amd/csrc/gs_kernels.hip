@@ -1204,10 +1204,8 @@ __global__ __launch_bounds__(256) void gs_sort_tiles_kernel(FrameParams fp, Buff
     wave_sort_tile<1>(b, s, L, lane);
   else if (L <= 128u)
     wave_sort_tile<2>(b, s, L, lane);
-  else if (L <= 256u)
-    wave_sort_tile<4>(b, s, L, lane);
   else
-    wave_sort_tile<8>(b, s, L, lane);
+    wave_sort_tile<4>(b, s, L, lane);
 }
 
 // -------------------------------------------------------------------- blend

@@ -88,7 +88,7 @@ struct Buffers {
 
 constexpr int GS_STAGE_EVENTS = 6;  // profile events: before project .. after blend
 constexpr int kSortLdsCap = 2048;  // largest tile list sorted by one workgroup (registers + LDS)
-constexpr uint32_t kSortRegCap = 512;  // largest tile list sorted in the registers of one wave
+constexpr uint32_t kSortRegCap = 256;  // largest tile list sorted in the registers of one wave
 constexpr size_t kBinLdsMax = 160 * 1024;  // LDS of one CU: chunk histograms up to 81920 tiles
 
 size_t bin_lds_bytes(int n_tiles);
