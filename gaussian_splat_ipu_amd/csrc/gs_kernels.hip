@@ -1178,9 +1178,13 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
 // the strides >= 64 E through LDS); the rest give each of their waves one
 // small list (L <= 512, sorted in one wave's registers).  Keys are unique (the
 // input index is in the low word), so the order is total and deterministic.
-__global__ __launch_bounds__(256) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
+  // the radix path's histograms alias the merge path's key buffer (a
+  // workgroup takes one path): 16 KB per workgroup, 8 workgroups per CU
   __shared__ unsigned long long keys[kSortLdsCap];
-  __shared__ uint32_t r_hist[256], r_base[256], r_wcnt[4][256];
+  uint32_t* const r_hist = (uint32_t*)keys;
+  uint32_t* const r_base = r_hist + 256;
+  uint32_t(*const r_wcnt)[256] = (uint32_t(*)[256])(r_hist + 512);
   const uint32_t n_big = b.counters[0];
   if (blockIdx.x < n_big) {  // the longest lists first
     radix_sort_tile<256>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
