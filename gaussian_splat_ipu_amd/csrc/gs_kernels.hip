@@ -22,6 +22,15 @@
 // the IEEE operations written (and matches the CPU oracle bit for bit).
 #include "gs_kernels.hpp"
 
+// blend: 1 = one record mask per pixel, 0 = per 2x2 quad (A/B switch)
+// blend: waves per workgroup (the waves are independent)
+#ifndef GS_BLEND_WPG
+#define GS_BLEND_WPG 4
+#endif
+#ifndef GS_BLEND_PIXEL_MASKS
+#define GS_BLEND_PIXEL_MASKS 0
+#endif
+
 namespace gsk {
 namespace {
 
@@ -1304,12 +1313,27 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers
   dst[2] = to_u8(o0);
 }
 
-// all four lanes of this lane's quad (lanes 4q..4q+3) have p
-__device__ __forceinline__ bool quad_all(bool p) {
-  int v = p ? 1 : 0;
-  v &= __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  v &= __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  return v != 0;
+// The records of one 32-bit word of a lane's batch mask (bit k = staged record
+// off + k), two per iteration in list order: their exponentials are
+// independent, the compositing is sequential.  The lane stops as soon as its
+// pixel has saturated (the reference's `break`).
+template <bool FAST>
+__device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t mw, int off) {
+  while (mw) {
+    const int ja = off + __builtin_ctz(mw);
+    mw &= mw - 1u;
+    const bool two = mw != 0u;
+    const int jb = two ? off + __builtin_ctz(mw) : ja;
+    mw &= mw - 1u;
+    const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
+    const float4 b0 = st[0][jb], b1 = st[1][jb], b2 = st[2][jb];
+    float pa, pb;
+    const float ea = blend_power_exp<FAST>(q, a0, a1, pa);
+    const float eb = blend_power_exp<FAST>(q, b0, b1, pb);
+    blend_composite(q, pa, ea, a1, a2, true);
+    blend_composite(q, pb, eb, b1, b2, two);
+    mw = q.done ? 0u : mw;
+  }
 }
 
 // One wave = 16 pixel quads (2x2) of one tile, one lane per pixel: a block of
@@ -1327,8 +1351,8 @@ __device__ __forceinline__ bool quad_all(bool p) {
 // no pixel of the quad can take it ("blend culling").
 template <int BQW>
 __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wid = blockIdx.x * 4 + wave;
+  const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wid = blockIdx.x * GS_BLEND_WPG + wave;
   const int tile = wid / fp.chunks_per_tile;
   const int chunk = wid - tile * fp.chunks_per_tile;
   if (tile >= fp.n_tiles) return;
@@ -1380,7 +1404,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   const uint32_t* __restrict__ list = b.list + s;
 
   // wave-private staging of one batch of 64 records (48 B each) in LDS
-  __shared__ float4 s_rec[4][3][64];
+  __shared__ float4 s_rec[GS_BLEND_WPG][3][64];
   float4(*const st)[64] = s_rec[wave];
 
   // software pipeline: records of batch `base`, index of batch `base + 64`
@@ -1411,6 +1435,9 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     const int ry0 = (int)(boxy << 16) >> 16, ry1 = (int)boxy >> 16;
     const bool rok = have && !(a2.y == 0.0f) &&  // con_o.w == 0 (codelets.cpp:389)
                      rx0 <= rx1 && ry0 <= ry1;
+    // the batch takes the clamp-free exponential when every record's pcut
+    // is >= -80 (wave-uniform, so the record loop carries no per-step test)
+    const bool fast = __ballot(rok && !(a1.y >= -80.0f)) == 0ull;
     // prefetch the next batch
     g_cur = g_next;
     a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1426,7 +1453,26 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     // record k).  Blocks: per quad column / row one ballot, then each lane
     // ANDs its column's and row's masks; quad runs: one ballot per quad.
     unsigned long long m = 0ull;
-    if constexpr (BQW != 0) {
+    if constexpr (BQW != 0 && GS_BLEND_PIXEL_MASKS) {
+      // per-pixel masks: one ballot per pixel column / row of the block
+      const int bx = tile_x0 + q_x, by = tile_y0 + q_y;
+      const int c0 = rx0 - bx, c1 = rx1 - bx, w0 = ry0 - by, w1 = ry1 - by;
+      const int col = lx - q_x, row = ly - q_y;
+      unsigned long long mc = 0ull, mr = 0ull;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (c >= 2 * bqw) break;
+        const unsigned long long bc = __ballot(rok && c0 <= c && c <= c1);
+        mc = (col == c) ? bc : mc;
+      }
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        if (w >= 32 / bqw) break;
+        const unsigned long long br = __ballot(rok && w0 <= w && w <= w1);
+        mr = (row == w) ? br : mr;
+      }
+      m = mc & mr;
+    } else if constexpr (BQW != 0) {
       const int bx = tile_x0 + q_x, by = tile_y0 + q_y;
       const int c0 = (rx0 - bx) >> 1, c1 = (rx1 - bx) >> 1;  // quad columns / rows
       const int w0 = (ry0 - by) >> 1, w1 = (ry1 - by) >> 1;
@@ -1464,28 +1510,15 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (quad_all(q.done)) m = 0ull;
-    // two records per iteration, in list order (ascending bits): their
-    // exponentials are independent, the compositing is sequential
-    while (m) {
-      const int ja = __builtin_ctzll(m);
-      m &= m - 1ull;
-      const bool two = m != 0ull;
-      const int jb = two ? __builtin_ctzll(m) : ja;
-      m &= m - 1ull;
-      const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
-      const float4 b0 = st[0][jb], b1 = st[1][jb], b2 = st[2][jb];
-      float pa, pb, ea, eb;
-      if (a1.y >= -80.0f && b1.y >= -80.0f) {  // pcut
-        ea = blend_power_exp<true>(q, a0, a1, pa);
-        eb = blend_power_exp<true>(q, b0, b1, pb);
-      } else {
-        ea = blend_power_exp<false>(q, a0, a1, pa);
-        eb = blend_power_exp<false>(q, b0, b1, pb);
-      }
-      blend_composite(q, pa, ea, a1, a2, true);
-      blend_composite(q, pb, eb, b1, b2, two);
-      if (quad_all(q.done)) m = 0ull;  // the quad has saturated
+    // list order = ascending bits: the low word's records, then the high word's.
+    // Each lane leaves as soon as its own pixel has saturated.
+    const uint32_t m_lo = q.done ? 0u : (uint32_t)m, m_hi = (uint32_t)(m >> 32);
+    if (fast) {
+      blend_records<true>(q, st, m_lo, 0);
+      blend_records<true>(q, st, q.done ? 0u : m_hi, 32);
+    } else {
+      blend_records<false>(q, st, m_lo, 0);
+      blend_records<false>(q, st, q.done ? 0u : m_hi, 32);
     }
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
@@ -1543,13 +1576,14 @@ void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
   if (waves == 0) return;
-  const unsigned grid = (unsigned)((waves + 3) / 4);
+  const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
+  const unsigned block = 64 * GS_BLEND_WPG;
   if (fp.blend_bqw == 4)
-    gs_blend_kernel<4><<<grid, 256, 0, s>>>(fp, b);
+    gs_blend_kernel<4><<<grid, block, 0, s>>>(fp, b);
   else if (fp.blend_bqw == 8)
-    gs_blend_kernel<8><<<grid, 256, 0, s>>>(fp, b);
+    gs_blend_kernel<8><<<grid, block, 0, s>>>(fp, b);
   else
-    gs_blend_kernel<0><<<grid, 256, 0, s>>>(fp, b);
+    gs_blend_kernel<0><<<grid, block, 0, s>>>(fp, b);
 }
 
 }  // namespace gsk
