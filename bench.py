@@ -37,11 +37,17 @@ def parse():
     ap.add_argument("--scale-div", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--sh-degree", type=int, default=3)
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="frames in flight: independent renderers, each on its own stream "
-                    "(> 1 raises throughput; kernel durations then include the other frames' "
-                    "kernels, so the roofline is quoted at the default 1)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="frames in flight: independent renderers, each with its own buffers and "
+                    "HIP stream, take frames round-robin, so one frame's latency-bound kernels "
+                    "overlap the next frames' work (every frame is rendered in full)")
+    ap.add_argument("--profile-frames", type=int, default=24,
+                    help="frames of the isolated one-in-flight pass that times each kernel "
+                    "(stage HIP events) for the kernel table and the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="run the band copy + RCCL all-gather path even at N = 1 (a one-rank "
+                    "process group; exercises the multi-GPU frame path on one GPU)")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return ap.parse_args()
@@ -102,7 +108,8 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("bench.py --gpus N>1 must be launched with torchrun / torch.distributed.run")
     torch.cuda.set_device(local)
-    if world > 1:
+    dist_on = world > 1 or a.gather
+    if dist_on:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from gaussian_splat_ipu_amd import camera, scene
@@ -117,9 +124,10 @@ def main():
     fb = TiledFramebuffer(W, H, TW, TW)
     # N > 1: interleaved tile-row bands (rank r owns rows r, r + N, ...), so
     # every rank gets an equal share of the scene's dense centre rows.
-    # F frames in flight: F renderers (own buffers, own stream) take frames
-    # round-robin, so one frame's latency-bound kernels (scans, list tails)
-    # overlap the next frame's work.  Every frame is rendered in full.
+    # F frames in flight: F renderers (own buffers, own non-blocking stream
+    # created by libgsplat) take frames round-robin, so one frame's
+    # latency-bound kernels (scans, list tails) overlap the next frames' work.
+    # Every frame is rendered in full.
     F = max(1, a.inflight)
     R, streams = [], []
     for f in range(F):
@@ -128,22 +136,20 @@ def main():
         r.set_view_wire(view)
         r.set_projection_wire(proj)
         r.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
-        st = torch.cuda.Stream()
-        r.set_stream(st.cuda_stream)
         R.append(r)
-        streams.append(st)
+        streams.append(torch.cuda.ExternalStream(r.get_stream()))
     s = R[0]
-    # stage events on every 8th frame: each event costs device time, so the
-    # throughput run samples (the averages still come from the timed frames)
-    s.set_profile_interval(8)
+    # no stage events in the timed region (each costs host and device time);
+    # the kernel table comes from the isolated pass after it
+    s.set_profile_interval(1 << 30)
 
     # N > 1: frame k's band is copied out and all-gathered (RCCL) on a comm
     # stream while later frames render; one band / frame buffer per renderer.
     band_bytes = fb.rows_per_band_padded(world) * W * 3
-    nbuf = F if world > 1 else 0
+    nbuf = F if dist_on else 0
     band = [torch.empty(band_bytes, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     frame = [torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
-    comm = torch.cuda.Stream() if world > 1 else None
+    comm = torch.cuda.Stream() if dist_on else None
     ev_copy = [torch.cuda.Event() for _ in range(nbuf)]
     ev_free = [torch.cuda.Event() for _ in range(nbuf)]
     nframe = [0]
@@ -152,7 +158,7 @@ def main():
         i = nframe[0] % F
         r, st = R[i], streams[i]
         r.execute_async()
-        if world > 1:
+        if dist_on:
             st.wait_event(ev_free[i])  # the gather of frame k-F read band[i]
             r.copy_bgr8_device(band[i].data_ptr(), band_bytes)
             ev_copy[i].record(st)
@@ -171,24 +177,33 @@ def main():
         r.sync()
     torch.cuda.synchronize()
     s.reset_kernel_times()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_frame()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     t1 = time.perf_counter()
     for r in R:
         r.sync()  # raises on pair overflow
     elapsed = t1 - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = s.stats()
+    # kernel table: the same frames with one in flight (renderer 0 alone,
+    # stage HIP events on its stream around every kernel of every frame), so
+    # each duration is the kernel's own, not shared with other frames' work
+    s.set_profile_interval(1)
+    s.execute()
+    s.reset_kernel_times()
+    for _ in range(a.profile_frames):
+        s.execute_async()
+    s.sync()
     kt = s.kernel_times()
     fps = a.steps / elapsed
     ms_per_step = 1e3 * elapsed / a.steps
@@ -307,6 +322,7 @@ def main():
                 "resolution": [W, H],
                 "tile": [TW, TW],
                 "frames_in_flight": F,
+                "kernel_table": f"{a.profile_frames} frames, one in flight (stage HIP events)",
                 "parallelism": f"row-band x{world}" + (" (interleaved tile rows) + RCCL all-gather" if world > 1 else ""),
             },
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "n_pairs_binned", "max_list", "n_tiles",
@@ -318,7 +334,7 @@ def main():
         print(json.dumps(out), flush=True)
     for r in R:
         r.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

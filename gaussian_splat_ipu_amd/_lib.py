@@ -129,6 +129,7 @@ _SIGS = {
     "gs_set_projection": (C.c_int, [_P, _FP]),
     "gs_set_focal": (C.c_int, [_P, C.c_float, C.c_float]),
     "gs_set_stream": (C.c_int, [_P, _P]),
+    "gs_get_stream": (C.c_int, [_P, C.POINTER(_P)]),
     "gs_render": (C.c_int, [_P]),
     "gs_render_async": (C.c_int, [_P]),
     "gs_sync": (C.c_int, [_P]),

@@ -1011,42 +1011,48 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
   }
 }
 
-// Medium lists (kSortRegCap < L <= kSortLdsCap): the 4 waves sort 256-key
-// runs in registers (wave_bitonic<4>), then log2(runs) merge-path levels run
-// in LDS.  At every level each thread produces K = runs consecutive outputs:
-// a co-rank binary search finds where its first output comes from, then it
-// merges sequentially, holding the outputs in registers across the barrier
-// (the merge is in place).  The last level writes the list.  Work is
-// O(L log L) over L rounded up to 256, against O(L log^2 L) over L rounded up
-// to a power of two for a bitonic network.
+// Medium lists (kSortRegCap < L <= kSortLdsCap), one NT-thread workgroup:
+// the waves sort RUN = 64 E-key runs in registers (wave_bitonic<E>), then
+// log2(runs) merge-path levels run in LDS.  At every level each thread
+// produces K = ceil(npad / NT) consecutive outputs: a co-rank binary search
+// finds where its first output comes from, then it merges sequentially,
+// holding the outputs in registers across the barrier (the merge is in
+// place).  The last level writes the list.  Work is O(L log L) over L rounded
+// up to RUN, against O(L log^2 L) over L rounded up to a power of two for a
+// bitonic network.  NT = 256, E = 4: 4 waves, 256-key runs (throughput);
+// NT = 1024, E = 2: 16 waves, 128-key runs, at most 2 outputs per thread and
+// level (latency: one list per CU when few lists are long, e.g. row bands).
+template <int NT, int E>
 __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
                                                 unsigned long long* lds) {
+  constexpr int RUN = 64 * E, NW = NT / 64;
+  constexpr int KMAX = (kSortLdsCap + NT - 1) / NT;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int runs = (int)((L + 255u) >> 8);  // 3 .. 8 for medium lists
-  const int npad = runs << 8;
-  for (int r = wave; r < runs; r += 4) {
-    unsigned long long v[4];
+  const int runs = (int)((L + (uint32_t)RUN - 1u) / (uint32_t)RUN);
+  const int npad = runs * RUN;
+  for (int r = wave; r < runs; r += NW) {
+    unsigned long long v[E];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t i = (uint32_t)(r * 256 + lane * 4 + e);
+    for (int e = 0; e < E; ++e) {
+      const uint32_t i = (uint32_t)(r * RUN + lane * E + e);
       v[e] = i < L ? b.pairs[s + i] : ~0ull;
     }
-    wave_bitonic<4>(v, lane);
+    wave_bitonic<E>(v, lane);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) lds[r * 256 + lane * 4 + e] = v[e];
+    for (int e = 0; e < E; ++e) lds[r * RUN + lane * E + e] = v[e];
   }
   __syncthreads();
-  const int K = runs;
+  const int K = (npad + NT - 1) / NT;
   const int d0 = (int)threadIdx.x * K;
-  for (int w = 256;; w <<= 1) {  // runs == 1 degenerates to a copy
-    unsigned long long out[8];
+  for (int w = RUN;; w <<= 1) {  // runs == 1 degenerates to a copy
+    unsigned long long out[KMAX];
     int i = 0, j = 0, la = 0, lb = 0, abase = 0, bbase = 0;
     unsigned long long av = 0ull, bv = 0ull;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (k < K) {
-        const int d = d0 + k;
+    for (int k = 0; k < KMAX; ++k) {
+      const int d = d0 + k;
+      if (k < K && d < npad) {
         if (k == 0 || (d & (2 * w - 1)) == 0) {  // (re)locate: first output or a new pair
           abase = d & ~(2 * w - 1);
           bbase = abase + w;
@@ -1078,12 +1084,12 @@ __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, ui
     __syncthreads();
     if (2 * w < npad) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k < K) lds[d0 + k] = out[k];
+      for (int k = 0; k < KMAX; ++k)
+        if (k < K && d0 + k < npad) lds[d0 + k] = out[k];
       __syncthreads();
     } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < KMAX; ++k)
         if (k < K && d0 + k < (int)L) b.list[s + d0 + k] = b.inv_perm[(uint32_t)out[k]];
       break;
     }
@@ -1183,20 +1189,27 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
 
 // Big, medium and small lists in one launch, longest first: workgroups
 // [0, n_big) radix-sort one big list each (> kSortLdsCap); the next n_medium
-// each sort one medium list (512 < L <= 2048: 4 waves x E keys in registers,
-// the strides >= 64 E through LDS); the rest give each of their waves one
-// small list (L <= 512, sorted in one wave's registers).  Keys are unique (the
-// input index is in the low word), so the order is total and deterministic.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
+// each sort one medium list (kSortRegCap < L <= kSortLdsCap, merge_sort_tile);
+// the rest give each of their waves one small list (L <= kSortRegCap, sorted
+// in one wave's registers).  Keys are unique (the input index is in the low
+// word), so the order is total and deterministic.  NT = 256: 8 workgroups
+// per CU.  (1024-thread workgroups, 16 waves per list, cut a 1000-key list's
+// sort from ~24 to ~12 us when alone, but hold one workgroup per CU and ran
+// no faster in a row band and 2.4x slower on the full frame.)
+template <int NT>
+__device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers& b) {
+  constexpr int NW = NT / 64;
   // the radix path's histograms alias the merge path's key buffer (a
-  // workgroup takes one path): 16 KB per workgroup, 8 workgroups per CU
-  __shared__ unsigned long long keys[kSortLdsCap];
+  // workgroup takes one path)
+  constexpr int kRadixWords = 512 + NW * 256;
+  constexpr int kWords = 2 * kSortLdsCap > kRadixWords ? 2 * kSortLdsCap : kRadixWords;
+  __shared__ unsigned long long keys[kWords / 2];
   uint32_t* const r_hist = (uint32_t*)keys;
   uint32_t* const r_base = r_hist + 256;
   uint32_t(*const r_wcnt)[256] = (uint32_t(*)[256])(r_hist + 512);
   const uint32_t n_big = b.counters[0];
   if (blockIdx.x < n_big) {  // the longest lists first
-    radix_sort_tile<256>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
+    radix_sort_tile<NT>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
     return;
   }
   const uint32_t n_med = b.counters[7], n_small = b.counters[9];
@@ -1204,11 +1217,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   if (item < n_med) {
     uint32_t s, L;
     tile_segment(fp, b, (int)b.medium_tiles[item], s, L);
-    merge_sort_tile(b, s, L, keys);
+    merge_sort_tile<NT, NT == 256 ? 4 : 2>(b, s, L, keys);
     return;
   }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t k = (item - n_med) * 4u + (uint32_t)wave;
+  const uint32_t k = (item - n_med) * (uint32_t)NW + (uint32_t)wave;
   if (k >= n_small) return;
   const int lane = threadIdx.x & 63;
   uint32_t s, L;
@@ -1219,6 +1232,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     wave_sort_tile<2>(b, s, L, lane);
   else
     wave_sort_tile<4>(b, s, L, lane);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
+  sort_tiles<256>(fp, b);
 }
 
 // -------------------------------------------------------------------- blend
@@ -1569,7 +1586,7 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
-  // big + medium + ceil(small / 4) <= n_tiles + 1 workgroups do work
+  // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
 }
 

@@ -579,6 +579,12 @@ int gs_set_stream(gs_renderer* r, void* hip_stream) {
   return GS_OK;
 }
 
+int gs_get_stream(gs_renderer* r, void** hip_stream) {
+  if (!r || !hip_stream) return GS_EINVAL;
+  *hip_stream = (void*)r->stream;
+  return GS_OK;
+}
+
 int gs_render_async(gs_renderer* r) {
   if (!r) return GS_EINVAL;
   int rc = select_device(r);

@@ -154,6 +154,13 @@ class GpuSplatter:
         check(lib().gs_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
 
     # ------------------------------------------------------------ execute
+    def get_stream(self) -> int:
+        """hipStream_t (as int) the frames are enqueued on; wrap it with
+        torch.cuda.ExternalStream to order work after a frame."""
+        s = C.c_void_p()
+        check(lib().gs_get_stream(self._h, C.byref(s)))
+        return int(s.value or 0)
+
     def execute(self) -> None:
         """GraphManager::execute -> IpuSplatter::execute (blocking)."""
         check(lib().gs_render(self._h), "gs_render")

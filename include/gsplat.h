@@ -155,6 +155,10 @@ int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor);
 /* HIP stream (hipStream_t as void*) the frame is enqueued on; NULL = the
  * renderer's own stream. */
 int gs_set_stream(gs_renderer* r, void* hip_stream);
+/* The HIP stream frames are currently enqueued on (the renderer's own
+ * non-blocking stream unless gs_set_stream chose another), e.g. to order a
+ * caller's copy or collective after the frame. */
+int gs_get_stream(gs_renderer* r, void** hip_stream);
 
 /* ------------------------------------------------------------ execute */
 /* Replaces GraphManager::execute -> IpuSplatter::execute (ipu_rasteriser.cpp:

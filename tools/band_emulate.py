@@ -1,0 +1,91 @@
+"""Multi-GPU critical path on ONE GPU: render each band of an N-way row split
+(band_count = N, the bench's band flags) on this device, one band at a time,
+and time its frames.  The slowest band bounds the N-GPU frame rate before the
+all-gather (which bench.py overlaps with the next frame).
+
+  python tools/band_emulate.py [--bands 1,2,4,8] [--steps 100] [--inflight 1]
+                               [--contiguous] [--no-cull]
+
+Prints one line per N: per-band us/frame, the slowest band, and the speed-up
+over N = 1.  Kernel stage times of the slowest band come from the renderer's
+sampled HIP events (GS_FLAG_PROFILE).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bands", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--inflight", type=int, default=1)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--contiguous", action="store_true")
+    ap.add_argument("--no-cull", action="store_true")
+    ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
+    a = ap.parse_args()
+    import torch
+
+    from gaussian_splat_ipu_amd import camera, scene
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    W, H, TW = 1920, 1080, 16
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=a.n, seed=1, sh_degree=3)))
+    view, proj = camera.headless(bb, W, H)
+    fb = TiledFramebuffer(W, H, TW, TW)
+    base = None
+    for N in [int(v) for v in a.bands.split(",")]:
+        per_band, stages = [], []
+        for r in range(N):
+            if a.only_band >= 0 and r != a.only_band:
+                continue
+            R, S = [], []
+            for f in range(a.inflight):
+                s = GpuSplatter(g, fb, device=0, band_index=r, band_count=N, profile=(f == 0),
+                                band_interleaved=(N > 1 and not a.contiguous),
+                                band_cull=(N > 1 and not a.no_cull), write_rgba=False)
+                s.set_view_wire(view)
+                s.set_projection_wire(proj)
+                s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+                st = torch.cuda.Stream()
+                s.set_stream(st.cuda_stream)
+                s.set_profile_interval(4)
+                R.append(s)
+                S.append(st)
+            for s in R:
+                s.execute()
+            for k in range(a.warmup):
+                R[k % len(R)].execute_async()
+            torch.cuda.synchronize()
+            R[0].reset_kernel_times()
+            t0 = time.perf_counter()
+            for k in range(a.steps):
+                R[k % len(R)].execute_async()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / a.steps
+            for s in R:
+                s.sync()
+            per_band.append(dt * 1e6)
+            stages.append({k: round(v[0] * 1e3, 1) for k, v in R[0].kernel_times().items()})
+            pairs = R[0].stats()["n_pairs"]
+            for s in R:
+                s.close()
+            del pairs
+        worst = max(per_band)
+        if base is None:
+            base = worst
+        i = per_band.index(worst)
+        print(json.dumps({"bands": N, "inflight": a.inflight, "us_per_frame_by_band": [round(v, 1) for v in per_band],
+                          "slowest_us": round(worst, 1), "speedup": round(base / worst, 2),
+                          "slowest_band_stage_us": stages[i]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

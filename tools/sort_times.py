@@ -10,13 +10,15 @@ W, H, TW = 1920, 1080, 16
 g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=1_000_000, seed=1, sh_degree=3)))
 view, proj = camera.headless(bb, W, H)
 fb = TiledFramebuffer(W, H, TW, TW)
-with GpuSplatter(g, fb, device=0) as s:
+NB = int(os.environ.get('BANDS', '1'))
+with GpuSplatter(g, fb, device=0, band_index=min(2, NB - 1), band_count=NB, band_interleaved=NB > 1, band_cull=NB > 1) as s:
     s.set_view_wire(view); s.set_projection_wire(proj); s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
     for _ in range(5):
         s.execute()
     rgba = s.get_rgba()
 u = rgba.reshape(-1, 4).view(np.uint32)
-nwg = 8160 + 8160 // 4
+nt = s_ntiles if False else None
+nwg = int(os.environ.get('NWG', '10200'))
 u = u[:nwg]
 t0, t1, L, C = [u[:, i].astype(np.int64) for i in range(4)]
 ok = t1 > 0

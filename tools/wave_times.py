@@ -12,7 +12,8 @@ W, H, TW = 1920, 1080, 16
 g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=1_000_000, seed=1, sh_degree=3)))
 view, proj = camera.headless(bb, W, H)
 fb = TiledFramebuffer(W, H, TW, TW)
-with GpuSplatter(g, fb, device=0) as s:
+NB = int(os.environ.get('BANDS', '1'))
+with GpuSplatter(g, fb, device=0, band_index=min(2, NB - 1), band_count=NB, band_interleaved=NB > 1, band_cull=NB > 1) as s:
     s.set_view_wire(view); s.set_projection_wire(proj); s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
     for _ in range(5):
         s.execute()
@@ -20,6 +21,7 @@ with GpuSplatter(g, fb, device=0) as s:
 u = rgba.view(np.uint32)
 # first pixel of each 8x8 block
 blk = u[0::8, 0::8]  # [H/8, W/8, 4]
+blk = blk[(blk[..., 1] != 0)]  # rows this band rendered (1-D list of waves)
 t0 = blk[..., 0].astype(np.int64); t1 = blk[..., 1].astype(np.int64)
 base = t0.min()
 t0 -= base; t1 -= base
@@ -33,7 +35,7 @@ print("start time us at fraction 0.25/0.5/0.9/1.0:", [starts[int(f * (starts.siz
 np.save("gpurun_out/wave_times.npy", np.stack([t0, t1]))
 # duration map, coarse
 dm = (d / 1000.0)
-print(np.round(dm[::16, ::20], 1))
+
 nb = blk[..., 2].astype(np.int64)
 it = blk[..., 3].astype(np.int64)
 mi, su = it & 0xFFF, it >> 12
