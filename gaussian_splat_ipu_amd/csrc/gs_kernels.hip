@@ -22,13 +22,13 @@
 // the IEEE operations written (and matches the CPU oracle bit for bit).
 #include "gs_kernels.hpp"
 
-// blend: 1 = one record mask per pixel, 0 = per 2x2 quad (A/B switch)
+// blend: 1 = one record mask per pixel (blend 82 -> 78 us), 0 = per 2x2 quad
 // blend: waves per workgroup (the waves are independent)
 #ifndef GS_BLEND_WPG
 #define GS_BLEND_WPG 4
 #endif
 #ifndef GS_BLEND_PIXEL_MASKS
-#define GS_BLEND_PIXEL_MASKS 0
+#define GS_BLEND_PIXEL_MASKS 1
 #endif
 
 namespace gsk {
@@ -67,6 +67,10 @@ __device__ __forceinline__ float gs_expf(float x) {
   res = (x > 88.72283935546875f) ? __builtin_huge_valf() : res;
   return (x != x) ? x : res;
 }
+
+// Wave ballot of a bool.  HIP's __ballot(int) turns the bool into 0 / 1 in a
+// VGPR and compares it again; the builtin takes the lane mask as is.
+__device__ __forceinline__ unsigned long long ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 __device__ __forceinline__ float smax(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float smin(float a, float b) { return a < b ? a : b; }
@@ -578,7 +582,7 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
         const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
         const uint32_t qx = (uint32_t)__shfl_up((int)q.x, 1, 64), qy = (uint32_t)__shfl_up((int)q.y, 1, 64);
         const bool start = lane == 0 || r.x != px || r.y != py || q.x != qx || q.y != qy;
-        const unsigned long long st = __ballot(start);
+        const unsigned long long st = ballot64(start);
         const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
         const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
         const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
@@ -605,7 +609,7 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
     const uint2 r = i < g1 ? b.rect[i] : kEmptyRect;
     const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
     const bool start = lane == 0 || r.x != px || r.y != py;
-    const unsigned long long st = __ballot(start);
+    const unsigned long long st = ballot64(start);
     const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
     const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
     const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
@@ -673,9 +677,9 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
       mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
     }
     const int cl = sort_class(L);
-    const uint32_t ns = (uint32_t)__popcll(__ballot(ok && cl == 0));
-    const uint32_t nm = (uint32_t)__popcll(__ballot(ok && cl == 1));
-    const uint32_t nb = (uint32_t)__popcll(__ballot(ok && cl == 2));
+    const uint32_t ns = (uint32_t)__popcll(ballot64(ok && cl == 0));
+    const uint32_t nm = (uint32_t)__popcll(ballot64(ok && cl == 1));
+    const uint32_t nb = (uint32_t)__popcll(ballot64(ok && cl == 2));
     if (lane == 0)
       b.tile_agg[2 * blockIdx.x] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), ns | (nm << 8) | (nb << 16), mx);
   }
@@ -753,8 +757,8 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
     const unsigned long long start = ps + inc - c;
     const int cl = sort_class(c);
     const unsigned long long lt = (1ull << lane) - 1ull;
-    const unsigned long long m0 = __ballot(ok && cl == 0), m1 = __ballot(ok && cl == 1),
-                             m2 = __ballot(ok && cl == 2);
+    const unsigned long long m0 = ballot64(ok && cl == 0), m1 = ballot64(ok && cl == 1),
+                             m2 = ballot64(ok && cl == 2);
     if (ok) {
       b.tile_start[t] = (uint32_t)(start < 0xFFFFFFFFull ? start : 0xFFFFFFFFull);
       if (cl == 0) b.small_tiles[pq[0] + (uint32_t)__popcll(m0 & lt)] = (uint32_t)t;
@@ -1150,11 +1154,11 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
       const bool valid = i < L;
       const unsigned long long key = valid ? src[i] : 0ull;
       const uint32_t d = (uint32_t)(key >> shift) & 255u;
-      unsigned long long m = __ballot(valid);
+      unsigned long long m = ballot64(valid);
 #pragma unroll
       for (int bit = 0; bit < 8; ++bit) {
         const bool set = (d >> bit) & 1u;
-        const unsigned long long bb = __ballot(set);
+        const unsigned long long bb = ballot64(set);
         m &= set ? bb : ~bb;
       }
       const uint32_t rank = (uint32_t)__popcll(m & lt_mask);
@@ -1441,7 +1445,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   uint32_t g_next = load_idx(64 + lane);
 
   for (uint32_t base = 0; base < L; base += 64) {
-    if (__ballot(!q.done) == 0ull) break;
+    if (ballot64(!q.done) == 0ull) break;
     // stage this batch
     const bool have = g_cur != 0xFFFFFFFFu;
     st[0][lane] = a0;
@@ -1454,7 +1458,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
                      rx0 <= rx1 && ry0 <= ry1;
     // the batch takes the clamp-free exponential when every record's pcut
     // is >= -80 (wave-uniform, so the record loop carries no per-step test)
-    const bool fast = __ballot(rok && !(a1.y >= -80.0f)) == 0ull;
+    const bool fast = ballot64(rok && !(a1.y >= -80.0f)) == 0ull;
     // prefetch the next batch
     g_cur = g_next;
     a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1470,42 +1474,27 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     // record k).  Blocks: per quad column / row one ballot, then each lane
     // ANDs its column's and row's masks; quad runs: one ballot per quad.
     unsigned long long m = 0ull;
-    if constexpr (BQW != 0 && GS_BLEND_PIXEL_MASKS) {
-      // per-pixel masks: one ballot per pixel column / row of the block
+    if constexpr (BQW != 0) {
+      // Quad (or pixel, GS_BLEND_PIXEL_MASKS) columns and rows of the block:
+      // one ballot per column / row, each a single unsigned compare
+      // (c - lo <= span; a lane without a record never matches), then each
+      // lane selects its column's and row's masks and ANDs them.
+      constexpr int SH = GS_BLEND_PIXEL_MASKS ? 0 : 1;
+      constexpr int NC = (2 * bqw) >> SH, NR = (32 / bqw) >> SH;
       const int bx = tile_x0 + q_x, by = tile_y0 + q_y;
-      const int c0 = rx0 - bx, c1 = rx1 - bx, w0 = ry0 - by, w1 = ry1 - by;
-      const int col = lx - q_x, row = ly - q_y;
+      const int xlo = rok ? (rx0 - bx) >> SH : 0x40000000, xsp = rok ? ((rx1 - bx) >> SH) - xlo : 0;
+      const int ylo = rok ? (ry0 - by) >> SH : 0x40000000, ysp = rok ? ((ry1 - by) >> SH) - ylo : 0;
+      const int mycol = (lx - q_x) >> SH, myrow = (ly - q_y) >> SH;
       unsigned long long mc = 0ull, mr = 0ull;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        if (c >= 2 * bqw) break;
-        const unsigned long long bc = __ballot(rok && c0 <= c && c <= c1);
-        mc = (col == c) ? bc : mc;
+      for (int c = 0; c < NC; ++c) {
+        const unsigned long long bc = ballot64((uint32_t)(c - xlo) <= (uint32_t)xsp);
+        mc = (mycol == c) ? bc : mc;
       }
 #pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        if (w >= 32 / bqw) break;
-        const unsigned long long br = __ballot(rok && w0 <= w && w <= w1);
-        mr = (row == w) ? br : mr;
-      }
-      m = mc & mr;
-    } else if constexpr (BQW != 0) {
-      const int bx = tile_x0 + q_x, by = tile_y0 + q_y;
-      const int c0 = (rx0 - bx) >> 1, c1 = (rx1 - bx) >> 1;  // quad columns / rows
-      const int w0 = (ry0 - by) >> 1, w1 = (ry1 - by) >> 1;
-      const int qx = myq % bqw, qy = myq / bqw;
-      unsigned long long mc = 0ull, mr = 0ull;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        if (c >= bqw) break;
-        const unsigned long long bc = __ballot(rok && c0 <= c && c <= c1);
-        mc = (qx == c) ? bc : mc;
-      }
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        if (w >= 16 / bqw) break;
-        const unsigned long long br = __ballot(rok && w0 <= w && w <= w1);
-        mr = (qy == w) ? br : mr;
+      for (int w = 0; w < NR; ++w) {
+        const unsigned long long br = ballot64((uint32_t)(w - ylo) <= (uint32_t)ysp);
+        mr = (myrow == w) ? br : mr;
       }
       m = mc & mr;
     } else {
@@ -1514,7 +1503,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
       for (int t = 0; t < 16; ++t) {
         const int X0 = tile_x0 + cx, Y0 = tile_y0 + cy;
         const bool h = rok && t < nq_wave && !(rx0 > X0 + 1 || rx1 < X0 || ry0 > Y0 + 1 || ry1 < Y0);
-        const unsigned long long bt = __ballot(h);
+        const unsigned long long bt = ballot64(h);
         m = (myq == t) ? bt : m;
         cx += 2;
         if (cx >= (qw << 1)) {
@@ -1542,6 +1531,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   }
   if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
+
 
 }  // namespace
 
