@@ -215,8 +215,20 @@ __device__ __forceinline__ void alpha_footprint(float mx, float my, float k0, fl
 }
 
 // ------------------------------------------------------------------ project
+// x / d.  P2: d is a power of two (FrameParams::pow2), so x * (1 / d) is the
+// same correctly rounded value (scaling by 2^k is exact; both round the same
+// real number), and a non-negative int divided by 2^k is a shift.
+template <bool P2>
+__device__ __forceinline__ float div_p2(float x, float d, float inv_d) {
+  return P2 ? x * inv_d : x / d;
+}
+template <bool P2>
+__device__ __forceinline__ int idiv_p2(int x, int d, int sh) {  // x >= 0
+  return P2 ? x >> sh : x / d;
+}
 // The band rows [yb0, yb1] (band-local) among absolute tile rows [fy0, fy1]
 // (clamped to the frame); empty when yb0 > yb1.
+template <bool P2>
 __device__ __forceinline__ void band_rows_of(const FrameParams& fp, float fy0, float fy1, int& yb0,
                                              int& yb1) {
   const float gy1 = (float)(fp.tiles_y - 1);
@@ -226,8 +238,9 @@ __device__ __forceinline__ void band_rows_of(const FrameParams& fp, float fy0, f
   yb1 = -1;
   if (fy0 <= fy1) {
     const int a0 = (int)fy0 - fp.band_ty0, a1 = (int)fy1 - fp.band_ty0, S = fp.band_stride;
-    yb0 = a0 <= 0 ? 0 : (a0 + S - 1) / S;
-    yb1 = a1 < 0 ? -1 : min(a1 / S, fp.band_nrows - 1);
+    // P2: S = 2^sh_stride, and both numerators are >= 0 here
+    yb0 = a0 <= 0 ? 0 : (P2 ? (a0 + S - 1) >> fp.sh_stride : (a0 + S - 1) / S);
+    yb1 = a1 < 0 ? -1 : min(P2 ? a1 >> fp.sh_stride : a1 / S, fp.band_nrows - 1);
   }
 }
 
@@ -242,27 +255,36 @@ __device__ __forceinline__ void band_rows_of(const FrameParams& fp, float fy0, f
 // The bound is inflated by 5 % + 2 px against fp32 rounding, and the tile-row
 // range is computed with the rectangle's own (monotone) formulas from the same
 // vy, so it contains the true rows.  Non-finite values never cull.
+template <bool P2>
 __device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, const M3& T, float4 sg) {
   float t2 = 0.0f;
 #pragma unroll
   for (int c = 0; c < 3; ++c)
 #pragma unroll
     for (int r = 0; r < 3; ++r) t2 += T.m[c][r] * T.m[c][r];
-  const float smax = fmaxf(fmaxf(sg.x, sg.y), sg.z) / fp.scale_div;
+  const float smax = div_p2<P2>(fmaxf(fmaxf(sg.x, sg.y), sg.z), fp.scale_div, fp.inv_sd);
   const float lc = __expf(2.0f * smax) * 1.01f;
   const float r = 3.0f * __builtin_sqrtf(1.05f * (2.0f * lc * t2) + 1.0f) + 2.0f;
   if (!(__builtin_fabsf(vy) < 1e30f) || !(r < 1e30f)) return false;
-  const float fy0 = __builtin_floorf(__builtin_floorf(vy - r) / fp.th);
-  const float fy1 = __builtin_floorf(__builtin_ceilf(vy + r) / fp.th);
+  const float fy0 = __builtin_floorf(div_p2<P2>(__builtin_floorf(vy - r), fp.th, fp.inv_th));
+  const float fy1 = __builtin_floorf(div_p2<P2>(__builtin_ceilf(vy + r), fp.th, fp.inv_th));
   int yb0, yb1;
-  band_rows_of(fp, fy0, fy1, yb0, yb1);
+  band_rows_of<P2>(fp, fy0, fy1, yb0, yb1);
   return yb0 > yb1;
 }
 
+template <bool P2>
 __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i) {
   bool rendered = false;
   const float4 mean = b.mean[i];
   const float4 sg = b.scale_gid[i];
+  // without the band cull every live Gaussian needs its colour and rotation:
+  // load them with the mean (one memory round trip instead of two)
+  float4 col = make_float4(0.f, 0.f, 0.f, 0.f), rot = col;
+  if (!fp.band_cull) {
+    col = b.colour[i];
+    rot = b.rot[i];
+  }
   float4* rec = b.rec + 3 * (size_t)i;  // 48-B record
   uint2 rect = kEmptyRect, crect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
@@ -308,16 +330,19 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
 #pragma unroll
       for (int r = 0; r < 3; ++r) W.m[c][r] = m[c * 4 + r];
     const M3 T = m3_mul(W, J);
-    if (fp.band_cull && band_culled(fp, vy, T, sg)) {
+    if (fp.band_cull && band_culled<P2>(fp, vy, T, sg)) {
       // no tile row in this band: empty rectangle; the record is never read
       b.rect[i] = rect;
       if (fp.pair_cull) b.crect[i] = crect;
       b.depth_key[i] = dkey;
       return false;
     }
-    const float4 col = b.colour[i];
-    const float4 rot = b.rot[i];
-    const M3 C3 = cov3d(rot, sg.x / fp.scale_div, sg.y / fp.scale_div, sg.z / fp.scale_div);
+    if (fp.band_cull) {
+      col = b.colour[i];
+      rot = b.rot[i];
+    }
+    const M3 C3 = cov3d(rot, div_p2<P2>(sg.x, fp.scale_div, fp.inv_sd), div_p2<P2>(sg.y, fp.scale_div, fp.inv_sd),
+                        div_p2<P2>(sg.z, fp.scale_div, fp.inv_sd));
     M3 cov = m3_mul(m3_mul(m3_t(T), m3_t(C3)), T);
     const float a = cov.m[0][0] + 0.3f;
     const float bb = cov.m[0][1];
@@ -353,16 +378,16 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       rendered = true;
       dkey = depth_key_of(cz);
       // converged lattice rectangle
-      float fx0 = __builtin_floorf(__builtin_floorf(minx) / fp.tw);
-      float fx1 = __builtin_floorf(__builtin_ceilf(maxx) / fp.tw);
-      float fy0 = __builtin_floorf(__builtin_floorf(miny) / fp.th);
-      float fy1 = __builtin_floorf(__builtin_ceilf(maxy) / fp.th);
+      float fx0 = __builtin_floorf(div_p2<P2>(__builtin_floorf(minx), fp.tw, fp.inv_tw));
+      float fx1 = __builtin_floorf(div_p2<P2>(__builtin_ceilf(maxx), fp.tw, fp.inv_tw));
+      float fy0 = __builtin_floorf(div_p2<P2>(__builtin_floorf(miny), fp.th, fp.inv_th));
+      float fy1 = __builtin_floorf(div_p2<P2>(__builtin_ceilf(maxy), fp.th, fp.inv_th));
       const float gx1 = (float)(fp.tiles_x - 1);
       if (fx0 < 0.0f) fx0 = 0.0f;
       if (fx1 > gx1) fx1 = gx1;
       // this band's rows among the absolute rows [fy0, fy1]
       int yb0, yb1;
-      band_rows_of(fp, fy0, fy1, yb0, yb1);
+      band_rows_of<P2>(fp, fy0, fy1, yb0, yb1);
       if (fx0 <= fx1 && yb0 <= yb1) {
         const uint32_t x0 = (uint32_t)(int)fx0, x1 = (uint32_t)(int)fx1;
         const uint32_t y0 = (uint32_t)yb0, y1 = (uint32_t)yb1;
@@ -373,12 +398,12 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
           // so leaving it out of that tile's list changes no pixel
           const int bx0 = (int)(b01 << 16) >> 16, bx1 = (int)b01 >> 16;
           const int by0 = (int)(b23 << 16) >> 16, by1 = (int)b23 >> 16;
-          const int cx0 = max((int)x0, max(bx0, 0) / fp.tile_w);
-          const int cx1 = min((int)x1, bx1 < 0 ? -1 : bx1 / fp.tile_w);
-          const float gy0 = smax(fy0, (float)(max(by0, 0) / fp.tile_h));
-          const float gy1 = smin(fy1, by1 < 0 ? -1.0f : (float)(by1 / fp.tile_h));
+          const int cx0 = max((int)x0, idiv_p2<P2>(max(bx0, 0), fp.tile_w, fp.sh_tw));
+          const int cx1 = min((int)x1, bx1 < 0 ? -1 : idiv_p2<P2>(bx1, fp.tile_w, fp.sh_tw));
+          const float gy0 = smax(fy0, (float)idiv_p2<P2>(max(by0, 0), fp.tile_h, fp.sh_th));
+          const float gy1 = smin(fy1, by1 < 0 ? -1.0f : (float)idiv_p2<P2>(by1, fp.tile_h, fp.sh_th));
           int cy0, cy1;
-          band_rows_of(fp, gy0, gy1, cy0, cy1);
+          band_rows_of<P2>(fp, gy0, gy1, cy0, cy1);
           crect = (cx0 <= cx1 && cy0 <= cy1 && bx0 <= bx1 && by0 <= by1)
                       ? make_uint2((uint32_t)cx0 | ((uint32_t)cx1 << 16),
                                    (uint32_t)cy0 | ((uint32_t)cy1 << 16))
@@ -401,10 +426,11 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   return rendered;
 }
 
+template <bool P2>
 __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool rendered = false;
-  if (i < fp.n) rendered = project_one(fp, b, i);
+  if (i < fp.n) rendered = project_one<P2>(fp, b, i);
   // V per workgroup (summed by the scan kernel): no single-address atomics
   const int v = __syncthreads_count(rendered);
   if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
@@ -1537,7 +1563,10 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
-  gs_project_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+  if (fp.pow2)
+    gs_project_kernel<true><<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+  else
+    gs_project_kernel<false><<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
 }
 
 size_t bin_lds_bytes(int n_tiles) { return (size_t)((n_tiles + 1) / 2) * 4; }

@@ -236,6 +236,23 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.n_chunks = r->n_chunks;
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
+  {
+    auto log2_exact = [](double v, int& sh) -> bool {  // v == 2^sh, sh in [-126, 126]
+      int e = 0;
+      const double m = std::frexp(v, &e);  // v = m * 2^e, m in [0.5, 1)
+      sh = e - 1;
+      return v > 0.0 && m == 0.5 && sh >= -126 && sh <= 126;
+    };
+    int stw = 0, sth = 0, sst = 0, ssd = 0;
+    fp.pow2 = (log2_exact(fp.tile_w, stw) && log2_exact(fp.tile_h, sth) && log2_exact(fp.band_stride, sst) &&
+               log2_exact(fp.scale_div, ssd)) ? 1 : 0;
+    fp.sh_tw = stw;
+    fp.sh_th = sth;
+    fp.sh_stride = sst;
+    fp.inv_tw = std::ldexp(1.0f, -stw);
+    fp.inv_th = std::ldexp(1.0f, -sth);
+    fp.inv_sd = std::ldexp(1.0f, -ssd);
+  }
   return fp;
 }
 
