@@ -1049,9 +1049,10 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
 // holding the outputs in registers across the barrier (the merge is in
 // place).  The last level writes the list.  Work is O(L log L) over L rounded
 // up to RUN, against O(L log^2 L) over L rounded up to a power of two for a
-// bitonic network.  NT = 256, E = 4: 4 waves, 256-key runs (throughput);
-// NT = 1024, E = 2: 16 waves, 128-key runs, at most 2 outputs per thread and
-// level (latency: one list per CU when few lists are long, e.g. row bands).
+// bitonic network.  E = 2 (128-key runs, one more merge level than 256-key
+// runs): the register bitonic phase was 80 % of a medium sort (per-workgroup
+// timestamps, tools/sort_times.py), and E = 2 took the sort from 45.0 to
+// 43.2 us; E = 1 took 49.1.
 template <int NT, int E>
 __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
                                                 unsigned long long* lds) {
@@ -1247,7 +1248,7 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   if (item < n_med) {
     uint32_t s, L;
     tile_segment(fp, b, (int)b.medium_tiles[item], s, L);
-    merge_sort_tile<NT, NT == 256 ? 4 : 2>(b, s, L, keys);
+    merge_sort_tile<NT, 2>(b, s, L, keys);
     return;
   }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

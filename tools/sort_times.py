@@ -39,3 +39,11 @@ if sel.any():
             print(f"  medium L in ({lo},{hi}]: n={m.sum()} mean dur us {((t1 - t0)[m] * 10 / 1000).mean():.2f}")
 tt = np.arange(0, t1.max() / 100 + 1, 2.0)
 print("live WGs over time:", [int(((t0 / 100 <= t) & (t1 / 100 > t)).sum()) for t in tt])
+# phase split of the medium sorts (t_sortphase build: column 3 holds the
+# timestamp after the register bitonic runs instead of the class)
+u2 = rgba.reshape(-1, 4).view(np.uint32)[:nwg]
+tb = u2[:, 3].astype(np.int64)
+med = (tb > 1000) & ok
+if med.any():
+    s0 = u2[med, 0].astype(np.int64); s1 = u2[med, 1].astype(np.int64); sb = tb[med]
+    print("medium phase us: bitonic (load+sort) mean", ((sb - s0) * 10 / 1000).mean(), " merge+store mean", ((s1 - sb) * 10 / 1000).mean())
