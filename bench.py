@@ -45,6 +45,10 @@ def parse():
                     help="frames of the isolated one-in-flight pass that times each kernel "
                     "(stage HIP events) for the kernel table and the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config5", action="store_true",
+                    help="BASELINE.json configs[4]: 8M Gaussians clustered around point_cloud_12's "
+                    "positions (N(0, 0.02) jitter, seed 8), 3840x2160, orbit camera (frame k: "
+                    "mvpStart * Ry(360 k / 120)); the tile load-imbalance stress")
     ap.add_argument("--gather", action="store_true",
                     help="run the band copy + RCCL all-gather path even at N = 1 (a one-rank "
                     "process group; exercises the multi-GPU frame path on one GPU)")
@@ -97,6 +101,9 @@ def alg_bytes(kernel: str, st: dict, n: int, px: int) -> float:
 
 def main():
     a = parse()
+    if a.config5:
+        a.n, a.width, a.height, a.seed, a.sh_degree = 8_000_000, 3840, 2160, 8, 0
+        a.cpu_frames = 1
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -117,7 +124,14 @@ def main():
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
 
     W, H, TW = a.width, a.height, a.tile
-    ply = scene.synthetic(scene.SynthSpec(n=a.n, seed=a.seed, sh_degree=a.sh_degree))
+    if a.config5:
+        src = scene.load_ply(os.path.join(ROOT, "tests", "golden", "point_cloud_12.ply"))
+        centres = np.stack([src["x"], src["y"], src["z"]], 1)
+        ply = scene.synthetic(scene.SynthSpec(n=a.n, seed=a.seed, sh_degree=a.sh_degree,
+                                              cluster_xyz=centres, cluster_sigma=0.02))
+        del src, centres
+    else:
+        ply = scene.synthetic(scene.SynthSpec(n=a.n, seed=a.seed, sh_degree=a.sh_degree))
     g, bb = scene.prepare_scene(ply)
     del ply
     view, proj = camera.headless(bb, W, H)
@@ -154,9 +168,13 @@ def main():
     ev_free = [torch.cuda.Event() for _ in range(nbuf)]
     nframe = [0]
 
+    views = [camera.orbit_view(k) for k in range(120)] if a.config5 else None
+
     def one_frame():
         i = nframe[0] % F
         r, st = R[i], streams[i]
+        if views is not None:  # orbit camera: a new view every frame
+            r.set_view_wire(views[nframe[0] % 120])
         r.execute_async()
         if dist_on:
             st.wait_event(ev_free[i])  # the gather of frame k-F read band[i]
@@ -168,9 +186,13 @@ def main():
                 ev_free[i].record(comm)
         nframe[0] += 1
 
-    # warm-up (the first blocking render sizes the pair buffers)
+    # warm-up (the first blocking render sizes the pair buffers; with the
+    # orbit camera every view once, so no timed frame can overflow them)
     for r in R:
-        r.execute()
+        for v in (views if views is not None else [None]):
+            if v is not None:
+                r.set_view_wire(v)
+            r.execute()
     for _ in range(a.warmup):
         one_frame()
     for r in R:
@@ -317,7 +339,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded xoshiro256**, INRIA 3DGS layout, SH degree 3; parity semantics use DC only)",
             "config": {
-                "workload": f"synthetic {a.n} Gaussians, {W}x{H}, {TW}x{TW} tiles, headless camera, fxy[1]={a.scale_div}",
+                "workload": (f"synthetic {a.n} Gaussians clustered around point_cloud_12 (sigma 0.02), {W}x{H}, "
+                             f"{TW}x{TW} tiles, orbit camera (120 views), fxy[1]={a.scale_div}" if a.config5 else
+                             f"synthetic {a.n} Gaussians, {W}x{H}, {TW}x{TW} tiles, headless camera, fxy[1]={a.scale_div}"),
                 "gaussians": a.n,
                 "resolution": [W, H],
                 "tile": [TW, TW],

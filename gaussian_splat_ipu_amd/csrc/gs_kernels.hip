@@ -1128,38 +1128,58 @@ __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, ui
 }
 
 // Large lists (> kSortLdsCap, clustered scenes): a block-wide stable LSD
-// radix sort (8 passes x 8 bits) over the tile's segment in global memory,
-// pairs <-> pairs_alt, by one NT-thread workgroup.  Ranking inside each
-// NT-key chunk: wave64 ballot multisplit (8 ballots give each lane the mask of
-// lanes holding the same digit), then a per-digit prefix over the waves.
-// Passes whose digit is the same for every key are skipped.
-template <int NT>
+// radix sort (8 x 8-bit passes) over the tile's segment in global memory,
+// pairs <-> pairs_alt, by one NT-thread workgroup.  One sweep first builds the
+// digit histograms of all 8 passes (the histogram of a digit does not depend
+// on the order); passes whose digit is the same for every key are skipped.
+// A pass walks the list in rounds of NT * KPL keys: wave w takes the round's
+// keys [w * 64 KPL, (w + 1) * 64 KPL) in KPL steps of 64, all loaded up front,
+// and ranks each step with a wave64 ballot multisplit (8 ballots give each
+// lane the mask of lanes with its digit) plus the wave's running per-digit
+// count in LDS; one cross-wave prefix per digit and the scatter follow, so a
+// round costs 3 barriers (the first version ranked 256 keys per 4 barriers,
+// with each chunk's global load exposed: 5.4 ms per frame on config 5's
+// 162 k-key tiles).
+template <int NT, int KPL>
 __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buffers& b, int t,
                                                 uint32_t* hist, uint32_t* base,
                                                 uint32_t (*wcnt)[256]) {
-  constexpr int NW = NT / 64;
+  constexpr int NW = NT / 64, RK = NT * KPL;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   uint32_t s, L;
   tile_segment(fp, b, t, s, L);
   unsigned long long* src = b.pairs + s;
   unsigned long long* dst = b.pairs_alt + s;
+  // hist[p * 256 + d]: keys whose pass-p digit is d (one sweep for all passes)
+  for (int k = tid; k < 8 * 256; k += NT) hist[k] = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < L; c0 += RK) {
+    unsigned long long key[KPL];
+#pragma unroll
+    for (int e = 0; e < KPL; ++e) {
+      const uint32_t i = c0 + (uint32_t)(e * NT + tid);
+      key[e] = i < L ? src[i] : 0ull;
+    }
+#pragma unroll
+    for (int e = 0; e < KPL; ++e) {
+      if (c0 + (uint32_t)(e * NT + tid) < L) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) atomicAdd(&hist[p * 256 + ((uint32_t)(key[e] >> (8 * p)) & 255u)], 1u);
+      }
+    }
+  }
+  __syncthreads();
   for (int pass = 0; pass < 8; ++pass) {
     const int shift = pass * 8;
-    for (int k = tid; k < 256; k += NT) hist[k] = 0;
-    __syncthreads();
-    for (uint32_t i = tid; i < L; i += NT) atomicAdd(&hist[(uint32_t)(src[i] >> shift) & 255u], 1u);
-    __syncthreads();
-    const bool trivial = hist[(uint32_t)(src[0] >> shift) & 255u] == L;
-    if (trivial) {
-      __syncthreads();
-      continue;  // every key has the same digit: order unchanged
-    }
+    const uint32_t* h = hist + pass * 256;
+    const bool trivial = L == 0 || h[(uint32_t)(src[0] >> shift) & 255u] == L;
+    if (trivial) continue;  // every key has the same digit: order unchanged (uniform branch)
     if (wave == 0) {  // exclusive scan of 256 bins, 4 per lane
       uint32_t v[4], tot = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        v[k] = hist[lane * 4 + k];
+        v[k] = h[lane * 4 + k];
         tot += v[k];
       }
       uint32_t inc = tot;
@@ -1176,25 +1196,43 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
       }
     }
     __syncthreads();
-    for (uint32_t c0 = 0; c0 < L; c0 += NT) {
-      const uint32_t i = c0 + tid;
-      const bool valid = i < L;
-      const unsigned long long key = valid ? src[i] : 0ull;
-      const uint32_t d = (uint32_t)(key >> shift) & 255u;
-      unsigned long long m = ballot64(valid);
+    for (uint32_t c0 = 0; c0 < L; c0 += RK) {
+      const uint32_t w0 = c0 + (uint32_t)(wave * 64 * KPL);
+      unsigned long long key[KPL];
 #pragma unroll
-      for (int bit = 0; bit < 8; ++bit) {
-        const bool set = (d >> bit) & 1u;
-        const unsigned long long bb = ballot64(set);
-        m &= set ? bb : ~bb;
+      for (int e = 0; e < KPL; ++e) {
+        const uint32_t i = w0 + (uint32_t)(e * 64 + lane);
+        key[e] = i < L ? src[i] : 0ull;
       }
-      const uint32_t rank = (uint32_t)__popcll(m & lt_mask);
 #pragma unroll
       for (int k = 0; k < 4; ++k) wcnt[wave][lane * 4 + k] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(m);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint32_t rank[KPL];
+#pragma unroll
+      for (int e = 0; e < KPL; ++e) {
+        const bool valid = w0 + (uint32_t)(e * 64 + lane) < L;
+        const uint32_t d = (uint32_t)(key[e] >> shift) & 255u;
+        unsigned long long m = ballot64(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+          const bool set = (d >> bit) & 1u;
+          const unsigned long long bb = ballot64(set);
+          m &= set ? bb : ~bb;
+        }
+        const uint32_t before = wcnt[wave][d];
+        rank[e] = before + (uint32_t)__popcll(m & lt_mask);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid && (m & lt_mask) == 0ull) wcnt[wave][d] = before + (uint32_t)__popcll(m);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
       __syncthreads();
-      uint32_t chunk_tot = 0;
+      uint32_t round_tot = 0;  // NT >= 256: one digit per thread
       for (int k = tid; k < 256; k += NT) {
         uint32_t run = 0;
 #pragma unroll
@@ -1203,12 +1241,16 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
           wcnt[w][k] = run;
           run += c;
         }
-        chunk_tot = run;  // NT >= 256: one digit per thread
+        round_tot = run;
       }
       __syncthreads();
-      if (valid) dst[base[d] + wcnt[wave][d] + rank] = key;
+#pragma unroll
+      for (int e = 0; e < KPL; ++e) {
+        const uint32_t d = (uint32_t)(key[e] >> shift) & 255u;
+        if (w0 + (uint32_t)(e * 64 + lane) < L) dst[base[d] + wcnt[wave][d] + rank[e]] = key[e];
+      }
       __syncthreads();
-      if (tid < 256) base[tid] += chunk_tot;
+      if (tid < 256) base[tid] += round_tot;
       __syncthreads();
     }
     unsigned long long* tmp = src;
@@ -1232,15 +1274,17 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   constexpr int NW = NT / 64;
   // the radix path's histograms alias the merge path's key buffer (a
   // workgroup takes one path)
-  constexpr int kRadixWords = 512 + NW * 256;
+  constexpr int kRadixWords = 8 * 256 + 256 + NW * 256;
   constexpr int kWords = 2 * kSortLdsCap > kRadixWords ? 2 * kSortLdsCap : kRadixWords;
   __shared__ unsigned long long keys[kWords / 2];
   uint32_t* const r_hist = (uint32_t*)keys;
-  uint32_t* const r_base = r_hist + 256;
-  uint32_t(*const r_wcnt)[256] = (uint32_t(*)[256])(r_hist + 512);
-  const uint32_t n_big = b.counters[0];
+  uint32_t* const r_base = r_hist + 8 * 256;
+  uint32_t(*const r_wcnt)[256] = (uint32_t(*)[256])(r_hist + 9 * 256);
+  // big lists: here (4 keys per lane and round) unless gs_sort_big_kernel
+  // has taken them this frame (FrameParams::big_separate)
+  const uint32_t n_big = fp.big_separate ? 0u : b.counters[0];
   if (blockIdx.x < n_big) {  // the longest lists first
-    radix_sort_tile<NT>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
+    radix_sort_tile<NT, 4>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
     return;
   }
   const uint32_t n_med = b.counters[7], n_small = b.counters[9];
@@ -1267,6 +1311,18 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
   sort_tiles<256>(fp, b);
+}
+
+// Big lists (> kSortLdsCap) in their own launch (FrameParams::big_separate,
+// chosen by the host when the last completed frame had big lists): one
+// 1024-thread workgroup per list, 8 keys per lane and round (8192 keys per
+// round: a round's latency is paid 1/8 as often as with 4 waves x 4 keys).
+__global__ __launch_bounds__(1024) void gs_sort_big_kernel(FrameParams fp, Buffers b) {
+  constexpr int NW = 16;
+  __shared__ uint32_t lds[8 * 256 + 256 + NW * 256];
+  if (blockIdx.x >= b.counters[0]) return;
+  radix_sort_tile<1024, 8>(fp, b, (int)b.big_tiles[blockIdx.x], lds, lds + 8 * 256,
+                           (uint32_t(*)[256])(lds + 9 * 256));
 }
 
 // -------------------------------------------------------------------- blend
@@ -1606,6 +1662,7 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
+  if (fp.big_separate) gs_sort_big_kernel<<<fp.n_tiles, 1024, 0, s>>>(fp, b);
   // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
 }

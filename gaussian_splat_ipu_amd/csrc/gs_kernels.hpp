@@ -41,6 +41,7 @@ struct FrameParams {
   int full_record;    // also write the readback-only record tail (radius, clip z)
   int pair_cull;      // bin only the tiles the alpha box meets (crect); the
                       // reference list lengths are counted alongside
+  int big_separate;   // big lists sorted by gs_sort_big_kernel (launched before the tile sort)
   int pow2;           // tile size, band stride and fxy[1] are powers of two: the
                       // projection divides by them with exact multiplies / shifts
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)

@@ -236,6 +236,10 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.n_chunks = r->n_chunks;
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
+  // the big-list launch only when the last frame the device completed had
+  // big lists (a hint read from the mapped counters: either choice sorts
+  // every list, the other launch handles them otherwise)
+  fp.big_separate = (r->h_counters && ((volatile const uint32_t*)r->h_counters)[0] > 0) ? 1 : 0;
   {
     auto log2_exact = [](double v, int& sh) -> bool {  // v == 2^sh, sh in [-126, 126]
       int e = 0;

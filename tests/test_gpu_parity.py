@@ -131,8 +131,9 @@ def test_synthetic_1080p_16x16(built):
 
 
 def test_large_tile_lists_take_the_radix_path(built):
-    """A clustered scene (config 5's construction) puts > 4096 Gaussians on
-    some tiles: those go through the block-wide LSD radix sort."""
+    """A clustered scene (config 5's construction) puts > 2048 Gaussians on
+    some tiles: those go through the block-wide LSD radix sort, first inside
+    the tile-sort launch, then (second frame) in the separate big-list launch."""
     from gaussian_splat_ipu_amd import camera, scene
 
     src = scene.load_ply(PC12)
@@ -143,6 +144,10 @@ def test_large_tile_lists_take_the_radix_path(built):
     s, f = _frame_pair(g, view, proj, 1280, 720, 16, 16, 1.0)
     _assert_parity(s, f, g)
     assert s.stats()["n_big_tiles"] > 0
+    # the next frame sees big lists in the last completed frame's counters and
+    # sorts them in their own 1024-thread launch (gs_sort_big_kernel)
+    s.execute()
+    _assert_parity(s, f, g)
 
 
 @pytest.mark.parametrize("band_count", [3, 8])

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--contiguous", action="store_true")
     ap.add_argument("--no-cull", action="store_true")
     ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
+    ap.add_argument("--config5", action="store_true", help="bench.py --config5's scene, 4K, orbit views")
     a = ap.parse_args()
     import torch
 
@@ -37,7 +38,17 @@ def main():
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
 
     W, H, TW = 1920, 1080, 16
-    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=a.n, seed=1, sh_degree=3)))
+    views = None
+    if a.config5:
+        import numpy as np
+        W, H = 3840, 2160
+        src = scene.load_ply(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "point_cloud_12.ply"))
+        cl = np.stack([src["x"], src["y"], src["z"]], 1)
+        g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=8_000_000, seed=8, sh_degree=0,
+                                                                    cluster_xyz=cl, cluster_sigma=0.02)))
+        views = [camera.orbit_view(k) for k in range(120)]
+    else:
+        g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=a.n, seed=1, sh_degree=3)))
     view, proj = camera.headless(bb, W, H)
     fb = TiledFramebuffer(W, H, TW, TW)
     base = None
@@ -60,14 +71,23 @@ def main():
                 R.append(s)
                 S.append(st)
             for s in R:
-                s.execute()
-            for k in range(a.warmup):
+                for v in (views or [None]):
+                    if v is not None:
+                        s.set_view_wire(v)
+                    s.execute()
+
+            def frame(k):
+                if views is not None:
+                    R[k % len(R)].set_view_wire(views[k % 120])
                 R[k % len(R)].execute_async()
+
+            for k in range(a.warmup):
+                frame(k)
             torch.cuda.synchronize()
             R[0].reset_kernel_times()
             t0 = time.perf_counter()
             for k in range(a.steps):
-                R[k % len(R)].execute_async()
+                frame(k)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / a.steps
             for s in R:
