@@ -65,11 +65,8 @@ def main():
                 s.set_view_wire(view)
                 s.set_projection_wire(proj)
                 s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
-                st = torch.cuda.Stream()
-                s.set_stream(st.cuda_stream)
-                s.set_profile_interval(4)
+                s.set_profile_interval(1 << 30)  # no stage events in the timed loop
                 R.append(s)
-                S.append(st)
             for s in R:
                 for v in (views or [None]):
                     if v is not None:
@@ -93,6 +90,14 @@ def main():
             for s in R:
                 s.sync()
             per_band.append(dt * 1e6)
+            # stage times: an isolated pass, one frame in flight, events on every frame
+            R[0].set_profile_interval(1)
+            R[0].reset_kernel_times()
+            for k in range(12):
+                if views is not None:
+                    R[0].set_view_wire(views[k % 120])
+                R[0].execute_async()
+            R[0].sync()
             stages.append({k: round(v[0] * 1e3, 1) for k, v in R[0].kernel_times().items()})
             pairs = R[0].stats()["n_pairs"]
             for s in R:

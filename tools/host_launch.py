@@ -15,7 +15,10 @@ for N in [int(v) for v in (sys.argv[1:] or ["1", "8"])]:
         R = []
         for f in range(F):
             s = GpuSplatter(g, fb, device=0, band_index=min(2, N - 1), band_count=N, band_interleaved=N > 1,
-                            band_cull=N > 1, write_rgba=False)
+                            band_cull=N > 1, write_rgba=False,
+                            profile=(f == 0 and bool(os.environ.get('PROFILE0'))))
+            if f == 0 and os.environ.get('PROFILE0'):
+                s.set_profile_interval(1 << 30)
             s.set_view_wire(view); s.set_projection_wire(proj); s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
             st = None
             if os.environ.get('TORCH_STREAMS'):
