@@ -45,6 +45,10 @@ def parse():
                     help="frames of the isolated one-in-flight pass that times each kernel "
                     "(stage HIP events) for the kernel table and the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--band-mode", choices=["balanced", "interleaved"], default="balanced",
+                    help="N > 1: contiguous tile-row bands split by the work of a calibration "
+                    "frame's row histogram (dist.balanced_bands; the band cull then skips ~7/8 "
+                    "of the scene per rank), or interleaved tile rows (rank r: rows r, r + N, ...)")
     ap.add_argument("--config5", action="store_true",
                     help="BASELINE.json configs[4]: 8M Gaussians clustered around point_cloud_12's "
                     "positions (N(0, 0.02) jitter, seed 8), 3840x2160, orbit camera (frame k: "
@@ -143,10 +147,28 @@ def main():
     # latency-bound kernels (scans, list tails) overlap the next frames' work.
     # Every frame is rendered in full.
     F = max(1, a.inflight)
+    # N > 1, balanced: one full frame on every rank gives the row histogram;
+    # every rank derives the same work-balanced split from it
+    bands, pad_rows = None, 0
+    if world > 1 and a.band_mode == "balanced":
+        from gaussian_splat_ipu_amd import dist as gdist
+
+        cal = GpuSplatter(g, fb, device=local, write_rgba=False)
+        cal.set_view_wire(view)
+        cal.set_projection_wire(proj)
+        cal.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
+        cal.execute()
+        bands = gdist.balanced_bands(gdist.row_work(cal.get_histogram(), fb), world)
+        cal.close()
+        pad_rows = max(t1 - t0 for t0, t1 in bands)
     R, streams = [], []
     for f in range(F):
-        r = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=(f == 0),
-                        band_interleaved=world > 1, band_cull=world > 1)
+        if bands is not None:
+            r = GpuSplatter(g, fb, device=local, band_rows=bands[rank], band_pad_rows=pad_rows,
+                            profile=(f == 0), band_cull=True)
+        else:
+            r = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=(f == 0),
+                            band_interleaved=world > 1, band_cull=world > 1)
         r.set_view_wire(view)
         r.set_projection_wire(proj)
         r.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
@@ -159,7 +181,7 @@ def main():
 
     # N > 1: frame k's band is copied out and all-gathered (RCCL) on a comm
     # stream while later frames render; one band / frame buffer per renderer.
-    band_bytes = fb.rows_per_band_padded(world) * W * 3
+    band_bytes = (pad_rows * TW if bands is not None else fb.rows_per_band_padded(world)) * W * 3
     nbuf = F if dist_on else 0
     band = [torch.empty(band_bytes, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     frame = [torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
@@ -347,7 +369,9 @@ def main():
                 "tile": [TW, TW],
                 "frames_in_flight": F,
                 "kernel_table": f"{a.profile_frames} frames, one in flight (stage HIP events)",
-                "parallelism": f"row-band x{world}" + (" (interleaved tile rows) + RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"row-band x{world}" + ((" (work-balanced contiguous bands " + str(bands) + ")"
+                                                         if bands is not None else " (interleaved tile rows)")
+                                                        + " + RCCL all-gather" if world > 1 else ""),
             },
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "n_pairs_binned", "max_list", "n_tiles",
                                          "n_big_tiles")},

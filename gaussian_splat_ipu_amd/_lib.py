@@ -75,6 +75,9 @@ class Config(C.Structure):
         ("band_count", C.c_uint32),
         ("pair_capacity", C.c_uint64),
         ("flags", C.c_uint32),
+        ("band_row_begin", C.c_uint32),
+        ("band_row_end", C.c_uint32),
+        ("band_pad_rows", C.c_uint32),
     ]
 
 

@@ -422,9 +422,22 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
     set_error("gs_create: tile grid too large");
     return fail(GS_EINVAL);
   }
-  const int rpb = (r->tiles_y + (int)cfg->band_count - 1) / (int)cfg->band_count;
+  int rpb = (r->tiles_y + (int)cfg->band_count - 1) / (int)cfg->band_count;
   const int th_px = (int)cfg->tile_height;
-  if (cfg->flags & GS_FLAG_BAND_INTERLEAVED) {
+  const bool explicit_band = cfg->band_row_end > cfg->band_row_begin;
+  if (explicit_band && (cfg->band_row_end > (uint32_t)r->tiles_y || (cfg->flags & GS_FLAG_BAND_INTERLEAVED))) {
+    set_error("gs_create: explicit band rows outside the tile grid (or combined with interleaving)");
+    return fail(GS_EINVAL);
+  }
+  if (explicit_band) {
+    // caller-chosen contiguous band (work-balanced row split)
+    r->band_ty0 = (int)cfg->band_row_begin;
+    r->band_stride = 1;
+    r->band_nrows = (int)(cfg->band_row_end - cfg->band_row_begin);
+    r->band_py0 = r->band_ty0 * th_px;
+    r->band_rows = std::max(0, std::min((int)cfg->height, (int)cfg->band_row_end * th_px) - r->band_py0);
+    rpb = std::max(r->band_nrows, (int)cfg->band_pad_rows);
+  } else if (cfg->flags & GS_FLAG_BAND_INTERLEAVED) {
     // rows band_index, band_index + band_count, ...; output = those tile rows
     // back to back (whole tiles; rows past the image stay 0)
     const int bc = (int)cfg->band_count, bi = (int)cfg->band_index;

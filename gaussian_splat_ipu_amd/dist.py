@@ -60,3 +60,48 @@ def extract_band(frame: np.ndarray, fb: TiledFramebuffer, world: int, rank: int,
         n = min(th, fb.height - y0)
         out[k * th:k * th + n] = frame[y0:y0 + n]
     return out
+
+
+def row_work(hist: np.ndarray, fb: TiledFramebuffer, tile_cost: float = 64.0) -> np.ndarray:
+    """Work per tile row from a frame's tile histogram (list lengths): the
+    pairs of the row (sort + blend work) plus a fixed cost per tile (its blend
+    waves and queue slots)."""
+    h = np.asarray(hist, np.float64).reshape(fb.tiles_down, fb.tiles_across)
+    return h.sum(1) + tile_cost * fb.tiles_across
+
+
+def balanced_bands(work, world: int):
+    """Contiguous tile-row bands [(ty0, ty1), ...] of nearly equal work: band
+    k ends at the row where the cumulative work is closest to k / world of the
+    total, every band keeping at least one row (needs len(work) >= world).
+    Deterministic, so every rank computes the same split from the same
+    histogram."""
+    w = np.asarray(work, np.float64)
+    T = w.size
+    if T < world:
+        raise ValueError(f"{T} tile rows cannot make {world} non-empty bands")
+    c = np.concatenate([[0.0], np.cumsum(w)])
+    bounds = [0]
+    for k in range(1, world):
+        target = c[-1] * k / world
+        b = int(np.searchsorted(c, target))
+        if b > 0 and abs(c[b - 1] - target) <= abs(c[min(b, T)] - target):
+            b -= 1
+        b = max(bounds[-1] + 1, min(b, T - (world - k)))
+        bounds.append(b)
+    bounds.append(T)
+    return [(bounds[i], bounds[i + 1]) for i in range(world)]
+
+
+def assemble_bands(gathered: np.ndarray, fb: TiledFramebuffer, bands, channels: int = 3) -> np.ndarray:
+    """All-gather output of explicit contiguous bands (each padded to the
+    tallest band, GpuSplatter(band_rows=..., band_pad_rows=...)) -> (H, W, C)."""
+    world = len(bands)
+    pad = max(t1 - t0 for t0, t1 in bands) * fb.tile_height
+    g = np.asarray(gathered).reshape(world, pad, fb.width, channels)
+    parts = []
+    for r, (t0, t1) in enumerate(bands):
+        y0 = t0 * fb.tile_height
+        y1 = min(fb.height, t1 * fb.tile_height)
+        parts.append(g[r, : max(0, y1 - y0)])
+    return np.concatenate(parts, 0)

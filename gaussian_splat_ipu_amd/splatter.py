@@ -68,6 +68,8 @@ class GpuSplatter:
         band_interleaved: bool = False,
         band_cull: bool = False,
         pair_cull: bool = True,
+        band_rows=None,
+        band_pad_rows: int = 0,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -85,6 +87,9 @@ class GpuSplatter:
         cfg.device = device
         cfg.band_index, cfg.band_count = band_index, band_count
         cfg.pair_capacity = pair_capacity
+        if band_rows is not None:  # explicit contiguous band: tile rows [begin, end)
+            cfg.band_row_begin, cfg.band_row_end = int(band_rows[0]), int(band_rows[1])
+        cfg.band_pad_rows = int(band_pad_rows)
         cfg.flags = (
             (0 if write_rgba else GS_FLAG_NO_RGBA32F)
             | (GS_FLAG_PROFILE if profile else 0)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 3
+#define GSPLAT_ABI_VERSION 4
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -63,6 +63,13 @@ typedef struct gs_config {
                                          band_index)                         */
   uint64_t pair_capacity;             /* initial (tile,Gaussian) capacity, 0 = auto */
   uint32_t flags;                     /* GS_FLAG_*                          */
+  /* ABI 4: an explicit contiguous band, tile rows [band_row_begin,
+   * band_row_end), used instead of band_index / band_count when
+   * band_row_end > band_row_begin (work-balanced bands chosen by the caller,
+   * e.g. from a frame's row histogram: dist.balanced_bands).  band_pad_rows:
+   * the BGR8 band is padded to this many tile rows (>= the band's), so every
+   * rank of an all-gather contributes the same number of bytes.  0 = none. */
+  uint32_t band_row_begin, band_row_end, band_pad_rows;
 } gs_config;
 
 #define GS_FLAG_NO_RGBA32F 1u  /* skip the RGBA f32 framebuffer store (BGR8 only) */

@@ -47,7 +47,7 @@ def test_abi_version_and_config_defaults(built):
     from gaussian_splat_ipu_amd import _lib
 
     L = _lib.lib()
-    assert L.gs_abi_version() == 3
+    assert L.gs_abi_version() == 4
     cfg = _lib.Config()
     assert L.gs_config_init(ctypes.byref(cfg)) == 0
     # tile_config.hpp:5-15 and codelets.cpp:622

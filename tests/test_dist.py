@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, interleaved=False):
+def _worker(rank, world, port, q, interleaved=False, balanced=False):
     import torch
     import torch.distributed as dist
 
@@ -34,6 +34,24 @@ def _worker(rank, world, port, q, interleaved=False):
         W, H, T = 640, 360, 16
         fb = TiledFramebuffer(W, H, T, T)
         view, proj = camera.headless(bb, W, H)
+        if balanced:
+            # work-balanced contiguous bands from the full frame's histogram
+            # (every rank computes the same split), padded to the tallest band
+            full0 = O.render(g, O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0), nthreads=2)
+            bands = gdist.balanced_bands(gdist.row_work(full0["hist"], fb), world)
+            ty0, ty1 = bands[rank]
+            f = O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
+            band = O.render(g, f, nthreads=2)["bgr"]
+            pad = max(b1 - b0 for b0, b1 in bands) * T
+            padded_np = np.zeros((pad, W, 3), np.uint8)
+            padded_np[: band.shape[0]] = band
+            padded = torch.from_numpy(padded_np.reshape(-1))
+            out = torch.empty(padded.numel() * world, dtype=torch.uint8)
+            dist.all_gather_into_tensor(out, padded)
+            frame = gdist.assemble_bands(out.numpy(), fb, bands)
+            if rank == 0:
+                q.put((np.array_equal(frame, full0["bgr"]), float(world), frame.shape))
+            return
         if interleaved:
             # tile rows rank, rank + world, ...: each rendered as a one-row
             # oracle band (the GPU renders them in one pass; test_gpu_parity)
@@ -61,14 +79,15 @@ def _worker(rank, world, port, q, interleaved=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,interleaved", [(2, False), (3, False), (3, True)])
-def test_band_allgather_equals_single_frame(built, world, interleaved):
+@pytest.mark.parametrize("world,interleaved,balanced", [(2, False, False), (3, False, False), (3, True, False),
+                                                       (3, False, True)])
+def test_band_allgather_equals_single_frame(built, world, interleaved, balanced):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, interleaved)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, interleaved, balanced)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -78,3 +97,22 @@ def test_band_allgather_equals_single_frame(built, world, interleaved):
     assert same
     assert tmax == float(world)
     assert shape == (360, 640, 3)
+
+
+def test_balanced_bands_partition():
+    """dist.balanced_bands: contiguous, covering, non-empty, and its heaviest
+    band exceeds the ideal share by at most two rows' work."""
+    from gaussian_splat_ipu_amd import dist as gdist
+
+    rng = np.random.default_rng(3)
+    for T, world in [(68, 8), (68, 2), (8, 8), (135, 7), (30, 4)]:
+        w = rng.gamma(0.5, 100.0, T) + 1.0
+        w[T // 3: T // 2] *= 20.0  # a dense centre
+        bands = gdist.balanced_bands(w, world)
+        assert bands[0][0] == 0 and bands[-1][1] == T
+        assert all(b0 < b1 for b0, b1 in bands)
+        assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
+        loads = [w[b0:b1].sum() for b0, b1 in bands]
+        assert max(loads) <= w.sum() / world + 2.0 * w.max() + 1e-9
+    with pytest.raises(ValueError):
+        gdist.balanced_bands(np.ones(3), 4)

@@ -186,6 +186,45 @@ def test_interleaved_bands_equal_full_frame_rows(pc12, band_count):
     np.testing.assert_array_equal(gdist.assemble(np.stack(gathered), fb, band_count, interleaved=True), bgr)
 
 
+@pytest.mark.parametrize("band_count", [2, 8])
+def test_balanced_explicit_bands_equal_full_frame(pc12, band_count):
+    """Work-balanced contiguous bands (gs_config.band_row_begin/end, ABI 4;
+    dist.balanced_bands over the full frame's histogram) with the band cull:
+    each band equals its rows of the full frame (itself checked against the
+    oracle), and the padded all-gather layout assembles back to it."""
+    from gaussian_splat_ipu_amd import camera, dist as gdist
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    g, bb = pc12
+    W, H, TW, TH = 1920, 1080, 16, 16
+    view, proj = camera.headless(bb, W, H)
+    full, f = _frame_pair(g, view, proj, W, H, TW, TH, 1.0)
+    _assert_parity(full, f, g, check_proj=False)
+    fb = TiledFramebuffer(W, H, TW, TH)
+    rgba, bgr = full.get_rgba(), full.get_frame_buffer()
+    hist = full.get_histogram().reshape(fb.tiles_down, fb.tiles_across)
+    bands = gdist.balanced_bands(gdist.row_work(hist, fb), band_count)
+    pad = max(t1 - t0 for t0, t1 in bands)
+    gathered = []
+    for t0, t1 in bands:
+        s = GpuSplatter(g, fb, device=0, band_rows=(t0, t1), band_pad_rows=pad, band_cull=True)
+        s.set_view_wire(view)
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        s.execute()
+        y0, y1 = t0 * TH, min(H, t1 * TH)
+        assert_same_bits(s.get_rgba(), rgba[y0:y1], f"band {t0}-{t1} rgba")
+        band_bgr = s.get_frame_buffer()
+        np.testing.assert_array_equal(band_bgr, bgr[y0:y1])
+        np.testing.assert_array_equal(s.get_histogram(), hist[t0:t1].reshape(-1))
+        dev = np.zeros((pad * TH, W, 3), np.uint8)
+        dev[: y1 - y0] = band_bgr
+        gathered.append(dev)
+        s.close()
+    np.testing.assert_array_equal(gdist.assemble_bands(np.stack(gathered), fb, bands), bgr)
+
+
 @pytest.mark.parametrize("band_count", [2, 3, 8])
 def test_row_bands_union_equals_full_frame(pc12, band_count):
     """The multi-GPU decomposition: each band renders its tile rows; every band

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=1)
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--contiguous", action="store_true")
+    ap.add_argument("--balanced", action="store_true", help="work-balanced contiguous bands (bench.py's N > 1 default)")
     ap.add_argument("--no-cull", action="store_true")
     ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
     ap.add_argument("--config5", action="store_true", help="bench.py --config5's scene, 4K, orbit views")
@@ -52,16 +53,33 @@ def main():
     view, proj = camera.headless(bb, W, H)
     fb = TiledFramebuffer(W, H, TW, TW)
     base = None
+    hist = None
+    if a.balanced:
+        from gaussian_splat_ipu_amd import dist as gdist
+
+        cal = GpuSplatter(g, fb, device=0, write_rgba=False)
+        cal.set_view_wire(view)
+        cal.set_projection_wire(proj)
+        cal.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        cal.execute()
+        hist = cal.get_histogram()
+        cal.close()
     for N in [int(v) for v in a.bands.split(",")]:
         per_band, stages = [], []
+        bands = gdist.balanced_bands(gdist.row_work(hist, fb), N) if hist is not None and N > 1 else None
+        pad = max(t1 - t0 for t0, t1 in bands) if bands else 0
         for r in range(N):
             if a.only_band >= 0 and r != a.only_band:
                 continue
             R, S = [], []
             for f in range(a.inflight):
-                s = GpuSplatter(g, fb, device=0, band_index=r, band_count=N, profile=(f == 0),
-                                band_interleaved=(N > 1 and not a.contiguous),
-                                band_cull=(N > 1 and not a.no_cull), write_rgba=False)
+                if bands is not None:
+                    s = GpuSplatter(g, fb, device=0, band_rows=bands[r], band_pad_rows=pad, profile=(f == 0),
+                                    band_cull=not a.no_cull, write_rgba=False)
+                else:
+                    s = GpuSplatter(g, fb, device=0, band_index=r, band_count=N, profile=(f == 0),
+                                    band_interleaved=(N > 1 and not a.contiguous),
+                                    band_cull=(N > 1 and not a.no_cull), write_rgba=False)
                 s.set_view_wire(view)
                 s.set_projection_wire(proj)
                 s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
