@@ -256,7 +256,8 @@ __device__ __forceinline__ void band_rows_of(const FrameParams& fp, float fy0, f
 // range is computed with the rectangle's own (monotone) formulas from the same
 // vy, so it contains the true rows.  Non-finite values never cull.
 template <bool P2>
-__device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, const M3& T, float4 sg) {
+__device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, const M3& T, float4 sg,
+                                            float extra = 0.0f) {
   float t2 = 0.0f;
 #pragma unroll
   for (int c = 0; c < 3; ++c)
@@ -264,13 +265,49 @@ __device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, con
     for (int r = 0; r < 3; ++r) t2 += T.m[c][r] * T.m[c][r];
   const float smax = div_p2<P2>(fmaxf(fmaxf(sg.x, sg.y), sg.z), fp.scale_div, fp.inv_sd);
   const float lc = __expf(2.0f * smax) * 1.01f;
-  const float r = 3.0f * __builtin_sqrtf(1.05f * (2.0f * lc * t2) + 1.0f) + 2.0f;
+  const float r = 3.0f * __builtin_sqrtf(1.05f * (2.0f * lc * t2) + 1.0f) + 2.0f + extra;
   if (!(__builtin_fabsf(vy) < 1e30f) || !(r < 1e30f)) return false;
   const float fy0 = __builtin_floorf(div_p2<P2>(__builtin_floorf(vy - r), fp.th, fp.inv_th));
   const float fy1 = __builtin_floorf(div_p2<P2>(__builtin_ceilf(vy + r), fp.th, fp.inv_th));
   int yb0, yb1;
   band_rows_of<P2>(fp, fy0, fy1, yb0, yb1);
   return yb0 > yb1;
+}
+
+// The band cull's first, cheap pass: the same bound as band_culled, from vy
+// and T computed with v_rcp instead of correctly rounded divisions (each
+// quotient within ~1 ulp; the bound's 5 % inflation covers T, and vy gets
+// 1e-5 |vy| + 0.05 px more).  Only a Gaussian this pass proves outside the
+// band is skipped; the exact test in project_one still runs for the rest.
+template <bool P2>
+__device__ __forceinline__ bool band_culled_fast(const FrameParams& fp, float4 mean, float4 sg) {
+  const float* m = fp.mvp;
+  const float cy = mv_row(m, 1, mean.x, mean.y, mean.z, mean.w);
+  const float cw = mv_row(m, 3, mean.x, mean.y, mean.z, mean.w);
+  const float vy = (cy * (0.5f * __builtin_amdgcn_rcpf(cw)) + 0.5f) * fp.H;
+  const float tx = mv_row(m, 0, mean.x, mean.y, mean.z, 1.0f);
+  const float ty = mv_row(m, 1, mean.x, mean.y, mean.z, 1.0f);
+  const float tz = mv_row(m, 2, mean.x, mean.y, mean.z, 1.0f);
+  const float itz = __builtin_amdgcn_rcpf(tz);
+  const float lim = 1.3f * fp.tanfov;
+  const float ctx = fminf(lim, fmaxf(-lim, tx * itz)) * tz;
+  const float cty = fminf(lim, fmaxf(-lim, ty * itz)) * tz;
+  M3 J;
+  J.m[0][0] = fp.focal_x * itz;
+  J.m[0][1] = 0.0f;
+  J.m[0][2] = -(fp.focal_x * ctx) * (itz * itz);
+  J.m[1][0] = 0.0f;
+  J.m[1][1] = fp.focal_y * itz;
+  J.m[1][2] = -(fp.focal_y * cty) * (itz * itz);
+  J.m[2][0] = 0.0f;
+  J.m[2][1] = 0.0f;
+  J.m[2][2] = 0.0f;
+  M3 W;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) W.m[c][r] = m[c * 4 + r];
+  return band_culled<P2>(fp, vy, m3_mul(W, J), sg, 1e-5f * __builtin_fabsf(vy) + 0.05f);
 }
 
 template <bool P2>
@@ -430,7 +467,29 @@ template <bool P2>
 __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool rendered = false;
-  if (i < fp.n) rendered = project_one<P2>(fp, b, i);
+  if (fp.band_cull) {
+    // the cheap band test first; a block of 256 Gaussians that it culls
+    // entirely writes only its V (0): count and emit skip such blocks
+    // without reading their rectangles, so nothing else needs writing
+    bool culled = false;
+    if (i < fp.n) {
+      const float4 sg = b.scale_gid[i];
+      culled = !(sg.w <= 0.0f) && band_culled_fast<P2>(fp, b.mean[i], sg);
+    }
+    if (__syncthreads_count(i < fp.n && !culled) == 0) {
+      if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = 0u;
+      return;
+    }
+    if (culled) {  // no tile row in this band: empty rectangle, no record
+      b.rect[i] = kEmptyRect;
+      if (fp.pair_cull) b.crect[i] = kEmptyRect;
+      b.depth_key[i] = 0xFFFFFFFFu;
+    } else if (i < fp.n) {
+      rendered = project_one<P2>(fp, b, i);
+    }
+  } else if (i < fp.n) {
+    rendered = project_one<P2>(fp, b, i);
+  }
   // V per workgroup (summed by the scan kernel): no single-address atomics
   const int v = __syncthreads_count(rendered);
   if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
@@ -575,6 +634,13 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
 //   colscan: per tile, exclusive scan over chunks (in place) + tile totals
 //   emit:    chunk c writes its pairs of tile t at
 //            tile_start[t] + chunk_off[c][t] + (LDS slot counter)
+// GS_FLAG_BAND_CULL: the projection skips every write of a 256-Gaussian block
+// its cheap band test culls entirely (block_rendered = 0), so binning must not
+// read such a block's rectangles
+__device__ __forceinline__ bool block_live(const FrameParams& fp, const Buffers& b, int i) {
+  return !fp.band_cull || b.block_rendered[i >> 8] != 0u;
+}
+
 __device__ __forceinline__ void lds_zero(uint32_t* cnt, int words) {
   for (int i = threadIdx.x; i < words; i += blockDim.x) cnt[i] = 0;
 }
@@ -596,11 +662,19 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
     __syncthreads();
     for (int i00 = g0; i00 < g1; i00 += 4096) {  // 4 Gaussians per thread, loaded up front
       uint2 rr[4], qq[4];
+      bool live[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int i = i00 + k * 1024 + (int)threadIdx.x;
-        rr[k] = i < g1 ? b.rect[i] : kEmptyRect;
-        qq[k] = i < g1 ? b.crect[i] : kEmptyRect;
+        // band cull: a 256-Gaussian block with no rendered Gaussian (project's
+        // block_rendered) has only empty rectangles; skip its loads (wave-uniform)
+        live[k] = i < g1 && block_live(fp, b, i);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i00 + k * 1024 + (int)threadIdx.x;
+        rr[k] = live[k] ? b.rect[i] : kEmptyRect;
+        qq[k] = live[k] ? b.crect[i] : kEmptyRect;
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -632,7 +706,7 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
   __syncthreads();
   for (int i0 = g0; i0 < g1; i0 += 1024) {
     const int i = i0 + (int)threadIdx.x;
-    const uint2 r = i < g1 ? b.rect[i] : kEmptyRect;
+    const uint2 r = (i < g1 && block_live(fp, b, i)) ? b.rect[i] : kEmptyRect;
     const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
     const bool start = lane == 0 || r.x != px || r.y != py;
     const unsigned long long st = ballot64(start);
@@ -859,12 +933,18 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
     for (int i0 = g0; i0 < g1; i0 += 4096) {  // 4 Gaussians per thread, loaded up front
       uint2 r[4];
       uint32_t dk[4], pm[4];
+      bool live[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int i = i0 + k * 1024 + (int)threadIdx.x;
-        r[k] = i < g1 ? rects[i] : kEmptyRect;
-        dk[k] = i < g1 ? b.depth_key[i] : 0u;
-        pm[k] = i < g1 ? b.perm[i] : 0u;
+        live[k] = i < g1 && block_live(fp, b, i);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + k * 1024 + (int)threadIdx.x;
+        r[k] = live[k] ? rects[i] : kEmptyRect;
+        dk[k] = live[k] ? b.depth_key[i] : 0u;
+        pm[k] = live[k] ? b.perm[i] : 0u;
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -883,6 +963,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
   lds_zero(cnt, (T + 1) >> 1);
   __syncthreads();
   for (int i = g0 + (int)threadIdx.x; i < g1; i += 1024) {
+    if (!block_live(fp, b, i)) continue;
     const uint2 r = fp.pair_cull ? b.crect[i] : b.rect[i];
     const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
     if (x0 > x1) continue;
@@ -903,6 +984,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
 __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= fp.n) return;
+  if (!block_live(fp, b, i)) return;
   const uint2 r = b.rect[i];
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   if (x0 > x1) return;
