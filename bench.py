@@ -49,6 +49,12 @@ def parse():
                     help="N > 1: contiguous tile-row bands split by the work of a calibration "
                     "frame's row histogram (dist.balanced_bands; the band cull then skips ~7/8 "
                     "of the scene per rank), or interleaved tile rows (rank r: rows r, r + N, ...)")
+    ap.add_argument("--zero-copy", type=int, default=0,
+                    help="N > 1: all-gather straight from the renderer's padded BGR8 band (1) or "
+                    "from a copy of it (0)")
+    ap.add_argument("--split", type=int, default=0,
+                    help="row bands of the split (default: the world size); with --gather on one "
+                    "GPU, rank 0 renders band 0 of a --split way split (exercises the N > 1 path)")
     ap.add_argument("--config5", action="store_true",
                     help="BASELINE.json configs[4]: 8M Gaussians clustered around point_cloud_12's "
                     "positions (N(0, 0.02) jitter, seed 8), 3840x2160, orbit camera (frame k: "
@@ -150,7 +156,8 @@ def main():
     # N > 1, balanced: one full frame on every rank gives the row histogram;
     # every rank derives the same work-balanced split from it
     bands, pad_rows = None, 0
-    if world > 1 and a.band_mode == "balanced":
+    split = a.split if a.split > 0 else world
+    if split > 1 and a.band_mode == "balanced":
         from gaussian_splat_ipu_amd import dist as gdist
 
         cal = GpuSplatter(g, fb, device=local, write_rgba=False)
@@ -158,7 +165,7 @@ def main():
         cal.set_projection_wire(proj)
         cal.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
         cal.execute()
-        bands = gdist.balanced_bands(gdist.row_work(cal.get_histogram(), fb), world)
+        bands = gdist.balanced_bands(gdist.row_work(cal.get_histogram(), fb), split)
         cal.close()
         pad_rows = max(t1 - t0 for t0, t1 in bands)
     R, streams = [], []
@@ -167,8 +174,8 @@ def main():
             r = GpuSplatter(g, fb, device=local, band_rows=bands[rank], band_pad_rows=pad_rows,
                             profile=(f == 0), band_cull=True)
         else:
-            r = GpuSplatter(g, fb, device=local, band_index=rank, band_count=world, profile=(f == 0),
-                            band_interleaved=world > 1, band_cull=world > 1)
+            r = GpuSplatter(g, fb, device=local, band_index=rank, band_count=split, profile=(f == 0),
+                            band_interleaved=split > 1, band_cull=split > 1)
         r.set_view_wire(view)
         r.set_projection_wire(proj)
         r.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
@@ -181,11 +188,23 @@ def main():
 
     # N > 1: frame k's band is copied out and all-gathered (RCCL) on a comm
     # stream while later frames render; one band / frame buffer per renderer.
-    band_bytes = (pad_rows * TW if bands is not None else fb.rows_per_band_padded(world)) * W * 3
+    band_bytes = (pad_rows * TW if bands is not None else fb.rows_per_band_padded(split)) * W * 3
     nbuf = F if dist_on else 0
     band = [torch.empty(band_bytes, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     frame = [torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     comm = torch.cuda.Stream() if dist_on else None
+
+    class _DeviceBytes:  # a renderer's BGR8 band as a torch tensor (no copy)
+        def __init__(self, ptr, n):
+            self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False),
+                                             "version": 3}
+
+    band_views = []
+    if dist_on and a.zero_copy:
+        for r in R:
+            ptr, nb = r.bgr8_device()
+            assert nb == band_bytes, (nb, band_bytes)
+            band_views.append(torch.as_tensor(_DeviceBytes(ptr, nb), device="cuda"))
     ev_copy = [torch.cuda.Event() for _ in range(nbuf)]
     ev_free = [torch.cuda.Event() for _ in range(nbuf)]
     nframe = [0]
@@ -197,14 +216,23 @@ def main():
         r, st = R[i], streams[i]
         if views is not None:  # orbit camera: a new view every frame
             r.set_view_wire(views[nframe[0] % 120])
+        if dist_on and a.zero_copy:
+            # the gather reads the renderer's own padded BGR8 band in place:
+            # this renderer's next frame waits until the gather of its last one
+            # has read it
+            st.wait_event(ev_free[i])
         r.execute_async()
         if dist_on:
-            st.wait_event(ev_free[i])  # the gather of frame k-F read band[i]
-            r.copy_bgr8_device(band[i].data_ptr(), band_bytes)
+            if a.zero_copy:
+                src = band_views[i]
+            else:
+                st.wait_event(ev_free[i])  # the gather of frame k-F read band[i]
+                r.copy_bgr8_device(band[i].data_ptr(), band_bytes)
+                src = band[i]
             ev_copy[i].record(st)
             with torch.cuda.stream(comm):
                 comm.wait_event(ev_copy[i])
-                dist.all_gather_into_tensor(frame[i], band[i])
+                dist.all_gather_into_tensor(frame[i], src)
                 ev_free[i].record(comm)
         nframe[0] += 1
 
