@@ -1135,7 +1135,7 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
 // runs): the register bitonic phase was 80 % of a medium sort (per-workgroup
 // timestamps, tools/sort_times.py), and E = 2 took the sort from 45.0 to
 // 43.2 us; E = 1 took 49.1.
-template <int NT, int E>
+template <int NT, int E, bool KEYS_OUT = false>
 __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
                                                 unsigned long long* lds) {
   constexpr int RUN = 64 * E, NW = NT / 64;
@@ -1203,7 +1203,10 @@ __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, ui
     } else {
 #pragma unroll
       for (int k = 0; k < KMAX; ++k)
-        if (k < K && d0 + k < (int)L) b.list[s + d0 + k] = b.inv_perm[(uint32_t)out[k]];
+        if (k < K && d0 + k < (int)L) {
+          if constexpr (KEYS_OUT) b.pairs[s + d0 + k] = out[k];  // a big list's sorted segment
+          else b.list[s + d0 + k] = b.inv_perm[(uint32_t)out[k]];
+        }
       break;
     }
   }
@@ -1362,8 +1365,8 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   uint32_t* const r_hist = (uint32_t*)keys;
   uint32_t* const r_base = r_hist + 8 * 256;
   uint32_t(*const r_wcnt)[256] = (uint32_t(*)[256])(r_hist + 9 * 256);
-  // big lists: here (4 keys per lane and round) unless gs_sort_big_kernel
-  // has taken them this frame (FrameParams::big_separate)
+  // big lists: radix-sorted here (4 keys per lane and round) unless the
+  // segmented merge sort has taken them this frame (FrameParams::big_separate)
   const uint32_t n_big = fp.big_separate ? 0u : b.counters[0];
   if (blockIdx.x < n_big) {  // the longest lists first
     radix_sort_tile<NT, 4>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
@@ -1395,17 +1398,200 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   sort_tiles<256>(fp, b);
 }
 
-// Big lists (> kSortLdsCap) in their own launch (FrameParams::big_separate,
-// chosen by the host when the last completed frame had big lists): one
-// 1024-thread workgroup per list, 8 keys per lane and round (8192 keys per
-// round: a round's latency is paid 1/8 as often as with 4 waves x 4 keys).
-__global__ __launch_bounds__(1024) void gs_sort_big_kernel(FrameParams fp, Buffers b) {
-  constexpr int NW = 16;
-  __shared__ uint32_t lds[8 * 256 + 256 + NW * 256];
-  if (blockIdx.x >= b.counters[0]) return;
-  radix_sort_tile<1024, 8>(fp, b, (int)b.big_tiles[blockIdx.x], lds, lds + 8 * 256,
-                           (uint32_t(*)[256])(lds + 9 * 256));
+// ---- big lists as a segmented merge sort over many workgroups
+// (FrameParams::big_separate).  A list > kSortLdsCap is cut into 2048-key
+// segments; every segment is sorted by one workgroup (the medium path, keys
+// written back in place), then merge passes p = 0, 1, ... each merge pairs of
+// sorted runs of 2048 << p keys, pairs <-> pairs_alt, every workgroup making
+// 2048 outputs of one list (merge path: two co-rank searches in global memory,
+// the two input ranges staged in LDS, 8 outputs per thread).  The pass whose
+// pair covers the whole list writes the list itself (device indices); later
+// passes skip it.  Work items are (big list j, segment c), numbered through
+// big_chunk_off (tile_cursor, unused by the chunked binning) and walked
+// grid-stride, so any grid size is correct.
+constexpr int kBigSeg = 2048;
+
+// one workgroup: segment counts of the big lists -> exclusive prefix
+__global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buffers b) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t s_maxl;
+  const uint32_t n_big = b.counters[0];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_maxl = 0;
+  uint32_t carry = 0, maxl = 0;
+  for (uint32_t j0 = 0; j0 < n_big; j0 += 1024) {
+    const uint32_t j = j0 + (uint32_t)tid;
+    uint32_t c = 0;
+    if (j < n_big) {
+      uint32_t s, L;
+      tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+      c = (L + kBigSeg - 1) / kBigSeg;
+      maxl = max(maxl, L);
+    }
+    uint32_t inc = c;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += w < wave ? wsum[w] : 0u;
+      tot += wsum[w];
+    }
+    if (j < n_big) {
+      const uint32_t off = carry + before + inc - c;
+      b.tile_cursor[j] = off;
+      for (uint32_t q = 0; q < c; ++q) b.big_item[off + q] = j;  // segment -> list slot
+    }
+    carry += tot;
+    __syncthreads();
+  }
+  atomicMax(&s_maxl, maxl);
+  __syncthreads();
+  if (tid == 0) {
+    b.counters[12] = carry;   // segments of all big lists
+    b.counters[13] = s_maxl;  // the longest big list (passes beyond it are no-ops)
+  }
 }
+
+// work item k -> (big list j, segment c), from the prefix kernel's tables
+__device__ __forceinline__ void big_item(const Buffers& b, uint32_t n_big, uint32_t k, uint32_t& j,
+                                         uint32_t& c) {
+  j = b.big_item[k];
+  c = k - b.tile_cursor[j];
+}
+
+// Co-rank of diagonal k in the merge of sorted A[0, la) and B[0, lb) (the
+// number of outputs < k taken from A), by one wave: 64 probes per step cut
+// the interval ~65-fold (log_65 instead of log_2 dependent global loads).
+__device__ __forceinline__ uint32_t corank_wave(const unsigned long long* A, uint32_t la,
+                                                const unsigned long long* B, uint32_t lb, uint32_t k,
+                                                int lane) {
+  uint32_t lo = k > lb ? k - lb : 0u, hi = min(k, la);  // answer in [lo, hi]
+  while (hi > lo) {
+    const uint32_t span = hi - lo;
+    // probe p: "A[p] <= B[k - 1 - p]" holds exactly for p < answer
+    const uint32_t p = span <= 64u ? lo + (uint32_t)lane
+                                   : lo + (uint32_t)(((unsigned long long)span * (uint32_t)(lane + 1)) / 65u);
+    const bool in = p < hi;
+    const bool t = in && A[p] <= B[k - 1 - p];
+    const unsigned long long mt = ballot64(t), mf = ballot64(in && !t);
+    // the last true probe + 1 and the first false probe bound the answer
+    const uint32_t nlo = mt ? (uint32_t)__builtin_amdgcn_readlane((int)p, 63 - __builtin_clzll(mt)) + 1u : lo;
+    const uint32_t nhi = mf ? (uint32_t)__builtin_amdgcn_readlane((int)p, __builtin_ctzll(mf)) : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_segsort_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long keys[kSortLdsCap];
+  __shared__ uint32_t s_item[2];
+  const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
+  for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
+    if (threadIdx.x == 0) {
+      uint32_t j, c;
+      big_item(b, n_big, k, j, c);
+      s_item[0] = j;
+      s_item[1] = c;
+    }
+    __syncthreads();
+    const uint32_t j = s_item[0], c = s_item[1];
+    __syncthreads();
+    uint32_t s, L;
+    tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+    const uint32_t s0 = s + c * kBigSeg;
+    const uint32_t n = min((uint32_t)kBigSeg, L - c * kBigSeg);
+    merge_sort_tile<256, 2, true>(b, s0, n, keys);
+  }
+}
+
+__global__ __launch_bounds__(256) void gs_big_merge_kernel(FrameParams fp, Buffers b, int pass) {
+  __shared__ unsigned long long sab[kBigSeg];  // the A range, then the B range
+  __shared__ uint32_t s_par[8];
+  const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
+  const uint32_t R = (uint32_t)kBigSeg << pass;  // sorted run length before this pass
+  if (R >= b.counters[13]) return;                // every list already merged
+  const unsigned long long* src = (pass & 1) ? b.pairs_alt : b.pairs;
+  unsigned long long* dst = (pass & 1) ? b.pairs : b.pairs_alt;
+  const int tid = threadIdx.x;
+  for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
+    if (tid == 0) {
+      uint32_t j, c;
+      big_item(b, n_big, k, j, c);
+      uint32_t s, L;
+      tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+      s_par[0] = s;
+      s_par[1] = L;
+      s_par[2] = c;
+    }
+    __syncthreads();
+    const uint32_t s = s_par[0], L = s_par[1], c = s_par[2];
+    __syncthreads();
+    if (R >= L) continue;  // merged by an earlier pass (uniform)
+    const bool last = 2 * R >= L;
+    const uint32_t d0 = c * kBigSeg, d1 = min(L, d0 + kBigSeg);
+    const uint32_t base = d0 / (2 * R) * (2 * R);
+    const uint32_t la = min(R, L - base), lb = L - base > R ? min(R, L - base - R) : 0u;
+    const unsigned long long* A = src + s + base;
+    const unsigned long long* B = A + la;
+    // the output range's split of the two runs (waves 0 and 1)
+    if (tid < 128) {
+      const uint32_t r = corank_wave(A, la, B, lb, (tid < 64 ? d0 : d1) - base, tid & 63);
+      if ((tid & 63) == 0) s_par[3 + (tid >> 6)] = r;
+    }
+    __syncthreads();
+    const uint32_t i0 = s_par[3], i1 = s_par[4];
+    const uint32_t j0 = d0 - base - i0, j1 = d1 - base - i1;
+    const uint32_t na = i1 - i0, nb = j1 - j0;
+    __syncthreads();
+    unsigned long long* const sa = sab;
+    unsigned long long* const sb = sab + na;
+    {  // stage A[i0, i1) then B[j0, j1): all 8 loads of a thread in flight at once
+      unsigned long long tmp[kBigSeg / 256];
+#pragma unroll
+      for (int q = 0; q < kBigSeg / 256; ++q) {
+        const uint32_t t = (uint32_t)tid + (uint32_t)q * 256u;
+        tmp[q] = t < na ? A[i0 + t] : (t < na + nb ? B[j0 + t - na] : 0ull);
+      }
+#pragma unroll
+      for (int q = 0; q < kBigSeg / 256; ++q) {
+        const uint32_t t = (uint32_t)tid + (uint32_t)q * 256u;
+        if (t < na + nb) sab[t] = tmp[q];
+      }
+    }
+    __syncthreads();
+    // 8 consecutive outputs per thread
+    const uint32_t o0 = (uint32_t)tid * 8u, nout = na + nb;
+    if (o0 < nout) {
+      uint32_t lo = o0 > nb ? o0 - nb : 0u, hi = min(o0, na);
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sa[mid] <= sb[o0 - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+      }
+      uint32_t ia = lo, ib = o0 - lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t o = o0 + (uint32_t)e;
+        if (o < nout) {
+          const unsigned long long av = ia < na ? sa[ia] : ~0ull, bv = ib < nb ? sb[ib] : ~0ull;
+          const bool ta = ib >= nb || (ia < na && av <= bv);
+          const unsigned long long v = ta ? av : bv;
+          ia += ta ? 1u : 0u;
+          ib += ta ? 0u : 1u;
+          if (last) b.list[s + d0 + o] = b.inv_perm[(uint32_t)v];
+          else dst[s + d0 + o] = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 
 // -------------------------------------------------------------------- blend
 __device__ __forceinline__ uint8_t to_u8(float v) {
@@ -1744,7 +1930,16 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
-  if (fp.big_separate) gs_sort_big_kernel<<<fp.n_tiles, 1024, 0, s>>>(fp, b);
+  if (fp.big_separate) {
+    // work items = 2048-key segments of the big lists; the passes run until a
+    // run covers the longest list the pair buffer can hold (passes after a
+    // list's last one skip it)
+    const unsigned grid = 4096;
+    gs_big_prefix_kernel<<<1, 1024, 0, s>>>(fp, b);
+    gs_big_segsort_kernel<<<grid, 256, 0, s>>>(fp, b);
+    for (int pass = 0; ((unsigned long long)kBigSeg << pass) < fp.pair_cap && pass < 24; ++pass)
+      gs_big_merge_kernel<<<grid, 256, 0, s>>>(fp, b, pass);
+  }
   // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
 }

@@ -73,6 +73,7 @@ struct Buffers {
   unsigned long long* pairs_alt;  // [pair_cap]  scratch of the large-list sort
   uint32_t* list;           // [pair_cap]  depth-sorted Gaussians (device indices)
   uint32_t* big_tiles;      // [n_tiles]  lists > kSortLdsCap (radix sort queue)
+  uint32_t* big_item;       // [pair_cap / 2048 + n_tiles + 1]  segment k of the big lists -> big-list slot
   uint32_t* medium_tiles;   // [n_tiles]  lists in (kSortRegCap, kSortLdsCap] (block sort queue)
   uint32_t* small_tiles;    // [n_tiles]  lists in [1, kSortRegCap] (one-wave sort queue)
   uint32_t* chunk_off;      // [n_chunks][n_tiles] chunk histograms -> offsets

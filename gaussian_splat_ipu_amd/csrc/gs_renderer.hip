@@ -156,13 +156,16 @@ std::vector<uint32_t> morton_order(const gs_gaussian3d* g, size_t n, bool keep) 
 
 int alloc_pairs(gs_renderer* r, uint64_t cap) {
   free_pairs(r);
-  const size_t bytes = (size_t)cap * (8 + 8 + 4);
+  // + one u32 per 2048-key segment a big list can have (segmented merge sort)
+  const size_t n_items = (size_t)(cap / 2048) + (size_t)r->n_tiles + 1;
+  const size_t bytes = (size_t)cap * (8 + 8 + 4) + n_items * 4;
   GS_HIP(hipMalloc(&r->d_pairs, bytes));
   r->pair_cap = cap;
   char* p = (char*)r->d_pairs;
   r->buf.pairs = (unsigned long long*)p;
   r->buf.pairs_alt = (unsigned long long*)(p + (size_t)cap * 8);
   r->buf.list = (uint32_t*)(p + (size_t)cap * 16);
+  r->buf.big_item = (uint32_t*)(p + (size_t)cap * 20);
   return GS_OK;
 }
 
