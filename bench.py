@@ -49,9 +49,9 @@ def parse():
                     help="N > 1: contiguous tile-row bands split by the work of a calibration "
                     "frame's row histogram (dist.balanced_bands; the band cull then skips ~7/8 "
                     "of the scene per rank), or interleaved tile rows (rank r: rows r, r + N, ...)")
-    ap.add_argument("--zero-copy", type=int, default=0,
-                    help="N > 1: all-gather straight from the renderer's padded BGR8 band (1) or "
-                    "from a copy of it (0)")
+    ap.add_argument("--gather-group", type=int, default=3,
+                    help="N > 1: frames per all-gather = frames in flight x this (the collective's "
+                    "host cost is paid once per group)")
     ap.add_argument("--split", type=int, default=0,
                     help="row bands of the split (default: the world size); with --gather on one "
                     "GPU, rank 0 renders band 0 of a --split way split (exercises the N > 1 path)")
@@ -186,55 +186,51 @@ def main():
     # the kernel table comes from the isolated pass after it
     s.set_profile_interval(1 << 30)
 
-    # N > 1: frame k's band is copied out and all-gathered (RCCL) on a comm
-    # stream while later frames render; one band / frame buffer per renderer.
+    # N > 1: each frame's padded band is copied into a group buffer; the G
+    # frames of a group (F renderers x --gather-group) are all-gathered by ONE RCCL call
+    # on a communication stream while the next group renders.  Two group
+    # buffers alternate.  (One gather per frame made the host loop the limit:
+    # ~57 us of Python/launch work per frame against ~42 us of GPU work at 8
+    # bands; a group amortises the collective's host cost over F frames.)
     band_bytes = (pad_rows * TW if bands is not None else fb.rows_per_band_padded(split)) * W * 3
-    nbuf = F if dist_on else 0
-    band = [torch.empty(band_bytes, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
-    frame = [torch.empty(band_bytes * world, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
+    G = F * max(1, a.gather_group)
+    gbuf = [torch.empty(G * band_bytes, dtype=torch.uint8, device="cuda") for _ in range(2)] if dist_on else []
+    gout = ([torch.empty(world * G * band_bytes, dtype=torch.uint8, device="cuda") for _ in range(2)]
+            if dist_on else [])
     comm = torch.cuda.Stream() if dist_on else None
-
-    class _DeviceBytes:  # a renderer's BGR8 band as a torch tensor (no copy)
-        def __init__(self, ptr, n):
-            self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False),
-                                             "version": 3}
-
-    band_views = []
-    if dist_on and a.zero_copy:
-        for r in R:
-            ptr, nb = r.bgr8_device()
-            assert nb == band_bytes, (nb, band_bytes)
-            band_views.append(torch.as_tensor(_DeviceBytes(ptr, nb), device="cuda"))
-    ev_copy = [torch.cuda.Event() for _ in range(nbuf)]
-    ev_free = [torch.cuda.Event() for _ in range(nbuf)]
+    ev_copy = [torch.cuda.Event() for _ in range(F)]
+    ev_free = [torch.cuda.Event() for _ in range(2)]
     nframe = [0]
 
     views = [camera.orbit_view(k) for k in range(120)] if a.config5 else None
 
+    def gather_group(g):
+        bsel = g % 2
+        with torch.cuda.stream(comm):
+            for e in ev_copy:
+                comm.wait_event(e)
+            dist.all_gather_into_tensor(gout[bsel], gbuf[bsel])  # (world, G, band) rank-major
+            ev_free[bsel].record(comm)
+
     def one_frame():
-        i = nframe[0] % F
+        k = nframe[0]
+        i, g, slot = k % F, k // G, k % G
         r, st = R[i], streams[i]
         if views is not None:  # orbit camera: a new view every frame
-            r.set_view_wire(views[nframe[0] % 120])
-        if dist_on and a.zero_copy:
-            # the gather reads the renderer's own padded BGR8 band in place:
-            # this renderer's next frame waits until the gather of its last one
-            # has read it
-            st.wait_event(ev_free[i])
+            r.set_view_wire(views[k % 120])
         r.execute_async()
         if dist_on:
-            if a.zero_copy:
-                src = band_views[i]
-            else:
-                st.wait_event(ev_free[i])  # the gather of frame k-F read band[i]
-                r.copy_bgr8_device(band[i].data_ptr(), band_bytes)
-                src = band[i]
+            bsel = g % 2
+            st.wait_event(ev_free[bsel])  # the gather of group g - 2 has read this buffer
+            r.copy_bgr8_device(gbuf[bsel].data_ptr() + slot * band_bytes, band_bytes)
             ev_copy[i].record(st)
-            with torch.cuda.stream(comm):
-                comm.wait_event(ev_copy[i])
-                dist.all_gather_into_tensor(frame[i], src)
-                ev_free[i].record(comm)
+            if slot == G - 1:
+                gather_group(g)
         nframe[0] += 1
+
+    def flush():  # a partial last group is gathered too
+        if dist_on and nframe[0] % G:
+            gather_group(nframe[0] // G)
 
     # warm-up (the first blocking render sizes the pair buffers; with the
     # orbit camera every view once, so no timed frame can overflow them)
@@ -245,6 +241,8 @@ def main():
             r.execute()
     for _ in range(a.warmup):
         one_frame()
+    flush()
+    nframe[0] = 0
     for r in R:
         r.sync()
     torch.cuda.synchronize()
@@ -255,6 +253,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_frame()
+    flush()
+    t_enq = time.perf_counter()  # host time to enqueue the K frames
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -383,6 +383,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "frame_latency_ms": latency_ms,
+            "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / a.steps, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
