@@ -186,7 +186,7 @@ def main():
     # the kernel table comes from the isolated pass after it
     s.set_profile_interval(1 << 30)
 
-    # N > 1: each frame's padded band is copied into a group buffer; the G
+    # N > 1: each frame writes its padded band into a group buffer; the G
     # frames of a group (F renderers x --gather-group) are all-gathered by ONE RCCL call
     # on a communication stream while the next group renders.  Two group
     # buffers alternate.  (One gather per frame made the host loop the limit:
@@ -218,11 +218,14 @@ def main():
         r, st = R[i], streams[i]
         if views is not None:  # orbit camera: a new view every frame
             r.set_view_wire(views[k % 120])
+        if dist_on:
+            # the frame writes its band straight into its group-buffer slot
+            # (gs_set_bgr8_target), after the gather of group g - 2 read it
+            bsel = g % 2
+            st.wait_event(ev_free[bsel])
+            r.set_bgr8_target(gbuf[bsel].data_ptr() + slot * band_bytes, band_bytes)
         r.execute_async()
         if dist_on:
-            bsel = g % 2
-            st.wait_event(ev_free[bsel])  # the gather of group g - 2 has read this buffer
-            r.copy_bgr8_device(gbuf[bsel].data_ptr() + slot * band_bytes, band_bytes)
             ev_copy[i].record(st)
             if slot == G - 1:
                 gather_group(g)
@@ -267,6 +270,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = s.stats()
+    for r in R:
+        r.set_bgr8_target(None)
     # kernel table: the same frames with one in flight (renderer 0 alone,
     # stage HIP events on its stream around every kernel of every frame), so
     # each duration is the kernel's own, not shared with other frames' work

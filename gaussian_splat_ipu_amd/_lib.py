@@ -144,6 +144,7 @@ _SIGS = {
     "gs_read_projected": (C.c_int, [_P, _FP, C.c_size_t]),
     "gs_bgr8_device": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_size_t)]),
     "gs_copy_bgr8_device": (C.c_int, [_P, _P, C.c_size_t]),
+    "gs_set_bgr8_target": (C.c_int, [_P, _P, C.c_size_t]),
     "gs_kernel_times": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
     "gs_reset_kernel_times": (C.c_int, [_P]),
     "gs_set_profile_interval": (C.c_int, [_P, C.c_uint32]),

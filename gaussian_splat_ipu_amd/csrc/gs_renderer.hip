@@ -72,6 +72,9 @@ struct gs_renderer {
   std::vector<uint32_t> hist_snapshot;
   std::mutex hist_mu;
   bool frame_pending = false;
+  uint8_t* own_bgr = nullptr;     // the renderer's BGR8 band buffer
+  uint8_t* bgr_target = nullptr;  // gs_set_bgr8_target: frames write their BGR8 here instead
+  uint8_t* last_bgr = nullptr;    // where the last enqueued frame wrote its BGR8
   bool have_frame = false;
   gs_frame_stats stats{};
 
@@ -281,6 +284,9 @@ int enqueue_frame(gs_renderer* r) {
   // hold the last one's counters after gs_sync
   const gsk::FrameParams fp = make_params(r);
   hipStream_t s = r->stream;
+  // BGR8 destination of this frame (gs_set_bgr8_target)
+  r->buf.bgr = r->bgr_target ? r->bgr_target : r->own_bgr;
+  r->last_bgr = r->buf.bgr;
   ProfileSlot* slot = nullptr;
   if (r->profile && r->frame_seq++ % r->profile_every == 0) {
     slot = &r->ring[r->ring_head];
@@ -562,6 +568,7 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
     return fail(hip_fail(e, "hipMalloc(framebuffer)"));
   r->buf.rgba = (float4*)r->d_out;
   r->buf.bgr = (uint8_t*)r->d_out + px * 16;
+  r->own_bgr = r->last_bgr = r->buf.bgr;
   if ((e = hipMemset(r->d_out, 0, px * 16 + r->bgr_bytes)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(framebuffer)"));
 
@@ -670,7 +677,7 @@ int gs_read_bgr8(gs_renderer* r, uint8_t* dst, size_t bytes) {
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
-  GS_HIP(hipMemcpy(dst, r->buf.bgr, need, hipMemcpyDeviceToHost));
+  GS_HIP(hipMemcpy(dst, r->last_bgr, need, hipMemcpyDeviceToHost));
   return GS_OK;
 }
 
@@ -815,7 +822,7 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
 
 int gs_bgr8_device(gs_renderer* r, void** dev_ptr, size_t* bytes) {
   if (!r || !dev_ptr || !bytes) return GS_EINVAL;
-  *dev_ptr = r->buf.bgr;
+  *dev_ptr = r->own_bgr;
   *bytes = r->bgr_bytes;
   return GS_OK;
 }
@@ -824,7 +831,17 @@ int gs_copy_bgr8_device(gs_renderer* r, void* dst_dev, size_t bytes) {
   if (!r || !dst_dev || bytes < r->bgr_bytes) return GS_EINVAL;
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
-  GS_HIP(hipMemcpyAsync(dst_dev, r->buf.bgr, r->bgr_bytes, hipMemcpyDeviceToDevice, r->stream));
+  GS_HIP(hipMemcpyAsync(dst_dev, r->last_bgr, r->bgr_bytes, hipMemcpyDeviceToDevice, r->stream));
+  return GS_OK;
+}
+
+int gs_set_bgr8_target(gs_renderer* r, void* dst_dev, size_t bytes) {
+  if (!r) return GS_EINVAL;
+  if (dst_dev && bytes < r->bgr_bytes) {
+    set_error("gs_set_bgr8_target: destination smaller than the padded band");
+    return GS_EINVAL;
+  }
+  r->bgr_target = (uint8_t*)dst_dev;
   return GS_OK;
 }
 

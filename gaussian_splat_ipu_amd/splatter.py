@@ -232,6 +232,11 @@ class GpuSplatter:
         check(lib().gs_bgr8_device(self._h, C.byref(p), C.byref(nbytes)))
         return p.value, nbytes.value
 
+    def set_bgr8_target(self, dst_ptr, nbytes: int = 0) -> None:
+        """Later frames write their padded BGR8 band at device address dst_ptr
+        (None: the renderer's own buffer)."""
+        check(lib().gs_set_bgr8_target(self._h, C.c_void_p(dst_ptr or 0), nbytes))
+
     def copy_bgr8_device(self, dst_ptr: int, nbytes: int) -> None:
         check(lib().gs_copy_bgr8_device(self._h, C.c_void_p(dst_ptr), nbytes))
 

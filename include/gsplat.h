@@ -200,6 +200,12 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats);
 int gs_bgr8_device(gs_renderer* r, void** dev_ptr, size_t* bytes);
 /* Enqueue a device-to-device copy of the band's BGR8 (padded) into dst. */
 int gs_copy_bgr8_device(gs_renderer* r, void* dst_dev, size_t bytes);
+/* Frames enqueued from now on write their (padded) BGR8 band straight into
+ * dst_dev (>= the padded band bytes; NULL = the renderer's own buffer), e.g.
+ * a slot of a caller's all-gather buffer: no copy.  The caller orders its
+ * reads of dst_dev after the frame (gs_get_stream).  gs_read_bgr8 and
+ * gs_copy_bgr8_device read the last frame's destination. */
+int gs_set_bgr8_target(gs_renderer* r, void* dst_dev, size_t bytes);
 /* Average device milliseconds per launch of each kernel (GS_K_*) over the
  * frames since the last reset (requires GS_FLAG_PROFILE). */
 int gs_kernel_times(gs_renderer* r, double* avg_ms, uint64_t* launches, int n);
