@@ -220,19 +220,26 @@ def main():
             r.set_view_wire(views[k % 120])
         if dist_on:
             # the frame writes its band straight into its group-buffer slot
-            # (gs_set_bgr8_target), after the gather of group g - 2 read it
+            # (gs_set_bgr8_target), after the gather of group g - 2 read it:
+            # a renderer's first frame of the group waits for that, and its
+            # last one marks the end of its writes (in-stream order covers the
+            # frames between)
             bsel = g % 2
-            st.wait_event(ev_free[bsel])
+            if slot < F:
+                st.wait_event(ev_free[bsel])
             r.set_bgr8_target(gbuf[bsel].data_ptr() + slot * band_bytes, band_bytes)
         r.execute_async()
         if dist_on:
-            ev_copy[i].record(st)
+            if slot >= G - F:
+                ev_copy[i].record(st)
             if slot == G - 1:
                 gather_group(g)
         nframe[0] += 1
 
     def flush():  # a partial last group is gathered too
         if dist_on and nframe[0] % G:
+            for e, st in zip(ev_copy, streams):
+                e.record(st)
             gather_group(nframe[0] // G)
 
     # warm-up (the first blocking render sizes the pair buffers; with the

@@ -937,7 +937,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
     const uint2* __restrict__ rects = fp.pair_cull ? b.crect : b.rect;
     for (int i0 = g0; i0 < g1; i0 += 4096) {  // 4 Gaussians per thread, loaded up front
       uint2 r[4];
-      uint32_t dk[4], pm[4];
+      uint32_t dk[4];
       bool live[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -949,13 +949,12 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
         const int i = i0 + k * 1024 + (int)threadIdx.x;
         r[k] = live[k] ? rects[i] : kEmptyRect;
         dk[k] = live[k] ? b.depth_key[i] : 0u;
-        pm[k] = live[k] ? b.perm[i] : 0u;
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t x0 = r[k].x & 0xFFFFu, x1 = r[k].x >> 16, y0 = r[k].y & 0xFFFFu, y1 = r[k].y >> 16;
         if (x0 > x1) continue;
-        const unsigned long long key = ((unsigned long long)dk[k] << 32) | pm[k];
+        const unsigned long long key = ((unsigned long long)dk[k] << 32) | (uint32_t)(i0 + k * 1024 + (int)threadIdx.x);
         for (uint32_t y = y0; y <= y1; ++y)
           for (uint32_t x = x0; x <= x1; ++x) {
             const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
@@ -972,7 +971,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
     const uint2 r = fp.pair_cull ? b.crect[i] : b.rect[i];
     const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
     if (x0 > x1) continue;
-    const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
+    const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | (uint32_t)i;
     for (uint32_t y = y0; y <= y1; ++y)
       for (uint32_t x = x0; x <= x1; ++x) {
         const uint32_t t = y * fp.tiles_x + x;
@@ -993,7 +992,7 @@ __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b)
   const uint2 r = b.rect[i];
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   if (x0 > x1) return;
-  const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | b.perm[i];
+  const unsigned long long key = ((unsigned long long)b.depth_key[i] << 32) | (uint32_t)i;
   for (uint32_t y = y0; y <= y1; ++y)
     for (uint32_t x = x0; x <= x1; ++x) {
       const uint32_t pos = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], 1u);
@@ -1138,8 +1137,84 @@ __device__ __forceinline__ void wave_bitonic(unsigned long long (&v)[E], int lan
   }
 }
 
+// Keys: (orderable clip z << 32) | device index, as the emit writes them.
+// The list order is (z, INPUT index) (the oracle's stable order), which the
+// device index gives too except among equal depths (the device order is 3D
+// Morton).  So a sorted list is checked for neighbours of equal depth; only a
+// list that has some (rare: exactly equal clip z in one tile) is re-keyed with
+// the input index (perm[]) and sorted again, and its list written through
+// inv_perm[].  The common case writes the low words: no gather.
+constexpr unsigned long long kDepthMask = 0xFFFFFFFF00000000ull;
+
+__device__ __forceinline__ unsigned long long rekey_input(const Buffers& b, unsigned long long k) {
+  return (k & kDepthMask) | b.perm[(uint32_t)k];
+}
+
+// Writes the list of sorted device-index keys k[0, L) (positions t, t + stride,
+// ... of this thread).  A key without an equal-depth neighbour is in place.
+// A run of equal depths shorter than kTieRun is put in input-index order: a
+// member's place is the run's start plus its input index's rank within the
+// run (perm[], only for these).  Returns true when this thread met a longer
+// run (e.g. a plane facing the camera): the caller re-sorts the list.  At
+// 1M/1080p clip z has only 943 k distinct values over 1M Gaussians; 182 of
+// the 8160 lists have equal depths, nearly all in runs of 2 (re-sorting those
+// lists cost the sort launch 13 us).
+constexpr uint32_t kTieRun = 16;
+
+__device__ __forceinline__ bool write_tied_list(const Buffers& b, uint32_t s, uint32_t L,
+                                                const unsigned long long* k, uint32_t t,
+                                                uint32_t stride) {
+  bool longrun = false;
+  for (uint32_t p = t; p < L; p += stride) {
+    const unsigned long long kp = k[p];
+    const uint32_t hi = (uint32_t)(kp >> 32);
+    const bool tp = p > 0u && (uint32_t)(k[p - 1] >> 32) == hi;
+    const bool tn = p + 1u < L && (uint32_t)(k[p + 1] >> 32) == hi;
+    if (!tp && !tn) {
+      b.list[s + p] = (uint32_t)kp;
+      continue;
+    }
+    uint32_t a = p, e = p + 1u;
+    while (a > 0u && p - a < kTieRun && (uint32_t)(k[a - 1] >> 32) == hi) --a;
+    while (e < L && e - p < kTieRun && (uint32_t)(k[e] >> 32) == hi) ++e;
+    if (e - a >= kTieRun) {
+      longrun = true;
+      continue;
+    }
+    const uint32_t me = b.perm[(uint32_t)kp];
+    uint32_t rank = 0;
+    for (uint32_t j = a; j < e; ++j) rank += b.perm[(uint32_t)k[j]] < me ? 1u : 0u;
+    b.list[s + a + rank] = (uint32_t)kp;
+  }
+  return longrun;
+}
+
+// The rare path of a small list with equal depths: input-index keys, the
+// rolled network, one copy for every E (the hot unrolled networks stay
+// compact in the instruction cache: a copy per E inside them doubled the
+// kernel's code and cost the isolated sort 13 us).
+__device__ __forceinline__ void wave_sort_tile_input(const Buffers& b, uint32_t s, uint32_t L,
+                                                               int lane) {
+  constexpr int E = 4;  // L <= kSortRegCap = 256
+  unsigned long long v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t i = (uint32_t)(lane * E + e);
+    v[e] = i < L ? rekey_input(b, b.pairs[s + i]) : ~0ull;
+  }
+  for (int k = 2; k <= 64 * E; k <<= 1) wave_merge<E>(v, lane, 0, k, k >> 1);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t i = (uint32_t)(lane * E + e);
+    if (i < L) b.list[s + i] = b.inv_perm[(uint32_t)v[e]];
+  }
+}
+
+// Returns false (nothing written; the sorted keys are left in slice[0, L))
+// when the list has equal depths.
 template <int E>
-__device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uint32_t L, int lane) {
+__device__ __forceinline__ bool wave_sort_tile(const Buffers& b, uint32_t s, uint32_t L, int lane,
+                                               unsigned long long* slice) {
   unsigned long long v[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -1147,11 +1222,26 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
     v[e] = i < L ? b.pairs[s + i] : ~0ull;
   }
   wave_bitonic<E>(v, lane);
+  // key i - 1 of key i: this lane's previous register, or lane - 1's last
+  const uint32_t prev_hi = (uint32_t)__shfl_up((int)(uint32_t)(v[E - 1] >> 32), 1, 64);
+  bool tie = false;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const uint32_t i = (uint32_t)(lane * E + e);
-    if (i < L) b.list[s + i] = b.inv_perm[(uint32_t)v[e]];
+    const uint32_t ph = e > 0 ? (uint32_t)(v[e - 1] >> 32) : prev_hi;
+    tie = tie || (i > 0u && i < L && ph == (uint32_t)(v[e] >> 32));
   }
+  if (ballot64(tie) != 0ull) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) slice[lane * E + e] = v[e];
+    return false;
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t i = (uint32_t)(lane * E + e);
+    if (i < L) b.list[s + i] = (uint32_t)v[e];
+  }
+  return true;
 }
 
 // Medium lists (kSortRegCap < L <= kSortLdsCap), one NT-thread workgroup:
@@ -1166,8 +1256,18 @@ __device__ __forceinline__ void wave_sort_tile(const Buffers& b, uint32_t s, uin
 // runs): the register bitonic phase was 80 % of a medium sort (per-workgroup
 // timestamps, tools/sort_times.py), and E = 2 took the sort from 45.0 to
 // 43.2 us; E = 1 took 49.1.
-template <int NT, int E, bool KEYS_OUT = false>
-__device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
+// SRC: where the keys come from (kSrcPairs: the tile's pairs; kSrcRekey: the
+// pairs re-keyed with the input index).
+// OUT: kOutKeys writes the sorted keys back to the pairs (a big list's
+// segment); kOutInput writes the list from input-index keys (inv_perm);
+// kOutDevice writes the list from device-index keys, checking equal depths
+// first (see wave_sort_tile) and re-sorting with input-index keys if any.
+// kOutDevice returns false (nothing written) when the list has equal depths.
+enum { kSrcPairs = 0, kSrcRekey = 1 };
+enum { kOutKeys = 0, kOutInput = 1, kOutDevice = 2 };
+
+template <int NT, int E, int OUT, int SRC = kSrcPairs>
+__device__ __forceinline__ bool merge_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
                                                 unsigned long long* lds) {
   constexpr int RUN = 64 * E, NW = NT / 64;
   constexpr int KMAX = (kSortLdsCap + NT - 1) / NT;
@@ -1180,7 +1280,8 @@ __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, ui
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const uint32_t i = (uint32_t)(r * RUN + lane * E + e);
-      v[e] = i < L ? b.pairs[s + i] : ~0ull;
+      if constexpr (SRC == kSrcRekey) v[e] = i < L ? rekey_input(b, b.pairs[s + i]) : ~0ull;
+      else v[e] = i < L ? b.pairs[s + i] : ~0ull;
     }
     wave_bitonic<E>(v, lane);
 #pragma unroll
@@ -1226,21 +1327,28 @@ __device__ __forceinline__ void merge_sort_tile(const Buffers& b, uint32_t s, ui
       }
     }
     __syncthreads();
-    if (2 * w < npad) {
+    if (2 * w < npad || OUT == kOutDevice) {
 #pragma unroll
       for (int k = 0; k < KMAX; ++k)
         if (k < K && d0 + k < npad) lds[d0 + k] = out[k];
       __syncthreads();
+      if (2 * w < npad) continue;
     } else {
 #pragma unroll
       for (int k = 0; k < KMAX; ++k)
         if (k < K && d0 + k < (int)L) {
-          if constexpr (KEYS_OUT) b.pairs[s + d0 + k] = out[k];  // a big list's sorted segment
+          if constexpr (OUT == kOutKeys) b.pairs[s + d0 + k] = out[k];  // a big list's sorted segment
           else b.list[s + d0 + k] = b.inv_perm[(uint32_t)out[k]];
         }
-      break;
+      return true;
     }
+    break;
   }
+  if constexpr (OUT == kOutDevice) {
+    // the sorted keys are in lds[0, L)
+    if (__syncthreads_or(write_tied_list(b, s, L, lds, threadIdx.x, NT))) return false;
+  }
+  return true;
 }
 
 // Large lists (> kSortLdsCap, clustered scenes): a block-wide stable LSD
@@ -1267,6 +1375,11 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
   tile_segment(fp, b, t, s, L);
   unsigned long long* src = b.pairs + s;
   unsigned long long* dst = b.pairs_alt + s;
+  // input-index keys (the order among equal depths), written to pairs_alt
+  // and sorted from there
+  for (uint32_t i = tid; i < L; i += NT) dst[i] = rekey_input(b, src[i]);
+  src = b.pairs_alt + s;
+  dst = b.pairs + s;
   // hist[p * 256 + d]: keys whose pass-p digit is d (one sweep for all passes)
   for (int k = tid; k < 8 * 256; k += NT) hist[k] = 0;
   __syncthreads();
@@ -1408,7 +1521,10 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   if (item < n_med) {
     uint32_t s, L;
     tile_segment(fp, b, (int)b.medium_tiles[item], s, L);
-    merge_sort_tile<NT, 2>(b, s, L, keys);
+    if (!merge_sort_tile<NT, 2, kOutDevice>(b, s, L, keys)) {
+      __syncthreads();  // a long run of equal depths: again with input-index keys
+      merge_sort_tile<NT, 2, kOutInput, kSrcRekey>(b, s, L, keys);
+    }
     return;
   }
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1417,12 +1533,27 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   const int lane = threadIdx.x & 63;
   uint32_t s, L;
   tile_segment(fp, b, (int)b.small_tiles[k], s, L);
+  // this wave's slice of the (here unused) merge buffer, for a list with
+  // equal depths
+  static_assert(NW * kSortRegCap <= kWords / 2, "small-list slices fit the merge buffer");
+  unsigned long long* const slice = keys + wave * kSortRegCap;
+  bool done;
   if (L <= 64u)
-    wave_sort_tile<1>(b, s, L, lane);
+    done = wave_sort_tile<1>(b, s, L, lane, slice);
   else if (L <= 128u)
-    wave_sort_tile<2>(b, s, L, lane);
+    done = wave_sort_tile<2>(b, s, L, lane, slice);
   else
-    wave_sort_tile<4>(b, s, L, lane);
+    done = wave_sort_tile<4>(b, s, L, lane, slice);
+  if (!done) {  // equal depths (wave-uniform)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool longrun = write_tied_list(b, s, L, slice, (uint32_t)lane, 64u);
+    if (ballot64(longrun) != 0ull) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // after the stores above
+      wave_sort_tile_input(b, s, L, lane);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
@@ -1536,7 +1667,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t s0 = s + c * kBigSeg;
     const uint32_t n = min((uint32_t)kBigSeg, L - c * kBigSeg);
-    merge_sort_tile<256, 2, true>(b, s0, n, keys);
+    merge_sort_tile<256, 2, kOutKeys, kSrcRekey>(b, s0, n, keys);
   }
 }
 

@@ -500,3 +500,44 @@ def test_render_server_cli(built, tmp_path):
     np.testing.assert_array_equal(raw[:, :, ::-1], ref["bgr"])
     bad = subprocess.run([exe, "--input", PC12, "--ui-port", "5000"], capture_output=True, text=True)
     assert bad.returncode != 0 and "remote UI" in bad.stderr
+
+
+@pytest.mark.parametrize("half_width,log_scale,planes", [
+    (1.5, -3.8, 4), (0.3, -4.0, 4), (1.5, -3.8, 64), (0.3, -4.0, 400)])
+def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
+    """Gaussians on planes of constant clip z (a view that only translates
+    along z), in shuffled input order: the tile lists hold runs of equal
+    depth, whose order must be the input index's (the oracle's stable order),
+    not the device (Morton) order the pair keys carry.  half_width 1.5 gives
+    small lists; 0.3 small, medium and > 2048-key lists (radix sort on the
+    first frame, the segmented merge sort on the second).  4 planes make long
+    runs (the list is re-sorted), 64 / 400 planes mostly short ones (put in
+    order in place)."""
+    from gaussian_splat_ipu_amd import camera, scene
+    from oracle import oracle as O
+
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=5, sh_degree=0)))
+    a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
+    rng = np.random.default_rng(11)
+    n = a.shape[0]
+    a[:, 0] = rng.uniform(-half_width, half_width, n)
+    a[:, 1] = rng.uniform(-half_width, half_width, n)
+    a[:, 2] = rng.choice(np.linspace(0.0, 1.5, planes, dtype=np.float32), n)
+    a[:, 3] = 1.0
+    a[:, 7] = rng.uniform(0.02, 0.3, n)  # low opacities: many records per pixel contribute
+    a[:, 12:15] = log_scale + rng.normal(0.0, 0.2, (n, 3))
+    _, proj = camera.headless(bb, 1280, 720)
+    view = np.float32([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, -4.0, 0, 0, 0, 1])
+    s, f = _frame_pair(a, view, proj, 1280, 720, 16, 16, 1.0)
+    ref = _assert_parity(s, f, a)
+    # the lists really hold equal depths next to each other
+    p = O.project(a, f)
+    ts, lst = O.bin_lists(p, f)
+    z = p["clip_z"][lst]
+    same = (z[1:] == z[:-1]) & (np.diff(np.searchsorted(ts, np.arange(len(lst)), side="right")) == 0)
+    assert same.sum() > 500
+    if half_width < 1.0:
+        assert s.stats()["n_big_tiles"] > 0
+        s.execute()  # big lists through the segmented merge sort
+        _assert_parity(s, f, a)
+    assert ref["stats"]["n_pairs"] > 0
