@@ -23,6 +23,10 @@
 #include "gs_kernels.hpp"
 
 // blend: 1 = one record mask per pixel (blend 82 -> 78 us), 0 = per 2x2 quad
+// big lists: 1 = sample sort, 0 = segmented merge sort
+#ifndef GS_BIG_SAMPLE
+#define GS_BIG_SAMPLE 1
+#endif
 // blend: waves per workgroup (the waves are independent)
 #ifndef GS_BLEND_WPG
 #define GS_BLEND_WPG 4
@@ -1257,14 +1261,16 @@ __device__ __forceinline__ bool wave_sort_tile(const Buffers& b, uint32_t s, uin
 // timestamps, tools/sort_times.py), and E = 2 took the sort from 45.0 to
 // 43.2 us; E = 1 took 49.1.
 // SRC: where the keys come from (kSrcPairs: the tile's pairs; kSrcRekey: the
-// pairs re-keyed with the input index).
+// pairs re-keyed with the input index; kSrcLds: lds[0, L) already holds them;
+// kSrcAlt: pairs_alt; kSrcAltRekey: pairs_alt re-keyed).  kOutLds leaves the
+// sorted keys in lds[0, L).
 // OUT: kOutKeys writes the sorted keys back to the pairs (a big list's
 // segment); kOutInput writes the list from input-index keys (inv_perm);
 // kOutDevice writes the list from device-index keys, checking equal depths
 // first (see wave_sort_tile) and re-sorting with input-index keys if any.
 // kOutDevice returns false (nothing written) when the list has equal depths.
-enum { kSrcPairs = 0, kSrcRekey = 1 };
-enum { kOutKeys = 0, kOutInput = 1, kOutDevice = 2 };
+enum { kSrcPairs = 0, kSrcRekey = 1, kSrcLds = 2, kSrcAlt = 3, kSrcAltRekey = 4 };
+enum { kOutKeys = 0, kOutInput = 1, kOutDevice = 2, kOutLds = 3 };
 
 template <int NT, int E, int OUT, int SRC = kSrcPairs>
 __device__ __forceinline__ bool merge_sort_tile(const Buffers& b, uint32_t s, uint32_t L,
@@ -1281,6 +1287,9 @@ __device__ __forceinline__ bool merge_sort_tile(const Buffers& b, uint32_t s, ui
     for (int e = 0; e < E; ++e) {
       const uint32_t i = (uint32_t)(r * RUN + lane * E + e);
       if constexpr (SRC == kSrcRekey) v[e] = i < L ? rekey_input(b, b.pairs[s + i]) : ~0ull;
+      else if constexpr (SRC == kSrcLds) v[e] = i < L ? lds[i] : ~0ull;  // run r: this wave's own slots
+      else if constexpr (SRC == kSrcAlt) v[e] = i < L ? b.pairs_alt[s + i] : ~0ull;
+      else if constexpr (SRC == kSrcAltRekey) v[e] = i < L ? rekey_input(b, b.pairs_alt[s + i]) : ~0ull;
       else v[e] = i < L ? b.pairs[s + i] : ~0ull;
     }
     wave_bitonic<E>(v, lane);
@@ -1327,7 +1336,7 @@ __device__ __forceinline__ bool merge_sort_tile(const Buffers& b, uint32_t s, ui
       }
     }
     __syncthreads();
-    if (2 * w < npad || OUT == kOutDevice) {
+    if (2 * w < npad || OUT == kOutDevice || OUT == kOutLds) {
 #pragma unroll
       for (int k = 0; k < KMAX; ++k)
         if (k < K && d0 + k < npad) lds[d0 + k] = out[k];
@@ -1364,22 +1373,21 @@ __device__ __forceinline__ bool merge_sort_tile(const Buffers& b, uint32_t s, ui
 // round costs 3 barriers (the first version ranked 256 keys per 4 barriers,
 // with each chunk's global load exposed: 5.4 ms per frame on config 5's
 // 162 k-key tiles).
-template <int NT, int KPL>
-__device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buffers& b, int t,
-                                                uint32_t* hist, uint32_t* base,
-                                                uint32_t (*wcnt)[256]) {
+// The device-index keys [s, s + L) of the pairs (FROM_ALT: of pairs_alt) are
+// re-keyed with the input index into the other buffer and sorted there; the
+// list [s, s + L) is written.
+template <int NT, int KPL, bool FROM_ALT>
+__device__ __forceinline__ void radix_sort_seg(const Buffers& b, uint32_t s, uint32_t L,
+                                               uint32_t* hist, uint32_t* base,
+                                               uint32_t (*wcnt)[256]) {
   constexpr int NW = NT / 64, RK = NT * KPL;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  uint32_t s, L;
-  tile_segment(fp, b, t, s, L);
-  unsigned long long* src = b.pairs + s;
-  unsigned long long* dst = b.pairs_alt + s;
-  // input-index keys (the order among equal depths), written to pairs_alt
-  // and sorted from there
-  for (uint32_t i = tid; i < L; i += NT) dst[i] = rekey_input(b, src[i]);
-  src = b.pairs_alt + s;
-  dst = b.pairs + s;
+  unsigned long long* src = (FROM_ALT ? b.pairs : b.pairs_alt) + s;
+  unsigned long long* dst = (FROM_ALT ? b.pairs_alt : b.pairs) + s;
+  // input-index keys (the order among equal depths), written to the other
+  // buffer and sorted from there
+  for (uint32_t i = tid; i < L; i += NT) src[i] = rekey_input(b, dst[i]);
   // hist[p * 256 + d]: keys whose pass-p digit is d (one sweep for all passes)
   for (int k = tid; k < 8 * 256; k += NT) hist[k] = 0;
   __syncthreads();
@@ -1489,6 +1497,15 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
   for (uint32_t i = tid; i < L; i += NT) b.list[s + i] = b.inv_perm[(uint32_t)src[i]];
 }
 
+template <int NT, int KPL>
+__device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buffers& b, int t,
+                                                uint32_t* hist, uint32_t* base,
+                                                uint32_t (*wcnt)[256]) {
+  uint32_t s, L;
+  tile_segment(fp, b, t, s, L);
+  radix_sort_seg<NT, KPL, false>(b, s, L, hist, base, wcnt);
+}
+
 // Big, medium and small lists in one launch, longest first: workgroups
 // [0, n_big) radix-sort one big list each (> kSortLdsCap); the next n_medium
 // each sort one medium list (kSortRegCap < L <= kSortLdsCap, merge_sort_tile);
@@ -1573,41 +1590,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // grid-stride, so any grid size is correct.
 constexpr int kBigSeg = 2048;
 
+// sample sort of the big lists: buckets of ~kBktAvg keys, at most kBktMax
+// per list (their splitters are staged in LDS)
+constexpr uint32_t kBktAvg = 1024, kBktMax = 2048;
+__device__ __forceinline__ uint32_t big_buckets(uint32_t L) {
+  return min(kBktMax, (L + kBktAvg - 1u) / kBktAvg);
+}
+
 // one workgroup: segment counts of the big lists -> exclusive prefix
 __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buffers b) {
-  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t wsum[16], wsum_b[16];
   __shared__ uint32_t s_maxl;
   const uint32_t n_big = b.counters[0];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_maxl = 0;
-  uint32_t carry = 0, maxl = 0;
+  uint32_t carry = 0, carry_b = 0, maxl = 0;
   for (uint32_t j0 = 0; j0 < n_big; j0 += 1024) {
     const uint32_t j = j0 + (uint32_t)tid;
-    uint32_t c = 0;
+    uint32_t c = 0, nb = 0;
     if (j < n_big) {
       uint32_t s, L;
       tile_segment(fp, b, (int)b.big_tiles[j], s, L);
       c = (L + kBigSeg - 1) / kBigSeg;
+      nb = big_buckets(L);
       maxl = max(maxl, L);
     }
-    uint32_t inc = c;
+    uint32_t inc = c, inc_b = nb;
     for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += o;
+      const uint32_t o = __shfl_up(inc, d, 64), ob = __shfl_up(inc_b, d, 64);
+      if (lane >= d) {
+        inc += o;
+        inc_b += ob;
+      }
     }
-    if (lane == 63) wsum[wave] = inc;
+    if (lane == 63) {
+      wsum[wave] = inc;
+      wsum_b[wave] = inc_b;
+    }
     __syncthreads();
-    uint32_t before = 0, tot = 0;
+    uint32_t before = 0, tot = 0, before_b = 0, tot_b = 0;
     for (int w = 0; w < 16; ++w) {
       before += w < wave ? wsum[w] : 0u;
       tot += wsum[w];
+      before_b += w < wave ? wsum_b[w] : 0u;
+      tot_b += wsum_b[w];
     }
     if (j < n_big) {
       const uint32_t off = carry + before + inc - c;
       b.tile_cursor[j] = off;
       for (uint32_t q = 0; q < c; ++q) b.big_item[off + q] = j;  // segment -> list slot
+      b.bk_off[j] = carry_b + before_b + inc_b - nb;              // the list's first bucket
     }
     carry += tot;
+    carry_b += tot_b;
     __syncthreads();
   }
   atomicMax(&s_maxl, maxl);
@@ -1615,6 +1650,7 @@ __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buf
   if (tid == 0) {
     b.counters[12] = carry;   // segments of all big lists
     b.counters[13] = s_maxl;  // the longest big list (passes beyond it are no-ops)
+    b.counters[14] = carry_b; // sample-sort buckets of all big lists
   }
 }
 
@@ -1625,6 +1661,7 @@ __device__ __forceinline__ void big_item(const Buffers& b, uint32_t n_big, uint3
   c = k - b.tile_cursor[j];
 }
 
+#if !GS_BIG_SAMPLE  // the segmented merge sort (A/B reference)
 // Co-rank of diagonal k in the merge of sorted A[0, la) and B[0, lb) (the
 // number of outputs < k taken from A), by one wave: 64 probes per step cut
 // the interval ~65-fold (log_65 instead of log_2 dependent global loads).
@@ -1753,7 +1790,187 @@ __global__ __launch_bounds__(256) void gs_big_merge_kernel(FrameParams fp, Buffe
     __syncthreads();
   }
 }
+#endif
 
+// ---- big lists as a sample sort (FrameParams::big_separate, the default):
+// per list, splitters from a sorted regular sample of its keys cut it into
+// buckets of ~1024 keys; one pass counts the keys per bucket, a scan turns
+// the counts into bucket starts, one pass scatters the keys (input-index
+// keys, pairs -> pairs_alt) and every bucket is then sorted by one workgroup
+// (the medium path; the radix path for a bucket > kSortLdsCap) straight into
+// its place in the list.  Buckets split the lists by depth only (keys of
+// equal depth share one), so the buckets sort device-index keys and put runs
+// of equal depth in input order like the medium lists.  The splitters only
+// set the buckets' sizes, never the order.  Every key is read 4 times and
+// written twice, against ~8 + 16 per key for the segmented merge sort's
+// seven passes at config 5's 162 k-key lists.
+
+// one workgroup per big list (grid-stride): sample, sort it, pick splitters;
+// zero the list's bucket counters
+__global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long keys[kSortLdsCap];
+  const uint32_t n_big = b.counters[0];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t j = blockIdx.x; j < n_big; j += gridDim.x) {
+    uint32_t s, L;
+    tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+    const uint32_t B = big_buckets(L), bo = b.bk_off[j];
+    const uint32_t S = min((uint32_t)kSortLdsCap, 16u * B);  // sample size
+    for (uint32_t k = tid; k < S; k += 256u) {
+      const uint32_t p = (uint32_t)(((2ull * k + 1ull) * L) / (2ull * S));
+      keys[k] = b.pairs[s + p];
+    }
+    __syncthreads();
+    merge_sort_tile<256, 2, kOutLds, kSrcLds>(b, 0u, S, keys);
+    for (uint32_t t = tid; t < B; t += 256u) {
+      if (t + 1u < B) b.bk_spl[bo + t] = keys[((unsigned long long)(t + 1u) * S) / B - 1u];
+      b.bk_cnt[bo + t] = 0u;
+      b.bk_list[bo + t] = j;
+    }
+    __syncthreads();
+  }
+}
+
+// the bucket of key k: the number of splitters of lower DEPTH (keys of equal
+// depth share a bucket, so the bucket sort puts their runs in input order)
+__device__ __forceinline__ uint32_t big_bucket_of(const unsigned long long* spl, uint32_t nspl,
+                                                  unsigned long long k) {
+  const uint32_t kz = (uint32_t)(k >> 32);
+  uint32_t lo = 0u, hi = nspl;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((uint32_t)(spl[mid] >> 32) < kz) lo = mid + 1u;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// one workgroup per 2048-key work item: count the keys per bucket (LDS
+// histogram, then one global add per non-empty bucket)
+// SCATTER: the second pass -- reserve each bucket's range and write the keys
+// to pairs_alt at bucket start + reserved base + rank
+template <bool SCATTER>
+__device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buffers& b) {
+  __shared__ unsigned long long s_spl[kBktMax];
+  __shared__ uint32_t s_h[kBktMax], s_base[SCATTER ? kBktMax : 1];
+  __shared__ uint32_t s_par[4];
+  const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
+  const uint32_t tid = threadIdx.x;
+  constexpr int Q = kBigSeg / 256;
+  for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
+    if (tid == 0) {
+      uint32_t j, c;
+      big_item(b, n_big, k, j, c);
+      uint32_t s, L;
+      tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+      s_par[0] = s;
+      s_par[1] = L;
+      s_par[2] = c;
+      s_par[3] = b.bk_off[j];
+    }
+    __syncthreads();
+    const uint32_t s = s_par[0], L = s_par[1], c = s_par[2], bo = s_par[3];
+    const uint32_t B = big_buckets(L);
+    for (uint32_t t = tid; t < B; t += 256u) {
+      if (t + 1u < B) s_spl[t] = b.bk_spl[bo + t];
+      s_h[t] = 0u;
+    }
+    __syncthreads();
+    unsigned long long key[Q];
+    uint32_t bk[Q], rk[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
+      key[q] = i < L ? b.pairs[s + i] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
+      if (i < L) {
+        bk[q] = big_bucket_of(s_spl, B - 1u, key[q]);
+        rk[q] = atomicAdd(&s_h[bk[q]], 1u);
+      }
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < B; t += 256u) {
+      const uint32_t n = s_h[t];
+      if constexpr (SCATTER) s_base[t] = n ? b.bk_start[bo + t] + atomicAdd(&b.bk_cnt[bo + t], n) : 0u;
+      else if (n) atomicAdd(&b.bk_cnt[bo + t], n);
+    }
+    __syncthreads();
+    if constexpr (SCATTER) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
+        if (i < L) b.pairs_alt[s + s_base[bk[q]] + rk[q]] = key[q];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gs_big_count_kernel(FrameParams fp, Buffers b) {
+  big_bucket_pass<false>(fp, b);
+}
+
+__global__ __launch_bounds__(256) void gs_big_scatter_kernel(FrameParams fp, Buffers b) {
+  big_bucket_pass<true>(fp, b);
+}
+
+// one wave per big list: bucket counts -> bucket starts (exclusive, within the
+// list); the counters are reset for the scatter's reservations
+__global__ __launch_bounds__(256) void gs_big_bscan_kernel(FrameParams fp, Buffers b) {
+  const uint32_t n_big = b.counters[0];
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * 4u;
+  for (uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6); j < n_big; j += nw) {
+    uint32_t s, L;
+    tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+    const uint32_t B = big_buckets(L), bo = b.bk_off[j];
+    uint32_t carry = 0u;
+    for (uint32_t t0 = 0; t0 < B; t0 += 64u) {
+      const uint32_t t = t0 + (uint32_t)lane;
+      const uint32_t n = t < B ? b.bk_cnt[bo + t] : 0u;
+      uint32_t inc = n;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+      }
+      if (t < B) {
+        b.bk_start[bo + t] = carry + inc - n;
+        b.bk_cnt[bo + t] = 0u;
+      }
+      carry += (uint32_t)__shfl(inc, 63, 64);
+    }
+  }
+}
+
+// one workgroup per bucket (grid-stride): sort it into its place in the list
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_bsort_kernel(FrameParams fp, Buffers b) {
+  constexpr int NT = 256, NW = NT / 64;
+  constexpr int kRadixWords = 8 * 256 + 256 + NW * 256;
+  constexpr int kWords = 2 * kSortLdsCap > kRadixWords ? 2 * kSortLdsCap : kRadixWords;
+  __shared__ unsigned long long keys[kWords / 2];
+  uint32_t* const r_hist = (uint32_t*)keys;
+  uint32_t* const r_base = r_hist + 8 * 256;
+  uint32_t(*const r_wcnt)[256] = (uint32_t(*)[256])(r_hist + 9 * 256);
+  const uint32_t n_bk = b.counters[0] ? b.counters[14] : 0u;
+  for (uint32_t k = blockIdx.x; k < n_bk; k += gridDim.x) {
+    const uint32_t j = b.bk_list[k];
+    uint32_t s, L;
+    tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+    const uint32_t bo = b.bk_off[j], B = big_buckets(L);
+    const uint32_t st = b.bk_start[k], en = k + 1u < bo + B ? b.bk_start[k + 1u] : L;
+    const uint32_t n = en - st;
+    if (n == 0u) continue;  // (uniform)
+    if (n > (uint32_t)kSortLdsCap) {
+      radix_sort_seg<NT, 4, true>(b, s + st, n, r_hist, r_base, r_wcnt);
+    } else if (!merge_sort_tile<NT, 2, kOutDevice, kSrcAlt>(b, s + st, n, keys)) {
+      __syncthreads();  // a long run of equal depths: again with input-index keys
+      merge_sort_tile<NT, 2, kOutInput, kSrcAltRekey>(b, s + st, n, keys);
+    }
+    __syncthreads();
+  }
+}
 
 // -------------------------------------------------------------------- blend
 __device__ __forceinline__ uint8_t to_u8(float v) {
@@ -2098,9 +2315,17 @@ void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     // list's last one skip it)
     const unsigned grid = 4096;
     gs_big_prefix_kernel<<<1, 1024, 0, s>>>(fp, b);
+#if GS_BIG_SAMPLE
+    gs_big_split_kernel<<<1024, 256, 0, s>>>(fp, b);
+    gs_big_count_kernel<<<grid, 256, 0, s>>>(fp, b);
+    gs_big_bscan_kernel<<<256, 256, 0, s>>>(fp, b);
+    gs_big_scatter_kernel<<<grid, 256, 0, s>>>(fp, b);
+    gs_big_bsort_kernel<<<grid, 256, 0, s>>>(fp, b);
+#else
     gs_big_segsort_kernel<<<grid, 256, 0, s>>>(fp, b);
     for (int pass = 0; ((unsigned long long)kBigSeg << pass) < fp.pair_cap && pass < 24; ++pass)
       gs_big_merge_kernel<<<grid, 256, 0, s>>>(fp, b, pass);
+#endif
   }
   // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);

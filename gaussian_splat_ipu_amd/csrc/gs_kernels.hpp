@@ -74,6 +74,12 @@ struct Buffers {
   uint32_t* list;           // [pair_cap]  depth-sorted Gaussians (device indices)
   uint32_t* big_tiles;      // [n_tiles]  lists > kSortLdsCap (radix sort queue)
   uint32_t* big_item;       // [pair_cap / 2048 + n_tiles + 1]  segment k of the big lists -> big-list slot
+  // big-list sample sort: buckets of all big lists, [pair_cap / 1024 + n_tiles + 1] each
+  unsigned long long* bk_spl;  // splitters (bucket t's upper bound, t < B - 1 of its list)
+  uint32_t* bk_start;       // bucket start within its list
+  uint32_t* bk_cnt;         // bucket key count, then the scatter's reservation cursor
+  uint32_t* bk_list;        // bucket -> big-list slot
+  uint32_t* bk_off;         // [n_tiles + 1]  big-list slot -> first bucket
   uint32_t* medium_tiles;   // [n_tiles]  lists in (kSortRegCap, kSortLdsCap] (block sort queue)
   uint32_t* small_tiles;    // [n_tiles]  lists in [1, kSortRegCap] (one-wave sort queue)
   uint32_t* chunk_off;      // [n_chunks][n_tiles] chunk histograms -> offsets
@@ -86,7 +92,8 @@ struct Buffers {
   uint32_t* counters;       // [16]: 0 n_big, 1 big_next, 2 n_rendered, 3 overflow,
                             //  4 max_list, 5 n_pairs (low), 6 n_pairs (high),
                             //  7 n_medium, 8 medium_next, 9 n_small,
-                            //  10 / 11 reference pairs (low / high: unculled lists)
+                            //  10 / 11 reference pairs (low / high: unculled lists),
+                            //  12 big-list work items, 13 longest big list, 14 big-list buckets
   // outputs
   float4* rgba;             // band_rows x width, row-major
   uint8_t* bgr;             // band rows (padded) x width x 3

@@ -159,16 +159,28 @@ std::vector<uint32_t> morton_order(const gs_gaussian3d* g, size_t n, bool keep) 
 
 int alloc_pairs(gs_renderer* r, uint64_t cap) {
   free_pairs(r);
-  // + one u32 per 2048-key segment a big list can have (segmented merge sort)
+  // + one u32 per 2048-key work item a big list can have, and the big-list
+  // sample sort's bucket tables (one bucket per ~1024 keys)
   const size_t n_items = (size_t)(cap / 2048) + (size_t)r->n_tiles + 1;
-  const size_t bytes = (size_t)cap * (8 + 8 + 4) + n_items * 4;
+  const size_t n_bk = (size_t)(cap / 1024) + (size_t)r->n_tiles + 1;
+  const size_t bytes = (size_t)cap * (8 + 8 + 4) + n_bk * 8 + n_items * 4 + n_bk * 12 +
+                       ((size_t)r->n_tiles + 1) * 4;
   GS_HIP(hipMalloc(&r->d_pairs, bytes));
   r->pair_cap = cap;
   char* p = (char*)r->d_pairs;
   r->buf.pairs = (unsigned long long*)p;
   r->buf.pairs_alt = (unsigned long long*)(p + (size_t)cap * 8);
-  r->buf.list = (uint32_t*)(p + (size_t)cap * 16);
-  r->buf.big_item = (uint32_t*)(p + (size_t)cap * 20);
+  p += (size_t)cap * 16;
+  r->buf.bk_spl = (unsigned long long*)p;
+  p += n_bk * 8;
+  r->buf.list = (uint32_t*)p;
+  p += (size_t)cap * 4;
+  r->buf.big_item = (uint32_t*)p;
+  p += n_items * 4;
+  r->buf.bk_start = (uint32_t*)p;
+  r->buf.bk_cnt = r->buf.bk_start + n_bk;
+  r->buf.bk_list = r->buf.bk_cnt + n_bk;
+  r->buf.bk_off = r->buf.bk_list + n_bk;
   return GS_OK;
 }
 

@@ -503,7 +503,7 @@ def test_render_server_cli(built, tmp_path):
 
 
 @pytest.mark.parametrize("half_width,log_scale,planes", [
-    (1.5, -3.8, 4), (0.3, -4.0, 4), (1.5, -3.8, 64), (0.3, -4.0, 400)])
+    (1.5, -3.8, 4), (0.3, -4.0, 4), (1.5, -3.8, 64), (0.3, -4.0, 400), (0.3, -4.0, 1)])
 def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
     """Gaussians on planes of constant clip z (a view that only translates
     along z), in shuffled input order: the tile lists hold runs of equal
@@ -512,7 +512,8 @@ def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
     small lists; 0.3 small, medium and > 2048-key lists (radix sort on the
     first frame, the segmented merge sort on the second).  4 planes make long
     runs (the list is re-sorted), 64 / 400 planes mostly short ones (put in
-    order in place)."""
+    order in place); one plane gives big lists of a single depth (one
+    sample-sort bucket > 2048 keys: its radix path)."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
 
