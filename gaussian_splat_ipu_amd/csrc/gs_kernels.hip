@@ -548,7 +548,7 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
       sum += c[j];
       mx = max(mx, c[j]);
       const int cl = sort_class(c[j]);
-      q += cl == 0 ? (c[j] != 0u ? 1u : 0u) : (cl == 1 ? (1u << 10) : (1u << 20));
+      q += cl == 0 ? 1u : (cl == 1 ? (1u << 10) : (1u << 20));  // small queue: empty tiles too
     }
     unsigned long long inc = sum;
     uint32_t qinc = q;
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
         b.tile_start[i] = (uint32_t)run;
         if (fp.bin_global) b.tile_cursor[i] = (uint32_t)run;
         const int cl = sort_class(c[j]);
-        if (cl == 0 && c[j] != 0u) b.small_tiles[sml++] = (uint32_t)i;
+        if (cl == 0) b.small_tiles[sml++] = (uint32_t)i;
         if (cl == 1) b.medium_tiles[med++] = (uint32_t)i;
         if (cl == 2) b.big_tiles[big++] = (uint32_t)i;
       }
@@ -2104,9 +2104,19 @@ template <int BQW>
 __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wid = blockIdx.x * GS_BLEND_WPG + wave;
-  const int tile = wid / fp.chunks_per_tile;
-  const int chunk = wid - tile * fp.chunks_per_tile;
-  if (tile >= fp.n_tiles) return;
+  const int slot = wid / fp.chunks_per_tile;
+  const int chunk = wid - slot * fp.chunks_per_tile;
+  if (slot >= fp.n_tiles) return;
+  // row bands: longest lists first (the sort queues: big, medium, then small
+  // and empty tiles), so the heaviest tiles' waves start at once instead of
+  // where the tile order puts them (8 bands: blend 35.7 -> 29.3 us).  The
+  // full frame keeps the tile order (neighbouring tiles share records in L2:
+  // 75.1 against 76.1 us in queue order).
+  int tile = slot;
+  if (fp.blend_lpt) {
+    const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
+    tile = (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
+  }
   const int lane = threadIdx.x & 63;
   const int myq = lane >> 2;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;

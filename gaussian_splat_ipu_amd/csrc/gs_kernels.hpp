@@ -31,6 +31,7 @@ struct FrameParams {
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
   int chunks_per_tile;  // blend waves per tile (16 pixel quads each)
   int blend_bqw;        // blend wave = 4x4 quads (8x8 px) | 8x2 quads (16x4 px) | 0: quad run
+  int blend_lpt;        // blend tiles longest list first (row bands), else in tile order
   unsigned long long pair_cap;
   int write_rgba;
   int bgr_pitch;      // bytes per row of the BGR8 output

@@ -246,6 +246,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.chunks_per_tile = fp.blend_bqw == 4   ? (int)((tw / 8) * (th / 8))
                        : fp.blend_bqw == 8 ? (int)((tw / 16) * (th / 4))
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
+  fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
