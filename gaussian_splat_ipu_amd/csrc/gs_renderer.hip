@@ -564,6 +564,11 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
     cs = std::min<size_t>(cs, 65535);
     r->chunk_size = (int)cs;
     r->n_chunks = (int)((n + cs - 1) / cs);
+    // gs_colscan_kernel holds at most 16 chunk rows per wave (16 waves): 256
+    if (r->n_chunks > 256) {
+      set_error("gs_create: internal: more than 256 binning chunks");
+      return fail(GS_EINVAL);
+    }
     if ((e = hipMalloc(&r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4)) != hipSuccess)
       return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
     r->buf.chunk_off = (uint32_t*)r->d_chunk;
