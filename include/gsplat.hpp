@@ -72,6 +72,21 @@ class GpuSplatter {
   // GraphManager::execute(splatter): one blocking frame
   void execute() { gs_check(gs_render(r_), "gs_render"); }
 
+  // frames in flight (no reference counterpart): enqueue on the renderer's
+  // stream / wait for it; the stream (a hipStream_t) for ordering caller work
+  void executeAsync() { gs_check(gs_render_async(r_), "gs_render_async"); }
+  void sync() { gs_check(gs_sync(r_), "gs_sync"); }
+  void* stream() {
+    void* s = nullptr;
+    gs_check(gs_get_stream(r_, &s), "gs_get_stream");
+    return s;
+  }
+  // later frames write their padded BGR8 band at dst (device memory; nullptr:
+  // the renderer's own buffer), e.g. a slot of an all-gather buffer
+  void setBgr8Target(void* dst, size_t bytes) {
+    gs_check(gs_set_bgr8_target(r_, dst, bytes), "gs_set_bgr8_target");
+  }
+
   // getFrameBuffer(cv::Mat&): band rows x width x 3, 8-bit BGR, row-major
   void getFrameBuffer(std::vector<uint8_t>& bgr) {
     const gs_frame_stats st = stats();
