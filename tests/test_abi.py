@@ -68,3 +68,32 @@ def test_create_rejects_bad_config_without_touching_the_device(built):
     assert rc == _lib.GS_EINVAL
     assert "invalid configuration" in _lib.last_error()
     assert L.gs_render(None) == _lib.GS_EINVAL
+
+
+def test_cpp_wrapper_compiles_and_links(built, tmp_path):
+    """include/gsplat.hpp (splat::GpuSplatter, the IpuSplatter mirror) compiles
+    against the header and links against libgsplat.so; the program calls only
+    device-free entry points."""
+    import subprocess
+
+    from gaussian_splat_ipu_amd import _lib
+
+    src = tmp_path / "w.cpp"
+    src.write_text(
+        '#include "gsplat.hpp"\n'
+        "#include <cstdio>\n"
+        "int main() {\n"
+        "  gs_config c;\n"
+        "  splat::gs_check(gs_config_init(&c), \"init\");\n"
+        "  splat::GpuSplatter* p = nullptr;  // the class is instantiable\n"
+        "  (void)p;\n"
+        "  std::printf(\"%d %u\\n\", gs_abi_version(), c.tile_width);\n"
+        "  return 0;\n"
+        "}\n"
+    )
+    exe = tmp_path / "w"
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                    "-L", libdir, "-lgsplat", f"-Wl,-rpath,{libdir}"], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    assert int(out[0]) == 4
