@@ -96,6 +96,8 @@ class FrameStats(C.Structure):
         ("n_big_tiles", C.c_uint32),
         ("band_stride", C.c_uint32),
         ("n_pairs_binned", C.c_uint64),
+        ("bin_global", C.c_uint32),
+        ("reserved0", C.c_uint32),
     ]
 
     def as_dict(self):

@@ -23,10 +23,6 @@
 #include "gs_kernels.hpp"
 
 // blend: 1 = one record mask per pixel (blend 82 -> 78 us), 0 = per 2x2 quad
-// big lists: 1 = sample sort, 0 = segmented merge sort
-#ifndef GS_BIG_SAMPLE
-#define GS_BIG_SAMPLE 1
-#endif
 // blend: waves per workgroup (the waves are independent)
 #ifndef GS_BLEND_WPG
 #define GS_BLEND_WPG 4
@@ -628,6 +624,7 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
     const unsigned long long total = carry;
     b.tile_start[T] = (uint32_t)(total < 0xFFFFFFFFull ? total : 0xFFFFFFFFull);
     b.counters[3] = total > fp.pair_cap ? 1u : 0u;
+    if (total > fp.pair_cap) *b.host_sticky = 1u;  // sticky until the host's sync
     b.counters[4] = m;
     b.counters[5] = (uint32_t)total;
     b.counters[6] = (uint32_t)(total >> 32);
@@ -898,6 +895,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
       b.counters[1] = 0;
       b.counters[2] = s_mx[0] + s_mx[1] + s_mx[2] + s_mx[3];
       b.counters[3] = ts > fp.pair_cap ? 1u : 0u;
+      if (ts > fp.pair_cap) *b.host_sticky = 1u;  // sticky until the host's sync
       b.counters[4] = mx;
       b.counters[5] = (uint32_t)ts;
       b.counters[6] = (uint32_t)(ts >> 32);
@@ -1661,136 +1659,6 @@ __device__ __forceinline__ void big_item(const Buffers& b, uint32_t n_big, uint3
   c = k - b.tile_cursor[j];
 }
 
-#if !GS_BIG_SAMPLE  // the segmented merge sort (A/B reference)
-// Co-rank of diagonal k in the merge of sorted A[0, la) and B[0, lb) (the
-// number of outputs < k taken from A), by one wave: 64 probes per step cut
-// the interval ~65-fold (log_65 instead of log_2 dependent global loads).
-__device__ __forceinline__ uint32_t corank_wave(const unsigned long long* A, uint32_t la,
-                                                const unsigned long long* B, uint32_t lb, uint32_t k,
-                                                int lane) {
-  uint32_t lo = k > lb ? k - lb : 0u, hi = min(k, la);  // answer in [lo, hi]
-  while (hi > lo) {
-    const uint32_t span = hi - lo;
-    // probe p: "A[p] <= B[k - 1 - p]" holds exactly for p < answer
-    const uint32_t p = span <= 64u ? lo + (uint32_t)lane
-                                   : lo + (uint32_t)(((unsigned long long)span * (uint32_t)(lane + 1)) / 65u);
-    const bool in = p < hi;
-    const bool t = in && A[p] <= B[k - 1 - p];
-    const unsigned long long mt = ballot64(t), mf = ballot64(in && !t);
-    // the last true probe + 1 and the first false probe bound the answer
-    const uint32_t nlo = mt ? (uint32_t)__builtin_amdgcn_readlane((int)p, 63 - __builtin_clzll(mt)) + 1u : lo;
-    const uint32_t nhi = mf ? (uint32_t)__builtin_amdgcn_readlane((int)p, __builtin_ctzll(mf)) : hi;
-    lo = nlo;
-    hi = nhi;
-  }
-  return lo;
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_segsort_kernel(FrameParams fp, Buffers b) {
-  __shared__ unsigned long long keys[kSortLdsCap];
-  __shared__ uint32_t s_item[2];
-  const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
-  for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
-    if (threadIdx.x == 0) {
-      uint32_t j, c;
-      big_item(b, n_big, k, j, c);
-      s_item[0] = j;
-      s_item[1] = c;
-    }
-    __syncthreads();
-    const uint32_t j = s_item[0], c = s_item[1];
-    __syncthreads();
-    uint32_t s, L;
-    tile_segment(fp, b, (int)b.big_tiles[j], s, L);
-    const uint32_t s0 = s + c * kBigSeg;
-    const uint32_t n = min((uint32_t)kBigSeg, L - c * kBigSeg);
-    merge_sort_tile<256, 2, kOutKeys, kSrcRekey>(b, s0, n, keys);
-  }
-}
-
-__global__ __launch_bounds__(256) void gs_big_merge_kernel(FrameParams fp, Buffers b, int pass) {
-  __shared__ unsigned long long sab[kBigSeg];  // the A range, then the B range
-  __shared__ uint32_t s_par[8];
-  const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
-  const uint32_t R = (uint32_t)kBigSeg << pass;  // sorted run length before this pass
-  if (R >= b.counters[13]) return;                // every list already merged
-  const unsigned long long* src = (pass & 1) ? b.pairs_alt : b.pairs;
-  unsigned long long* dst = (pass & 1) ? b.pairs : b.pairs_alt;
-  const int tid = threadIdx.x;
-  for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
-    if (tid == 0) {
-      uint32_t j, c;
-      big_item(b, n_big, k, j, c);
-      uint32_t s, L;
-      tile_segment(fp, b, (int)b.big_tiles[j], s, L);
-      s_par[0] = s;
-      s_par[1] = L;
-      s_par[2] = c;
-    }
-    __syncthreads();
-    const uint32_t s = s_par[0], L = s_par[1], c = s_par[2];
-    __syncthreads();
-    if (R >= L) continue;  // merged by an earlier pass (uniform)
-    const bool last = 2 * R >= L;
-    const uint32_t d0 = c * kBigSeg, d1 = min(L, d0 + kBigSeg);
-    const uint32_t base = d0 / (2 * R) * (2 * R);
-    const uint32_t la = min(R, L - base), lb = L - base > R ? min(R, L - base - R) : 0u;
-    const unsigned long long* A = src + s + base;
-    const unsigned long long* B = A + la;
-    // the output range's split of the two runs (waves 0 and 1)
-    if (tid < 128) {
-      const uint32_t r = corank_wave(A, la, B, lb, (tid < 64 ? d0 : d1) - base, tid & 63);
-      if ((tid & 63) == 0) s_par[3 + (tid >> 6)] = r;
-    }
-    __syncthreads();
-    const uint32_t i0 = s_par[3], i1 = s_par[4];
-    const uint32_t j0 = d0 - base - i0, j1 = d1 - base - i1;
-    const uint32_t na = i1 - i0, nb = j1 - j0;
-    __syncthreads();
-    unsigned long long* const sa = sab;
-    unsigned long long* const sb = sab + na;
-    {  // stage A[i0, i1) then B[j0, j1): all 8 loads of a thread in flight at once
-      unsigned long long tmp[kBigSeg / 256];
-#pragma unroll
-      for (int q = 0; q < kBigSeg / 256; ++q) {
-        const uint32_t t = (uint32_t)tid + (uint32_t)q * 256u;
-        tmp[q] = t < na ? A[i0 + t] : (t < na + nb ? B[j0 + t - na] : 0ull);
-      }
-#pragma unroll
-      for (int q = 0; q < kBigSeg / 256; ++q) {
-        const uint32_t t = (uint32_t)tid + (uint32_t)q * 256u;
-        if (t < na + nb) sab[t] = tmp[q];
-      }
-    }
-    __syncthreads();
-    // 8 consecutive outputs per thread
-    const uint32_t o0 = (uint32_t)tid * 8u, nout = na + nb;
-    if (o0 < nout) {
-      uint32_t lo = o0 > nb ? o0 - nb : 0u, hi = min(o0, na);
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sa[mid] <= sb[o0 - 1 - mid]) lo = mid + 1;
-        else hi = mid;
-      }
-      uint32_t ia = lo, ib = o0 - lo;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t o = o0 + (uint32_t)e;
-        if (o < nout) {
-          const unsigned long long av = ia < na ? sa[ia] : ~0ull, bv = ib < nb ? sb[ib] : ~0ull;
-          const bool ta = ib >= nb || (ia < na && av <= bv);
-          const unsigned long long v = ta ? av : bv;
-          ia += ta ? 1u : 0u;
-          ib += ta ? 0u : 1u;
-          if (last) b.list[s + d0 + o] = b.inv_perm[(uint32_t)v];
-          else dst[s + d0 + o] = v;
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-#endif
 
 // ---- big lists as a sample sort (FrameParams::big_separate, the default):
 // per list, splitters from a sorted regular sample of its keys cut it into
@@ -2325,17 +2193,11 @@ void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     // list's last one skip it)
     const unsigned grid = 4096;
     gs_big_prefix_kernel<<<1, 1024, 0, s>>>(fp, b);
-#if GS_BIG_SAMPLE
     gs_big_split_kernel<<<1024, 256, 0, s>>>(fp, b);
     gs_big_count_kernel<<<grid, 256, 0, s>>>(fp, b);
     gs_big_bscan_kernel<<<256, 256, 0, s>>>(fp, b);
     gs_big_scatter_kernel<<<grid, 256, 0, s>>>(fp, b);
     gs_big_bsort_kernel<<<grid, 256, 0, s>>>(fp, b);
-#else
-    gs_big_segsort_kernel<<<grid, 256, 0, s>>>(fp, b);
-    for (int pass = 0; ((unsigned long long)kBigSeg << pass) < fp.pair_cap && pass < 24; ++pass)
-      gs_big_merge_kernel<<<grid, 256, 0, s>>>(fp, b, pass);
-#endif
   }
   // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);

@@ -90,6 +90,8 @@ struct Buffers {
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
   uint32_t* host_counters;  // mapped pinned mirror of counters[16] + tile_count[n_tiles],
                             //   written by the chunked scan (no D2H copy per frame)
+  uint32_t* host_sticky;    // mapped pinned word: set by the scan of any frame that
+                            //   overflowed the pair capacity, cleared by the host at sync
   uint32_t* counters;       // [16]: 0 n_big, 1 big_next, 2 n_rendered, 3 overflow,
                             //  4 max_list, 5 n_pairs (low), 6 n_pairs (high),
                             //  7 n_medium, 8 medium_next, 9 n_small,

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -77,6 +78,11 @@ struct gs_renderer {
   uint8_t* last_bgr = nullptr;    // where the last enqueued frame wrote its BGR8
   bool have_frame = false;
   gs_frame_stats stats{};
+  // the parameters of the last enqueued frame: the debug readbacks
+  // (gs_read_projected, gs_read_bins) reproduce THAT frame, not the current
+  // camera (a gs_set_view after the frame changes nothing they return)
+  gsk::FrameParams last_fp{};
+  bool have_fp = false;
 
   // profiling
   bool profile = false;
@@ -296,6 +302,8 @@ int enqueue_frame(gs_renderer* r) {
   // several frames may be in flight on the stream; the host mirrors always
   // hold the last one's counters after gs_sync
   const gsk::FrameParams fp = make_params(r);
+  r->last_fp = fp;
+  r->have_fp = true;
   hipStream_t s = r->stream;
   // BGR8 destination of this frame (gs_set_bgr8_target)
   r->buf.bgr = r->bgr_target ? r->bgr_target : r->own_bgr;
@@ -354,9 +362,14 @@ int finish_frame(gs_renderer* r) {
   r->stats.max_list = mx;
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
-  if (c[3]) {
-    set_error("pair list overflow: " + std::to_string(P) + " pairs > capacity " +
-              std::to_string(r->pair_cap));
+  // the scan of EVERY frame ORs its overflow into the sticky word (several
+  // frames may have run since the last sync; counters[3] is only the last one's)
+  volatile uint32_t* sticky = r->h_counters + 16 + r->n_tiles;
+  const bool ovf = c[3] != 0 || *sticky != 0;
+  *sticky = 0;
+  if (ovf) {
+    set_error("pair list overflow: a frame since the last sync binned more pairs than the capacity " +
+              std::to_string(r->pair_cap) + " (last frame: " + std::to_string(P) + " pairs)");
     return GS_EOVERFLOW;
   }
   {
@@ -559,20 +572,26 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   // large for one CU's LDS (or the caller asks for the global-atomic path)
   r->bin_global = ((cfg->flags & GS_FLAG_BIN_GLOBAL) || !gsk::bin_lds_fits(r->n_tiles)) ? 1 : 0;
   if (!r->bin_global && n > 0 && r->n_tiles > 0) {
-    if ((e = gsk::init_kernel_attributes()) != hipSuccess) return fail(hip_fail(e, "hipFuncSetAttribute"));
     size_t cs = std::max<size_t>(4096, (n + 255) / 256);
     cs = std::min<size_t>(cs, 65535);
-    r->chunk_size = (int)cs;
-    r->n_chunks = (int)((n + cs - 1) / cs);
     // gs_colscan_kernel holds at most 16 chunk rows per wave (16 waves): 256
-    if (r->n_chunks > 256) {
-      set_error("gs_create: internal: more than 256 binning chunks");
-      return fail(GS_EINVAL);
+    // chunks of <= 65535 Gaussians, i.e. scenes up to ~16.7 M.  Larger scenes
+    // bin with the global-atomic path instead of failing.  (GSPLAT_BIN_MAX_CHUNKS
+    // lowers the limit so the fallback can be tested at small N.)
+    int max_chunks = 256;
+    if (const char* ev = std::getenv("GSPLAT_BIN_MAX_CHUNKS")) max_chunks = std::max(1, std::min(256, std::atoi(ev)));
+    if ((n + cs - 1) / cs > (size_t)max_chunks) {
+      r->bin_global = 1;
+    } else {
+      if ((e = gsk::init_kernel_attributes()) != hipSuccess) return fail(hip_fail(e, "hipFuncSetAttribute"));
+      r->chunk_size = (int)cs;
+      r->n_chunks = (int)((n + cs - 1) / cs);
+      if ((e = hipMalloc(&r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4)) != hipSuccess)
+        return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
+      r->buf.chunk_off = (uint32_t*)r->d_chunk;
     }
-    if ((e = hipMalloc(&r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4)) != hipSuccess)
-      return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
-    r->buf.chunk_off = (uint32_t*)r->d_chunk;
   }
+  r->stats.bin_global = (uint32_t)r->bin_global;
 
   uint64_t cap = cfg->pair_capacity;
   if (cap == 0) cap = std::max<uint64_t>(1u << 20, 8ull * n);
@@ -590,12 +609,14 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   if ((e = hipMemset(r->d_out, 0, px * 16 + r->bgr_bytes)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(framebuffer)"));
 
-  if ((e = hipHostMalloc((void**)&r->h_counters, r->zero_bytes,
+  // + one sticky overflow word after the list lengths (h_counters[16 + T])
+  if ((e = hipHostMalloc((void**)&r->h_counters, r->zero_bytes + 16,
                          hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
     return fail(hip_fail(e, "hipHostMalloc"));
-  std::memset(r->h_counters, 0, r->zero_bytes);
+  std::memset(r->h_counters, 0, r->zero_bytes + 16);
   if ((e = hipHostGetDevicePointer((void**)&r->buf.host_counters, r->h_counters, 0)) != hipSuccess)
     return fail(hip_fail(e, "hipHostGetDevicePointer"));
+  r->buf.host_sticky = r->buf.host_counters + 16 + T;
   r->hist_snapshot.assign((size_t)r->n_tiles, 0u);
   if (r->profile) {
     for (auto& s : r->ring)
@@ -768,18 +789,47 @@ int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t*
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
-  if (make_params(r).pair_cull) {
-    // the frame's lists hold only the tiles each alpha box meets: bin the
-    // reference lists again (the frame itself comes out identical)
-    r->pair_cull = false;
-    rc = gs_render(r);
-    r->pair_cull = true;
-    if (rc != GS_OK) return rc;
+  if (!r->have_frame || !r->have_fp) {
+    set_error("gs_read_bins: no frame rendered yet");
+    return GS_EINVAL;
   }
   const size_t T = (size_t)r->n_tiles;
   if (n_start < T + 1 || n_list < r->stats.n_pairs) {
     set_error("gs_read_bins: destination too small");
     return GS_EINVAL;
+  }
+  if (r->last_fp.pair_cull) {
+    // The frame binned each Gaussian only into the tiles its alpha box meets.
+    // Bin the reference lists of THAT frame again (its FrameParams, pair cull
+    // off): project, scan, emit and sort only -- no blend, so the framebuffer,
+    // the BGR8 target, the stats and the histogram snapshot are untouched.
+    gsk::FrameParams fp = r->last_fp;
+    fp.pair_cull = 0;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+      fp.pair_cap = r->pair_cap;
+      fp.big_separate = 0;  // the tile sort radix-sorts big lists itself
+      if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
+        GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, r->stream));
+      gsk::launch_project(fp, r->buf, r->stream);
+      gsk::launch_scan(fp, r->buf, r->stream);
+      gsk::launch_emit(fp, r->buf, r->stream);
+      gsk::launch_sort(fp, r->buf, r->stream);
+      GS_HIP(hipGetLastError());
+      if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
+        GS_HIP(hipMemcpyAsync(r->h_counters, r->d_zero, (16 + T) * 4, hipMemcpyDeviceToHost, r->stream));
+      GS_HIP(hipStreamSynchronize(r->stream));
+      volatile uint32_t* sticky = r->h_counters + 16 + r->n_tiles;
+      *sticky = 0;
+      const uint32_t* c = r->h_counters;
+      const uint64_t P = (uint64_t)c[5] | ((uint64_t)c[6] << 32);
+      if (!c[3]) break;
+      const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(P + P / 4 + 1024, 2 * r->pair_cap), 0xFFFFFFF0ull);
+      if (P > 0xFFFFFFF0ull || attempt == 7) {
+        set_error("gs_read_bins: reference lists exceed the pair capacity");
+        return GS_EOVERFLOW;
+      }
+      if ((rc = alloc_pairs(r, cap)) != GS_OK) return rc;
+    }
   }
   std::vector<uint32_t> ts(T + 1);
   GS_HIP(hipMemcpy(ts.data(), r->buf.tile_start, (T + 1) * 4, hipMemcpyDeviceToHost));
@@ -801,13 +851,20 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
+  if (!r->have_fp) {
+    set_error("gs_read_projected: no frame rendered yet");
+    return GS_EINVAL;
+  }
   std::vector<float> rec(r->n * 12), tail(r->n * 2);
   std::vector<uint32_t> rect(r->n * 2);
   if (r->n) {
-    // project again with the readback tail of the record (radius, clip z),
-    // which frames skip, and without the band cull (same values otherwise)
-    gsk::FrameParams fp = make_params(r);
+    // project the last frame's camera again (its FrameParams) with the
+    // readback tail of the record (radius, clip z), which frames skip, and
+    // without the band cull (same values otherwise).  Only the per-Gaussian
+    // scratch of the finished frame is rewritten.
+    gsk::FrameParams fp = r->last_fp;
     fp.band_cull = 0;
+    fp.bin_global = 0;  // (no tile_count atomics)
     fp.full_record = 1;
     gsk::launch_project(fp, r->buf, r->stream);
     GS_HIP(hipGetLastError());

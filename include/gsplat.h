@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 4
+#define GSPLAT_ABI_VERSION 5
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -119,6 +119,10 @@ typedef struct gs_frame_stats {
   uint64_t n_pairs_binned; /* pairs binned, sorted and blended: P minus
                               the pairs culled by the alpha box (= P with
                               GS_FLAG_NO_PAIR_CULL)                   */
+  uint32_t bin_global;    /* ABI 5: 1 = the global-atomic binning path (tile
+                             grids beyond one CU's LDS, scenes beyond 256
+                             binning chunks ~ 16.7 M, or GS_FLAG_BIN_GLOBAL) */
+  uint32_t reserved0;
 } gs_frame_stats;
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */

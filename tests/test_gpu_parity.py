@@ -510,7 +510,7 @@ def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
     depth, whose order must be the input index's (the oracle's stable order),
     not the device (Morton) order the pair keys carry.  half_width 1.5 gives
     small lists; 0.3 small, medium and > 2048-key lists (radix sort on the
-    first frame, the segmented merge sort on the second).  4 planes make long
+    first frame, the big-list sample sort on the second).  4 planes make long
     runs (the list is re-sorted), 64 / 400 planes mostly short ones (put in
     order in place); one plane gives big lists of a single depth (one
     sample-sort bucket > 2048 keys: its radix path)."""
@@ -539,6 +539,6 @@ def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
     assert same.sum() > 500
     if half_width < 1.0:
         assert s.stats()["n_big_tiles"] > 0
-        s.execute()  # big lists through the segmented merge sort
+        s.execute()  # big lists through the big-list sample sort
         _assert_parity(s, f, a)
     assert ref["stats"]["n_pairs"] > 0
