@@ -1,7 +1,8 @@
 """Headline benchmark: frames/sec + Gaussians-splatted/sec of the
 project -> bin -> sort -> blend -> BGR8 frame path at 1920x1080 on a synthetic
-1M-Gaussian SH-3 scene (BASELINE.json configs[2]; configs[3] for N > 1:
-framebuffer tile rows split into N bands, one RCCL all-gather per frame).
+1M-Gaussian SH-3 scene (BASELINE.json configs[2]; configs[3] for N > 1: the
+framebuffer's tile rows split into N bands, one per GPU, one RCCL all-gather
+per frame inside gs_render -- the row-band group of gs_group.hip).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -9,20 +10,33 @@ framebuffer tile rows split into N bands, one RCCL all-gather per frame).
 Prints ONE JSON line on rank 0.  A "step" is one full frame.  The timed region
 covers K frames enqueued back to back (inputs resident in HBM), bracketed by a
 barrier + device synchronise; the value is K / max-over-ranks elapsed.
+
+N = 1: F renderers (frames in flight) take frames round-robin on their own
+streams.  N > 1: each rank is one member of a row-band group
+(gs_create_rank): it renders its band of every frame and joins that frame's
+ncclAllGather; torch.distributed (gloo, host only) carries the RCCL id, the
+barriers and the max-over-ranks reduction.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
-import math
 import os
+import subprocess
 import sys
 import time
+
+# the CPU baseline's OpenMP threads stay on their cores (SURVEY §8 d); set
+# before any OpenMP runtime (torch's, the oracle's) starts
+os.environ.setdefault("OMP_PROC_BIND", "close")
+os.environ.setdefault("OMP_PLACES", "cores")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HEADLINE_METRIC = "frames/sec + Gaussians-splatted/sec at 1080p, 1M-Gaussian scene, 1/2/4/8 MI355X"
 
 
 def parse():
@@ -38,31 +52,29 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--sh-degree", type=int, default=3)
     ap.add_argument("--inflight", type=int, default=3,
-                    help="frames in flight: independent renderers, each with its own buffers and "
-                    "HIP stream, take frames round-robin, so one frame's latency-bound kernels "
-                    "overlap the next frames' work (every frame is rendered in full)")
+                    help="frames in flight: independent renderers (N = 1) or band renderers per GPU "
+                    "(group), each with its own buffers and HIP stream, take frames round-robin, so one "
+                    "frame's latency-bound kernels overlap the next frames' work (every frame is "
+                    "rendered in full)")
     ap.add_argument("--profile-frames", type=int, default=24,
                     help="frames of the isolated one-in-flight pass that times each kernel "
                     "(stage HIP events) for the kernel table and the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--band-mode", choices=["balanced", "interleaved"], default="balanced",
-                    help="N > 1: contiguous tile-row bands split by the work of a calibration "
-                    "frame's row histogram (dist.balanced_bands; the band cull then skips ~7/8 "
-                    "of the scene per rank), or interleaved tile rows (rank r: rows r, r + N, ...)")
-    ap.add_argument("--gather-group", type=int, default=3,
-                    help="N > 1: frames per all-gather = frames in flight x this (the collective's "
-                    "host cost is paid once per group)")
     ap.add_argument("--split", type=int, default=0,
-                    help="row bands of the split (default: the world size); with --gather on one "
-                    "GPU, rank 0 renders band 0 of a --split way split (exercises the N > 1 path)")
+                    help="one process: a row-band group of S bands emulated on this GPU (device ids "
+                    "repeat, device-copy gather): the N > 1 frame path's total work on one GPU")
     ap.add_argument("--config5", action="store_true",
                     help="BASELINE.json configs[4]: 8M Gaussians clustered around point_cloud_12's "
                     "positions (N(0, 0.02) jitter, seed 8), 3840x2160, orbit camera (frame k: "
                     "mvpStart * Ry(360 k / 120)); the tile load-imbalance stress")
     ap.add_argument("--gather", action="store_true",
-                    help="run the band copy + RCCL all-gather path even at N = 1 (a one-rank "
-                    "process group; exercises the multi-GPU frame path on one GPU)")
-    ap.add_argument("--cpu-frames", type=int, default=2)
+                    help="N = 1 through the group path (gs_create_rank, world 1: one ncclAllGather per "
+                    "frame), to exercise the multi-GPU frame path on one GPU")
+    ap.add_argument("--no-rebalance", action="store_true", help="group: keep the first (equal-rows) split")
+    ap.add_argument("--cpu-frames", type=int, default=20, help="timed CPU baseline frames (median)")
+    ap.add_argument("--cpu-warmup", type=int, default=3)
+    ap.add_argument("--cpu-budget-s", type=float, default=30.0,
+                    help="cap on the CPU baseline's timed frames (fewer frames if one takes longer)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return ap.parse_args()
 
@@ -70,9 +82,10 @@ def parse():
 # the kernels behind each timed stage (rocprof short names)
 STAGE_KERNELS = {
     "project": ["gs_project"],
-    "scan": ["gs_count", "gs_colscan", "gs_scan"],
+    "scan": ["gs_count", "gs_colscan", "gs_scan_multi", "gs_scan"],
     "emit": ["gs_emit_chunk", "gs_emit"],
-    "sort": ["gs_sort_tiles", "gs_sort_big"],
+    "sort": ["gs_sort_tiles", "gs_big_prefix", "gs_big_split", "gs_big_count", "gs_big_bscan",
+             "gs_big_scatter", "gs_big_bsort"],
     "blend": ["gs_blend"],
 }
 
@@ -95,25 +108,44 @@ def measured_copy_peak(torch) -> float:
     return round(2 * n / best / 1e9, 1)
 
 
-def alg_bytes(kernel: str, st: dict, n: int, px: int) -> float:
-    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md).
-    P = the pairs actually binned, sorted and blended (n_pairs_binned: the
-    reference rectangle's pairs minus those the alpha box culls)."""
-    T, P = st["n_tiles"], st["n_pairs_binned"]
+def alg_bytes(kernel: str, T: int, P: int, n: int, px: int) -> float:
+    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md §4).
+    P = the pairs actually binned, sorted and blended (the reference rectangle's
+    pairs minus those the alpha box culls); T = tiles; px = pixels written."""
     return {
         "project": n * (56 + 52),
-        "scan": T * 12,
+        "scan": n * 16 + T * 12,  # count reads each Gaussian's two rectangles; tile starts
         "emit": n * 12 + P * 12,
         "sort": P * 24,
         "blend": T * 8 + P * (4 + 36) + px * (16 + 3),
     }[kernel]
 
 
+def host_cpus():
+    """(usable CPUs, physical cores among them) from the affinity mask and lscpu."""
+    cpus = sorted(os.sched_getaffinity(0))
+    phys = None
+    try:
+        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        core_of = {}
+        for line in out.splitlines():
+            if line and not line.startswith("#"):
+                c, core, sock = line.split(",")[:3]
+                core_of[int(c)] = (core, sock)
+        phys = len({core_of[c] for c in cpus if c in core_of}) or None
+    except Exception:
+        phys = None
+    return len(cpus), phys
+
+
+def frame_digest(bgr) -> str:
+    return hashlib.sha1(bgr.tobytes()).hexdigest()[:16]
+
+
 def main():
     a = parse()
     if a.config5:
         a.n, a.width, a.height, a.seed, a.sh_degree = 8_000_000, 3840, 2160, 8, 0
-        a.cpu_frames = 1
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -121,16 +153,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("bench.py --gpus N>1 must be launched with torchrun / torch.distributed.run")
+    if world != a.gpus and world == 1 and a.gpus > 1:
+        raise SystemExit("bench.py --gpus N>1 must be launched with torchrun / torch.distributed.run")
     torch.cuda.set_device(local)
-    dist_on = world > 1 or a.gather
-    if dist_on:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world > 1:
+        # host-side plumbing only (RCCL id, barriers, max over ranks); the
+        # frame's all-gather is libgsplat's own RCCL call inside gs_render
+        dist.init_process_group("gloo")
+    group = world > 1 or a.gather or a.split > 1
 
     from gaussian_splat_ipu_amd import camera, scene
-    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter, comm_id_create
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
 
     W, H, TW = a.width, a.height, a.tile
@@ -146,166 +179,142 @@ def main():
     del ply
     view, proj = camera.headless(bb, W, H)
     fb = TiledFramebuffer(W, H, TW, TW)
-    # N > 1: interleaved tile-row bands (rank r owns rows r, r + N, ...), so
-    # every rank gets an equal share of the scene's dense centre rows.
-    # F frames in flight: F renderers (own buffers, own non-blocking stream
-    # created by libgsplat) take frames round-robin, so one frame's
-    # latency-bound kernels (scans, list tails) overlap the next frames' work.
-    # Every frame is rendered in full.
     F = max(1, a.inflight)
-    # N > 1, balanced: one full frame on every rank gives the row histogram;
-    # every rank derives the same work-balanced split from it
-    bands, pad_rows = None, 0
-    split = a.split if a.split > 0 else world
-    if split > 1 and a.band_mode == "balanced":
-        from gaussian_splat_ipu_amd import dist as gdist
+    views = [camera.orbit_view(k) for k in range(120)] if a.config5 else [view]
 
-        cal = GpuSplatter(g, fb, device=local, write_rgba=False)
-        cal.set_view_wire(view)
-        cal.set_projection_wire(proj)
-        cal.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
-        cal.execute()
-        bands = gdist.balanced_bands(gdist.row_work(cal.get_histogram(), fb), split)
-        cal.close()
-        pad_rows = max(t1 - t0 for t0, t1 in bands)
-    R, streams = [], []
-    for f in range(F):
-        if bands is not None:
-            r = GpuSplatter(g, fb, device=local, band_rows=bands[rank], band_pad_rows=pad_rows,
-                            profile=(f == 0), band_cull=True)
-        else:
-            r = GpuSplatter(g, fb, device=local, band_index=rank, band_count=split, profile=(f == 0),
-                            band_interleaved=split > 1, band_cull=split > 1)
+    def setup(r):
         r.set_view_wire(view)
         r.set_projection_wire(proj)
         r.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
-        R.append(r)
-        streams.append(torch.cuda.ExternalStream(r.get_stream()))
+
+    # ------------------------------------------------------------ renderers
+    split = a.split if a.split > 1 else world
+    if group:
+        if world > 1 or a.gather:
+            cid = comm_id_create() if rank == 0 else None
+            if world > 1:
+                box = [cid]
+                dist.broadcast_object_list(box, src=0)
+                cid = box[0]
+            R = [GpuSplatter(g, fb, device=local, comm_id=cid, rank=rank, world=world, frames_in_flight=F,
+                             profile=True, rebalance=not a.no_rebalance)]
+        else:  # --split S: S bands emulated on this GPU
+            R = [GpuSplatter(g, fb, num_gpus=split, device_ids=[local] * split, frames_in_flight=F,
+                             profile=True, rebalance=not a.no_rebalance)]
+    else:
+        R = [GpuSplatter(g, fb, device=local, profile=(f == 0)) for f in range(F)]
+    for r in R:
+        setup(r)
     s = R[0]
     # no stage events in the timed region (each costs host and device time);
     # the kernel table comes from the isolated pass after it
     s.set_profile_interval(1 << 30)
 
-    # N > 1: each frame writes its padded band into a group buffer; the G
-    # frames of a group (F renderers x --gather-group) are all-gathered by ONE RCCL call
-    # on a communication stream while the next group renders.  Two group
-    # buffers alternate.  (One gather per frame made the host loop the limit:
-    # ~57 us of Python/launch work per frame against ~42 us of GPU work at 8
-    # bands; a group amortises the collective's host cost over F frames.)
-    band_bytes = (pad_rows * TW if bands is not None else fb.rows_per_band_padded(split)) * W * 3
-    G = F * max(1, a.gather_group)
-    gbuf = [torch.empty(G * band_bytes, dtype=torch.uint8, device="cuda") for _ in range(2)] if dist_on else []
-    gout = ([torch.empty(world * G * band_bytes, dtype=torch.uint8, device="cuda") for _ in range(2)]
-            if dist_on else [])
-    comm = torch.cuda.Stream() if dist_on else None
-    ev_copy = [torch.cuda.Event() for _ in range(F)]
-    ev_free = [torch.cuda.Event() for _ in range(2)]
     nframe = [0]
-
-    views = [camera.orbit_view(k) for k in range(120)] if a.config5 else None
-
-    def gather_group(g):
-        bsel = g % 2
-        with torch.cuda.stream(comm):
-            for e in ev_copy:
-                comm.wait_event(e)
-            dist.all_gather_into_tensor(gout[bsel], gbuf[bsel])  # (world, G, band) rank-major
-            ev_free[bsel].record(comm)
 
     def one_frame():
         k = nframe[0]
-        i, g, slot = k % F, k // G, k % G
-        r, st = R[i], streams[i]
-        if views is not None:  # orbit camera: a new view every frame
+        r = R[k % len(R)]
+        if a.config5:  # orbit camera: a new view every frame
             r.set_view_wire(views[k % 120])
-        if dist_on:
-            # the frame writes its band straight into its group-buffer slot
-            # (gs_set_bgr8_target), after the gather of group g - 2 read it:
-            # a renderer's first frame of the group waits for that, and its
-            # last one marks the end of its writes (in-stream order covers the
-            # frames between)
-            bsel = g % 2
-            if slot < F:
-                st.wait_event(ev_free[bsel])
-            r.set_bgr8_target(gbuf[bsel].data_ptr() + slot * band_bytes, band_bytes)
         r.execute_async()
-        if dist_on:
-            if slot >= G - F:
-                ev_copy[i].record(st)
-            if slot == G - 1:
-                gather_group(g)
         nframe[0] += 1
 
-    def flush():  # a partial last group is gathered too
-        if dist_on and nframe[0] % G:
-            for e, st in zip(ev_copy, streams):
-                e.record(st)
-            gather_group(nframe[0] // G)
-
-    # warm-up (the first blocking render sizes the pair buffers; with the
-    # orbit camera every view once, so no timed frame can overflow them)
+    # warm-up: a blocking frame of every view sizes the pair buffers (no timed
+    # frame can overflow them); the group's split settles on the headline view
     for r in R:
-        for v in (views if views is not None else [None]):
-            if v is not None:
-                r.set_view_wire(v)
+        for v in views:
+            r.set_view_wire(v)
             r.execute()
+        r.set_view_wire(views[0])
     for _ in range(a.warmup):
         one_frame()
-    flush()
-    nframe[0] = 0
     for r in R:
         r.sync()
+    nframe[0] = 0
     torch.cuda.synchronize()
-    s.reset_kernel_times()
-    if dist_on:
+    if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_frame()
-    flush()
     t_enq = time.perf_counter()  # host time to enqueue the K frames
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    t1 = time.perf_counter()
     for r in R:
         r.sync()  # raises on pair overflow
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
     elapsed = t1 - t0
-    if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    fps = a.steps / elapsed
+    ms_per_step = 1e3 * elapsed / a.steps
+
+    # the timed frames did the work: each renderer's last timed frame equals a
+    # blocking render of the same view on it
+    check = []
+    for i, r in enumerate(R):
+        last_k = max(k for k in range(a.steps) if k % len(R) == i) if a.steps > i else None
+        if last_k is None:
+            continue
+        d0 = frame_digest(r.get_frame_buffer())
+        r.set_view_wire(views[last_k % 120] if a.config5 else view)
+        r.execute()
+        d1 = frame_digest(r.get_frame_buffer())
+        check.append(d0 == d1)
+    frame_check = {"renderers": len(check), "last_timed_frame_equals_blocking_render": all(check)}
     st = s.stats()
-    for r in R:
-        r.set_bgr8_target(None)
+    bands = s.bands() if group else None
+
     # kernel table: the same frames with one in flight (renderer 0 alone,
     # stage HIP events on its stream around every kernel of every frame), so
     # each duration is the kernel's own, not shared with other frames' work
+    s.set_view_wire(view)
     s.set_profile_interval(1)
     s.execute()
     s.reset_kernel_times()
     for _ in range(a.profile_frames):
-        s.execute_async()
-    s.sync()
+        s.execute()  # blocking: one frame in flight (a group's band + its all-gather)
     kt = s.kernel_times()
-    fps = a.steps / elapsed
-    ms_per_step = 1e3 * elapsed / a.steps
+    st_view = s.stats()
 
-    # per-kernel roofline of this rank's band (rank 0 reports)
-    px = st["band_rows"] * W
+    # algorithmic bytes of the band renderer the table timed (group: rank 0's
+    # band, its pairs estimated from the gathered histogram)
+    if group:
+        hist = s.get_histogram().reshape(fb.tiles_down, fb.tiles_across).astype(np.float64)
+        b0, b1 = bands[rank] if world > 1 else bands[0]
+        share = hist[b0:b1].sum() / max(1.0, hist.sum())
+        T_b = (b1 - b0) * fb.tiles_across
+        P_b = int(round(st_view["n_pairs_binned"] * share))
+        px = (min(H, b1 * TW) - b0 * TW) * W
+    else:
+        T_b, P_b, px = st_view["n_tiles"], st_view["n_pairs_binned"], st_view["band_rows"] * W
     kern = {}
     for name, (avg_ms, cnt) in kt.items():
-        b = alg_bytes(name, st, a.n, px)
+        if name == "gather":
+            if group:
+                kern[name] = {"avg_ms": round(avg_ms, 5), "launches": int(cnt),
+                              "note": "ncclAllGather on the comm stream, local band done -> frame gathered "
+                                      "(includes waiting for the slowest rank)"}
+            continue
+        b = alg_bytes(name, T_b, P_b, a.n, px)
         kern[name] = {
             "avg_ms": round(avg_ms, 5),
             "launches": int(cnt),
             "alg_bytes": int(b),
             "alg_GBps": round(b / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None,
         }
-    dom = max(kern, key=lambda k: kern[k]["avg_ms"])
+    stage = {k: v for k, v in kern.items() if k != "gather"}
+    dom = max(stage, key=lambda k: stage[k]["avg_ms"])
+    # PMC counters are per launch (kernel properties): the key names the
+    # workload, the split and the band, not the frames in flight
+    pmc_key = f"{'c5' if a.config5 else 'c3'}:{a.n}@{W}x{H}/t{TW}/world{world}/split{split}/band{rank}"
     # HBM bytes per launch of the same stage, from the committed PMC summary of
-    # this workload (tools/profile.sh + tools/pmc_summary.py), when it matches
+    # this exact workload (tools/profile.sh + tools/pmc_summary.py), if any
     pmc = None
     valu = None
     if os.path.exists(a.pmc_json):
@@ -313,13 +322,13 @@ def main():
             pm = json.load(open(a.pmc_json))
             ks = pm.get("kernels", {})
             names = [k for k in STAGE_KERNELS[dom] if k in ks]
-            if pm.get("config") == f"{a.n}@{W}x{H}/t{TW}/w{world}" and names:
+            if pm.get("config") == pmc_key and names:
                 pmc = int(sum(ks[k]["hbm_bytes_per_launch"] for k in names))
                 # VALU issue-slot fraction beside the HBM fraction (SURVEY §8 d):
                 # wave64 VALU instructions x 2 cycles over 1024 SIMDs x 2.4 GHz
                 vi = sum(ks[k].get("SQ_INSTS_VALU", 0.0) for k in names)
                 if vi:
-                    valu = round(vi * 2.0 / (1024 * 2.4e9 * kern[dom]["avg_ms"] * 1e-3), 3)
+                    valu = round(min(1.0, vi * 2.0 / (1024 * 2.4e9 * kern[dom]["avg_ms"] * 1e-3)), 3)
         except Exception:
             pmc = None
     dk = kern[dom]
@@ -332,6 +341,7 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": pmc,
+        "traffic_key": pmc_key,
         "alg_bytes_per_launch": dk["alg_bytes"],
         "avg_launch_ms": dk["avg_ms"],
         "valu_issue_frac": valu,
@@ -349,47 +359,32 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        from oracle import oracle as O
-
-        threads = min(16, os.cpu_count() or 1)
-        f = O.make_frame(view, proj, W, H, TW, TW, camera.FOV_DEFAULT, a.scale_div)
-        O.render(g, f, nthreads=threads, want_rgba=False)  # warm (page-in)
-        tc0 = time.perf_counter()
-        for _ in range(a.cpu_frames):
-            O.render(g, f, nthreads=threads, want_rgba=False)
-        tc = (time.perf_counter() - tc0) / a.cpu_frames
-        cpu = {
-            "value": round(1.0 / tc, 4),
-            "unit": "frames/s",
-            "cores": threads,
-            "kind": "port",
-            "sample": f"{a.cpu_frames} full frames of the same {a.n}-Gaussian {W}x{H} workload through the "
-            f"CPU oracle Gaussian rasteriser (OpenMP, {threads} threads)",
-            "gaussians_per_sec": round(a.n / tc, 1),
-        }
-        # the reference's own CPU path is a point splatter (cpu_rasteriser.cpp:
-        # 9-92), restated in the oracle: reported beside, not comparable
-        xyz = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16)[:, 0:3]
-        O.point_splat(xyz, view, proj, W, H, TW, TW, nthreads=threads)
-        tp0 = time.perf_counter()
-        for _ in range(5):
-            O.point_splat(xyz, view, proj, W, H, TW, TW, nthreads=threads)
-        tp = (time.perf_counter() - tp0) / 5
-        cpu["reference_cpu_path"] = {
-            "value": round(1.0 / tp, 2),
-            "unit": "frames/s",
-            "kind": "port",
-            "sample": f"5 frames of the reference's CPU point splatter (projectPoints + splatPoints + "
-            f"buildTileHistogram) on the same {a.n} points, {threads} threads",
-        }
+        cpu = cpu_baseline(a, g, view, proj, W, H, TW, np)
 
     if rank == 0:
+        if a.config5:
+            metric = "frames/sec + Gaussians-splatted/sec at 4K, 8M-Gaussian clustered scene, orbit camera, 1/8 MI355X"
+            workload = (f"synthetic {a.n} Gaussians clustered around point_cloud_12 (sigma 0.02), {W}x{H}, "
+                        f"{TW}x{TW} tiles, orbit camera (120 views), fxy[1]={a.scale_div}")
+        else:
+            metric = HEADLINE_METRIC
+            workload = f"synthetic {a.n} Gaussians, {W}x{H}, {TW}x{TW} tiles, headless camera, fxy[1]={a.scale_div}"
+        if a.split > 1:
+            metric = f"frames/sec, {a.split} row bands emulated on one MI355X (group path, device-copy gather)"
+        if world > 1:
+            par = f"row-band x{world}: one process per GPU, work-balanced contiguous bands, one ncclAllGather/frame"
+        elif a.split > 1:
+            par = f"row-band x{a.split} emulated on one GPU (copy gather)"
+        elif a.gather:
+            par = "row-band group, world 1 (ncclAllGather over one rank)"
+        else:
+            par = "single GPU"
         out = {
-            "metric": "frames/sec + Gaussians-splatted/sec at 1080p, 1M-Gaussian scene, 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(fps, 3),
             "unit": "frames/s",
             "gaussians_per_sec": round(fps * a.n, 1),
-            "pairs_per_sec": round(fps * st["n_pairs"] * world, 1) if world == 1 else None,
+            "pairs_per_sec": round(fps * st["n_pairs"], 1),
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
@@ -400,31 +395,90 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded xoshiro256**, INRIA 3DGS layout, SH degree 3; parity semantics use DC only)",
+            "data": "synthetic (seeded xoshiro256**, INRIA 3DGS layout"
+                    + (", SH degree 3; parity semantics use DC only)" if a.sh_degree == 3 else ", SH degree 0)"),
             "config": {
-                "workload": (f"synthetic {a.n} Gaussians clustered around point_cloud_12 (sigma 0.02), {W}x{H}, "
-                             f"{TW}x{TW} tiles, orbit camera (120 views), fxy[1]={a.scale_div}" if a.config5 else
-                             f"synthetic {a.n} Gaussians, {W}x{H}, {TW}x{TW} tiles, headless camera, fxy[1]={a.scale_div}"),
+                "workload": workload,
                 "gaussians": a.n,
                 "resolution": [W, H],
                 "tile": [TW, TW],
                 "frames_in_flight": F,
-                "kernel_table": f"{a.profile_frames} frames, one in flight (stage HIP events)",
-                "parallelism": f"row-band x{world}" + ((" (work-balanced contiguous bands " + str(bands) + ")"
-                                                         if bands is not None else " (interleaved tile rows)")
-                                                        + " + RCCL all-gather" if world > 1 else ""),
+                "kernel_table": f"{a.profile_frames} blocking frames, one in flight (stage HIP events)",
+                "parallelism": par,
+                "bands": bands,
+                "pmc_key": pmc_key,
             },
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "n_pairs_binned", "max_list", "n_tiles",
                                          "n_big_tiles")},
+            "frame_check": frame_check,
             "kernels": kern,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if group:
+            out["gather_ms_per_frame"] = kern.get("gather", {}).get("avg_ms")
         print(json.dumps(out), flush=True)
     for r in R:
         r.close()
-    if dist_on:
+    if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_baseline(a, g, view, proj, W, H, TW, np):
+    """The oracle Gaussian rasteriser on the same frame (the apples-to-apples
+    CPU baseline, SURVEY §8 d) and the reference's own CPU point splatter
+    restated (cpu_rasteriser.cpp:9-92): OpenMP over the host's cores, pinned
+    close, median of --cpu-frames after --cpu-warmup frames, bounded by
+    --cpu-budget-s."""
+    from gaussian_splat_ipu_amd import camera
+    from oracle import oracle as O
+
+    n_cpus, phys = host_cpus()
+    omp_env = os.environ.get("OMP_NUM_THREADS")
+    # the GPU box sets OMP_NUM_THREADS to its CPU share (16 per GPU); the
+    # affinity mask of this (torch-initialised) thread can be narrower than
+    # the cores the OpenMP team actually gets, so it does not cap the count
+    threads = int(omp_env) if omp_env and omp_env.isdigit() else (phys or n_cpus)
+    threads = max(1, threads)
+    f = O.make_frame(view, proj, W, H, TW, TW, camera.FOV_DEFAULT, a.scale_div)
+
+    def timed(fn, frames, warm):
+        for _ in range(warm):
+            fn()
+        ts = []
+        tb = time.perf_counter()
+        for _ in range(frames):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+            if time.perf_counter() - tb > a.cpu_budget_s:
+                break
+        return float(np.median(ts)), len(ts)
+
+    tc, nf = timed(lambda: O.render(g, f, nthreads=threads, want_rgba=False), a.cpu_frames, a.cpu_warmup)
+    xyz = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16)[:, 0:3]
+    tp, npf = timed(lambda: O.point_splat(xyz, view, proj, W, H, TW, TW, nthreads=threads), a.cpu_frames,
+                    a.cpu_warmup)
+    host = (f"{os.cpu_count()} CPUs on the host, {n_cpus} in this thread's affinity mask, {phys} physical "
+            f"cores among those (lscpu); "
+            f"OMP_NUM_THREADS={omp_env} (the GPU box's CPU share), OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}")
+    return {
+        "value": round(1.0 / tc, 4),
+        "unit": "frames/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"median of {nf} full frames (after {a.cpu_warmup} warm-up) of the same {a.n}-Gaussian {W}x{H} "
+                  f"workload through the CPU oracle Gaussian rasteriser (OpenMP, {threads} threads)",
+        "host": host,
+        "gaussians_per_sec": round(a.n / tc, 1),
+        "reference_cpu_path": {
+            "value": round(1.0 / tp, 2),
+            "unit": "frames/s",
+            "kind": "port",
+            "sample": f"median of {npf} frames of the reference's CPU point splatter (projectPoints + "
+                      f"splatPoints + buildTileHistogram) on the same {a.n} points, {threads} threads",
+        },
+    }
 
 
 if __name__ == "__main__":

@@ -22,10 +22,13 @@ GS_FLAG_INPUT_ORDER = 8
 GS_FLAG_BAND_INTERLEAVED = 16
 GS_FLAG_BAND_CULL = 32
 GS_FLAG_NO_PAIR_CULL = 64
+GS_FLAG_NO_REBALANCE = 128
+GS_FLAG_GATHER_COPY = 256
+GS_MAX_GPUS = 16
 GS_LAYOUT_ROW_MAJOR = 0
 GS_LAYOUT_REF_TILE_MAJOR = 1
-GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_COUNT = range(6)
-KERNEL_NAMES = ("project", "scan", "emit", "sort", "blend")
+GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_GATHER, GS_K_COUNT = range(7)
+KERNEL_NAMES = ("project", "scan", "emit", "sort", "blend", "gather")
 
 _STATUS_NAMES = {
     GS_EINVAL: "GS_EINVAL",
@@ -78,7 +81,17 @@ class Config(C.Structure):
         ("band_row_begin", C.c_uint32),
         ("band_row_end", C.c_uint32),
         ("band_pad_rows", C.c_uint32),
+        # ABI 6: row-band group
+        ("num_gpus", C.c_uint32),
+        ("device_ids", C.c_int32 * 16),
+        ("frames_in_flight", C.c_uint32),
     ]
+
+
+class CommId(C.Structure):
+    """gs_comm_id: the 128 bytes of an ncclUniqueId."""
+
+    _fields_ = [("bytes", C.c_ubyte * 128)]
 
 
 class FrameStats(C.Structure):
@@ -130,6 +143,11 @@ _SIGS = {
     "gs_config_init": (C.c_int, [C.POINTER(Config)]),
     "gs_create": (C.c_int, [C.POINTER(Gaussian3D), C.c_size_t, C.POINTER(Config), C.POINTER(_P)]),
     "gs_destroy": (None, [_P]),
+    "gs_comm_id_create": (C.c_int, [C.POINTER(CommId)]),
+    "gs_create_rank": (C.c_int, [C.POINTER(Gaussian3D), C.c_size_t, C.POINTER(Config), C.POINTER(CommId),
+                                 C.c_int, C.c_int, C.POINTER(_P)]),
+    "gs_group_bands": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_size_t]),
+    "gs_balanced_bands": (C.c_int, [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
     "gs_set_view": (C.c_int, [_P, _FP]),
     "gs_set_projection": (C.c_int, [_P, _FP]),
     "gs_set_focal": (C.c_int, [_P, C.c_float, C.c_float]),
@@ -159,6 +177,9 @@ _SIGS = {
     "gs_synth_params_init": (C.c_int, [C.POINTER(SynthParams)]),
     "gs_ply_synthetic": (C.c_int, [C.POINTER(SynthParams), C.POINTER(_P)]),
     "gs_scene_prepare": (C.c_int, [_P, C.POINTER(Gaussian3D), C.c_size_t, _FP]),
+    "gs_cpu_point_splat": (C.c_int, [_FP, C.c_size_t, _FP, _FP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.c_uint8, C.POINTER(C.c_uint8), C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint32), C.c_int]),
     "gs_mat4_mul": (C.c_int, [_FP, _FP, _FP]),
     "gs_mat4_mul_vec4": (C.c_int, [_FP, _FP, _FP]),
     "gs_mat4_transpose": (C.c_int, [_FP, _FP]),

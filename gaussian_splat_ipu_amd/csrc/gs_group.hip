@@ -1,0 +1,847 @@
+// gs_group.hip -- the row-band group behind one C ABI handle (SURVEY §8 b/e):
+// the framebuffer's tile rows are split into contiguous bands, one per GPU;
+// every GPU renders its band (project -> bin -> sort -> blend, gs_kernels.hip)
+// and every frame ends with ONE all-gather of the BGR8 bands over RCCL.  This
+// replaces the reference's single-IPU execute (ipu_rasteriser.cpp:408-420,
+// splat.cpp:257-265), which has no multi-device path.
+//
+// Two ways to form a group:
+//   * gs_create with cfg->num_gpus = G: one process drives G devices
+//     (ncclCommInitAll; one ncclAllGather per device inside ncclGroupStart/End);
+//   * gs_create_rank: one process per GPU (ncclCommInitRank from an id rank 0
+//     made), as torchrun launches bench.py.
+//
+// Per frame, each rank's all-gather slot holds its padded BGR8 band followed
+// by a footer: the band's frame counters and reference tile-list lengths.
+// After the gather every rank holds every band's footer, so every rank derives
+// the same next split from the same numbers (no extra collective) and reports
+// the whole frame's histogram.  Overflow is decided from the footers too, so a
+// blocking gs_render re-renders on every rank or on none.
+//
+// Frames in flight: F band renderers per device take frames round-robin, each
+// on its own stream; the all-gathers run in frame order on one communication
+// stream per device.  Enqueueing frame k waits (host) for the footers of frame
+// k - F, which bounds the pipeline at F frames and feeds the re-balancing.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gsplat.h"
+#include "gs_internal.hpp"
+#include "gs_kernels.hpp"
+#include "host/gs_host.hpp"
+
+using gsh::set_error;
+
+namespace gsg {
+
+namespace {
+
+constexpr double kTileCost = 64.0;   // fixed work per tile of a row (dist.row_work)
+constexpr double kRebalanceGain = 0.97;  // switch splits only if the slowest band gains > 3 %
+constexpr int kMaxInFlight = 8;
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// RCCL is bound at run time, on first use: the librccl.so.1 already in the
+// process (e.g. the one torch loaded) if there is one, else $GSPLAT_RCCL, else
+// ROCm's.  Linking it would pull a second ROCm runtime stack into processes
+// that load torch's after libgsplat.
+struct Rccl {
+  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  std::string error;
+};
+
+const Rccl& rccl() {
+  static Rccl R;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h)
+      if (const char* p = std::getenv("GSPLAT_RCCL")) h = dlopen(p, RTLD_NOW);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    if (!h) {
+      const char* e = dlerror();
+      R.error = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+      return;
+    }
+    bool ok = true;
+    auto sym = [&](auto& f, const char* name) {
+      f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+      ok = ok && f != nullptr;
+    };
+    sym(R.GetUniqueId, "ncclGetUniqueId");
+    sym(R.CommInitRank, "ncclCommInitRank");
+    sym(R.CommInitAll, "ncclCommInitAll");
+    sym(R.CommDestroy, "ncclCommDestroy");
+    sym(R.AllGather, "ncclAllGather");
+    sym(R.GroupStart, "ncclGroupStart");
+    sym(R.GroupEnd, "ncclGroupEnd");
+    sym(R.GetErrorString, "ncclGetErrorString");
+    if (!ok) {
+      R.error = "librccl.so.1 lacks an RCCL entry point";
+      R.GetUniqueId = nullptr;
+    }
+  });
+  return R;
+}
+
+int rccl_check() {
+  if (rccl().GetUniqueId) return GS_OK;
+  set_error(rccl().error);
+  return GS_EDEVICE;
+}
+
+}  // namespace
+
+struct Member {
+  int device = 0;
+  int rank = 0;                       // the band this member renders
+  std::vector<gs_renderer*> slot;     // F band renderers (each its own stream)
+  hipStream_t comm_stream = nullptr;  // all-gathers, in frame order
+  ncclComm_t comm = nullptr;
+  uint8_t* d_send = nullptr;          // F x slot_cap: the band + footer of each in-flight frame
+  uint8_t* d_recv = nullptr;          // F x world x slot_cap: the gathered frames
+  std::vector<hipEvent_t> ev_render;    // per slot: the band is rendered
+  std::vector<hipEvent_t> ev_gathered;  // per slot: the all-gather read the send slot
+};
+
+struct SlotInfo {
+  bool used = false;
+  bool footers_read = false;
+  bool gather_timed = false;
+  uint64_t frame = 0;
+  std::vector<uint32_t> bounds;  // world + 1 tile-row bounds of the frame
+  int pad_rows = 0;
+  size_t bgr_part = 0;  // bytes of the padded BGR8 band (256-aligned)
+  size_t bytes = 0;     // bytes per rank of the all-gather
+};
+
+struct Group {
+  gs_config cfg{};
+  int world = 1, F = 1;
+  bool rccl = true;
+  bool multi_process = false;
+  bool rebalance = true;
+  bool profile = false;
+  int W = 0, H = 0, tw = 0, th = 0, tiles_x = 0, tiles_y = 0, T = 0;
+  size_t n = 0;
+  size_t slot_cap = 0;     // bytes per rank per slot (the full frame's band + footer)
+  size_t foot_words = 0;   // 16 + T
+  std::vector<Member> mem;
+  std::vector<uint32_t> bounds;  // split of the next frame
+  std::vector<SlotInfo> sinfo;
+  uint32_t* h_foot = nullptr;    // pinned: F x world x foot_words
+  std::vector<hipEvent_t> ev_foot, ev_g0, ev_g1;  // on mem[0].comm_stream
+  uint64_t frame = 0;
+  int last_slot = -1;
+  uint64_t newest_read = 0;
+  bool have_read = false;
+  bool overflow_seen = false;
+  float view[16], proj[16];
+  float fov = 0.6981317f, sd = 0.1f;
+  // the last frame whose footers were read
+  std::mutex hist_mu;
+  std::vector<uint32_t> hist;
+  gs_frame_stats stats{};
+  // gather timing (GS_FLAG_PROFILE)
+  uint32_t profile_every = 1;
+  double g_ms = 0.0;
+  uint64_t g_n = 0;
+  uint64_t rebalances = 0;
+};
+
+void balanced_bands(const double* work, int rows, int world, uint32_t* bounds) {
+  std::vector<double> c((size_t)rows + 1, 0.0);
+  for (int i = 0; i < rows; ++i) c[i + 1] = c[i] + work[i];
+  bounds[0] = 0;
+  for (int k = 1; k < world; ++k) {
+    const double target = c[rows] * k / world;
+    int b = (int)(std::lower_bound(c.begin(), c.end(), target) - c.begin());
+    if (b > 0 && std::fabs(c[b - 1] - target) <= std::fabs(c[std::min(b, rows)] - target)) b -= 1;
+    b = std::max((int)bounds[k - 1] + 1, std::min(b, rows - (world - k)));
+    bounds[k] = (uint32_t)b;
+  }
+  bounds[world] = (uint32_t)rows;
+}
+
+namespace {
+
+double max_band_work(const std::vector<double>& w, const std::vector<uint32_t>& b) {
+  double mx = 0.0;
+  for (size_t r = 0; r + 1 < b.size(); ++r) {
+    double s = 0.0;
+    for (uint32_t y = b[r]; y < b[r + 1]; ++y) s += w[y];
+    mx = std::max(mx, s);
+  }
+  return mx;
+}
+
+int set_dev(int d) {
+  hipError_t e = hipSetDevice(d);
+  return e == hipSuccess ? GS_OK : gsr::hip_fail(e, "hipSetDevice");
+}
+
+int nccl_fail(ncclResult_t r, const char* what) {
+  set_error(std::string(what) + ": " + rccl().GetErrorString(r));
+  return GS_EDEVICE;
+}
+
+#define GS_NCCL(call)                                   \
+  do {                                                  \
+    ncclResult_t r_ = (call);                           \
+    if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
+  } while (0)
+
+// Footers of the frame in slot i (its all-gather is complete once ev_foot[i]
+// fired): overflow, the whole frame's histogram and stats, and -- for the
+// newest frame read -- the next split.
+int read_footers(Group* g, int i) {
+  SlotInfo& si = g->sinfo[i];
+  if (!si.used || si.footers_read) return GS_OK;
+  int rc = set_dev(g->mem[0].device);
+  if (rc != GS_OK) return rc;
+  GS_HIP(hipEventSynchronize(g->ev_foot[i]));
+  si.footers_read = true;
+  if (si.gather_timed) {
+    float ms = 0.0f;
+    GS_HIP(hipEventElapsedTime(&ms, g->ev_g0[i], g->ev_g1[i]));
+    g->g_ms += ms;
+    g->g_n += 1;
+    si.gather_timed = false;
+  }
+  const bool chunked = !g->mem[0].slot[0]->bin_global && g->mem[0].slot[0]->n_chunks > 0;
+  bool ovf = false;
+  uint64_t P = 0, Pb = 0, V = 0, nbig = 0;
+  std::vector<uint32_t> hist((size_t)g->T, 0u);
+  for (int r = 0; r < g->world; ++r) {
+    const uint32_t* f = g->h_foot + ((size_t)i * g->world + r) * g->foot_words;
+    ovf = ovf || f[3] != 0;
+    const uint64_t pb = (uint64_t)f[5] | ((uint64_t)f[6] << 32);
+    Pb += pb;
+    P += chunked ? ((uint64_t)f[10] | ((uint64_t)f[11] << 32)) : pb;
+    V = std::max<uint64_t>(V, f[2]);
+    nbig += f[0];
+    const size_t t0 = (size_t)si.bounds[r] * g->tiles_x, t1 = (size_t)si.bounds[r + 1] * g->tiles_x;
+    std::memcpy(hist.data() + t0, f + 16, (t1 - t0) * 4);
+  }
+  if (ovf) g->overflow_seen = true;
+  if (g->have_read && si.frame < g->newest_read) return GS_OK;
+  g->have_read = true;
+  g->newest_read = si.frame;
+  uint32_t mx = 0;
+  for (uint32_t v : hist) mx = std::max(mx, v);
+  {
+    std::lock_guard<std::mutex> lk(g->hist_mu);
+    g->hist.swap(hist);
+    g->stats.n_rendered = V;
+    g->stats.n_pairs = P;
+    g->stats.n_pairs_binned = Pb;
+    g->stats.max_list = mx;
+    g->stats.n_big_tiles = (uint32_t)nbig;
+  }
+  if (g->rebalance && g->world > 1 && !ovf) {
+    std::vector<double> w((size_t)g->tiles_y, 0.0);
+    {
+      std::lock_guard<std::mutex> lk(g->hist_mu);
+      for (int y = 0; y < g->tiles_y; ++y) {
+        double s = 0.0;
+        for (int x = 0; x < g->tiles_x; ++x) s += g->hist[(size_t)y * g->tiles_x + x];
+        w[y] = s + kTileCost * g->tiles_x;
+      }
+    }
+    std::vector<uint32_t> nb((size_t)g->world + 1);
+    balanced_bands(w.data(), g->tiles_y, g->world, nb.data());
+    if (nb != g->bounds && max_band_work(w, nb) < kRebalanceGain * max_band_work(w, g->bounds)) {
+      g->bounds = nb;
+      g->rebalances += 1;
+    }
+  }
+  return GS_OK;
+}
+
+int enqueue(Group* g) {
+  const int i = (int)(g->frame % (uint64_t)g->F);
+  SlotInfo& si = g->sinfo[i];
+  int rc = read_footers(g, i);  // frame k - F: bounds the pipeline, feeds the split
+  if (rc != GS_OK) return rc;
+  int pad = 0;
+  for (int r = 0; r < g->world; ++r) pad = std::max(pad, (int)(g->bounds[r + 1] - g->bounds[r]));
+  const size_t bgr_part = align256((size_t)pad * g->th * g->W * 3);
+  const size_t bytes = align256(bgr_part + (16 + (size_t)pad * g->tiles_x) * 4);
+  const bool was_used = si.used;
+  for (Member& m : g->mem) {
+    if ((rc = set_dev(m.device)) != GS_OK) return rc;
+    gs_renderer* c = m.slot[i];
+    if ((rc = gsr::set_band_rows(c, (int)g->bounds[m.rank], (int)g->bounds[m.rank + 1], pad)) != GS_OK) return rc;
+    std::memcpy(c->view_rm, g->view, sizeof(g->view));
+    std::memcpy(c->proj_rm, g->proj, sizeof(g->proj));
+    c->fov = g->fov;
+    c->scale_div = g->sd;
+    c->bgr_target = m.d_send + (size_t)i * g->slot_cap;
+    c->buf.footer = (uint32_t*)(c->bgr_target + bgr_part);
+    // the gather of frame k - F read this send slot
+    if (was_used) GS_HIP(hipStreamWaitEvent(c->stream, m.ev_gathered[i], 0));
+    if ((rc = gsr::enqueue_frame(c)) != GS_OK) return rc;
+    GS_HIP(hipEventRecord(m.ev_render[i], c->stream));
+  }
+  for (Member& m : g->mem) {
+    if ((rc = set_dev(m.device)) != GS_OK) return rc;
+    if (g->rccl) {
+      GS_HIP(hipStreamWaitEvent(m.comm_stream, m.ev_render[i], 0));
+    } else {  // copies read every member's band
+      for (Member& o : g->mem) GS_HIP(hipStreamWaitEvent(m.comm_stream, o.ev_render[i], 0));
+    }
+  }
+  const bool timed = g->profile && g->frame % g->profile_every == 0;
+  if (timed) {
+    if ((rc = set_dev(g->mem[0].device)) != GS_OK) return rc;
+    GS_HIP(hipEventRecord(g->ev_g0[i], g->mem[0].comm_stream));
+  }
+  if (g->rccl) {
+    const bool grouped = g->mem.size() > 1;
+    if (grouped) GS_NCCL(rccl().GroupStart());
+    for (Member& m : g->mem) {
+      if (!grouped && (rc = set_dev(m.device)) != GS_OK) return rc;
+      GS_NCCL(rccl().AllGather(m.d_send + (size_t)i * g->slot_cap, m.d_recv + (size_t)i * g->world * g->slot_cap,
+                            bytes, ncclUint8, m.comm, m.comm_stream));
+    }
+    if (grouped) GS_NCCL(rccl().GroupEnd());
+  } else {
+    for (Member& m : g->mem) {
+      if ((rc = set_dev(m.device)) != GS_OK) return rc;
+      uint8_t* recv = m.d_recv + (size_t)i * g->world * g->slot_cap;
+      for (const Member& o : g->mem)
+        GS_HIP(hipMemcpyAsync(recv + (size_t)o.rank * bytes, o.d_send + (size_t)i * g->slot_cap, bytes,
+                              hipMemcpyDeviceToDevice, m.comm_stream));
+    }
+  }
+  for (Member& m : g->mem) {
+    if ((rc = set_dev(m.device)) != GS_OK) return rc;
+    GS_HIP(hipEventRecord(m.ev_gathered[i], m.comm_stream));
+  }
+  // every band's footer to the host (one strided copy), for frame k + F
+  Member& m0 = g->mem[0];
+  if ((rc = set_dev(m0.device)) != GS_OK) return rc;
+  if (timed) GS_HIP(hipEventRecord(g->ev_g1[i], m0.comm_stream));
+  GS_HIP(hipMemcpy2DAsync(g->h_foot + (size_t)i * g->world * g->foot_words, g->foot_words * 4,
+                          m0.d_recv + (size_t)i * g->world * g->slot_cap + bgr_part, bytes,
+                          (16 + (size_t)pad * g->tiles_x) * 4, (size_t)g->world, hipMemcpyDeviceToHost,
+                          m0.comm_stream));
+  GS_HIP(hipEventRecord(g->ev_foot[i], m0.comm_stream));
+  si.used = true;
+  si.footers_read = false;
+  si.gather_timed = timed;
+  si.frame = g->frame;
+  si.bounds = g->bounds;
+  si.pad_rows = pad;
+  si.bgr_part = bgr_part;
+  si.bytes = bytes;
+  g->last_slot = i;
+  g->frame += 1;
+  return GS_OK;
+}
+
+int ensure_capacity(Group* g) {
+  // after an overflow: every local band renderer gets room for the largest
+  // band list any of them binned (the next frames may move the bands)
+  uint64_t need = 0;
+  for (Member& m : g->mem)
+    for (gs_renderer* c : m.slot) need = std::max(need, c->stats.n_pairs_binned);
+  need = std::min<uint64_t>(need + need / 4 + 1024, 0xFFFFFFF0ull);
+  for (Member& m : g->mem) {
+    int rc = set_dev(m.device);
+    if (rc != GS_OK) return rc;
+    for (gs_renderer* c : m.slot) {
+      if (c->pair_cap >= need) continue;
+      GS_HIP(hipStreamSynchronize(c->stream));
+      if ((rc = gsr::alloc_pairs(c, std::min<uint64_t>(std::max<uint64_t>(need, 2 * c->pair_cap), 0xFFFFFFF0ull))) !=
+          GS_OK)
+        return rc;
+    }
+  }
+  return GS_OK;
+}
+
+void release(Group* g) {
+  for (Member& m : g->mem) {
+    (void)hipSetDevice(m.device);
+    if (m.comm_stream) (void)hipStreamSynchronize(m.comm_stream);
+    for (gs_renderer* c : m.slot) gsr::destroy(c);
+    m.slot.clear();
+    if (m.comm) (void)rccl().CommDestroy(m.comm);
+    if (m.d_send) (void)hipFree(m.d_send);
+    if (m.d_recv) (void)hipFree(m.d_recv);
+    for (hipEvent_t e : m.ev_render)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : m.ev_gathered)
+      if (e) (void)hipEventDestroy(e);
+    if (m.comm_stream) (void)hipStreamDestroy(m.comm_stream);
+  }
+  if (!g->mem.empty()) (void)hipSetDevice(g->mem[0].device);
+  for (auto* v : {&g->ev_foot, &g->ev_g0, &g->ev_g1})
+    for (hipEvent_t e : *v)
+      if (e) (void)hipEventDestroy(e);
+  if (g->h_foot) (void)hipHostFree(g->h_foot);
+  g->mem.clear();
+}
+
+}  // namespace
+
+int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_comm_id* id, int rank,
+           int world, gs_renderer** out) {
+  if (!out || !cfg || (n > 0 && !gs)) {
+    set_error("gs_create: null argument");
+    return GS_EINVAL;
+  }
+  *out = nullptr;
+  const bool mp = id != nullptr;
+  const int G = mp ? world : (int)cfg->num_gpus;
+  if (G < 1 || (!mp && G > GS_MAX_GPUS) || (mp && (rank < 0 || rank >= world)) || cfg->tile_height == 0 ||
+      cfg->tile_width == 0 || cfg->width == 0 || cfg->height == 0) {
+    set_error("gs_create: invalid row-band group (num_gpus / rank / world)");
+    return GS_EINVAL;
+  }
+  const int tiles_y = (int)((cfg->height + cfg->tile_height - 1) / cfg->tile_height);
+  if (tiles_y < G) {
+    set_error("gs_create: fewer tile rows than bands");
+    return GS_EINVAL;
+  }
+  Group* g = new Group();
+  auto fail = [&](int rc) {
+    release(g);
+    delete g;
+    return rc;
+  };
+  g->cfg = *cfg;
+  g->n = n;
+  g->world = G;
+  g->multi_process = mp;
+  g->F = std::max(1, std::min(kMaxInFlight, (int)cfg->frames_in_flight));
+  g->rebalance = (cfg->flags & GS_FLAG_NO_REBALANCE) == 0;
+  g->profile = (cfg->flags & GS_FLAG_PROFILE) != 0;
+  g->W = (int)cfg->width;
+  g->H = (int)cfg->height;
+  g->tw = (int)cfg->tile_width;
+  g->th = (int)cfg->tile_height;
+  g->tiles_x = (int)((cfg->width + cfg->tile_width - 1) / cfg->tile_width);
+  g->tiles_y = tiles_y;
+  g->T = g->tiles_x * g->tiles_y;
+  g->foot_words = 16 + (size_t)g->T;
+  g->slot_cap = align256(align256((size_t)g->tiles_y * g->th * g->W * 3) + g->foot_words * 4);
+  for (int i = 0; i < 16; ++i) g->view[i] = g->proj[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+
+  // members: the bands this process renders
+  std::vector<int> devs;
+  if (mp) {
+    int dev = cfg->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return fail(gsr::hip_fail(hipGetDevice(&dev), "hipGetDevice"));
+    devs.push_back(dev);
+  } else {
+    for (int k = 0; k < G; ++k) devs.push_back(cfg->device_ids[k]);
+  }
+  bool dup = false;
+  for (size_t a = 0; a < devs.size(); ++a)
+    for (size_t b = a + 1; b < devs.size(); ++b) dup = dup || devs[a] == devs[b];
+  g->rccl = mp || !(dup || (cfg->flags & GS_FLAG_GATHER_COPY));
+  if (mp && (cfg->flags & GS_FLAG_GATHER_COPY)) {
+    set_error("gs_create_rank: the copy gather needs every band in one process");
+    return fail(GS_EINVAL);
+  }
+  g->mem.resize(devs.size());
+  for (size_t k = 0; k < devs.size(); ++k) {
+    g->mem[k].device = devs[k];
+    g->mem[k].rank = mp ? rank : (int)k;
+  }
+
+  // the initial split: equal work per tile (nearly equal rows); later frames
+  // re-balance from the gathered histograms
+  g->bounds.assign((size_t)G + 1, 0u);
+  {
+    std::vector<double> ones((size_t)tiles_y, 1.0);
+    balanced_bands(ones.data(), tiles_y, G, g->bounds.data());
+  }
+  g->sinfo.assign((size_t)g->F, SlotInfo{});
+
+  // band renderers: sized for the whole frame (any split fits), band cull on
+  gs_config cc = *cfg;
+  cc.num_gpus = 0;
+  cc.frames_in_flight = 0;
+  cc.band_index = 0;
+  cc.band_count = 1;
+  cc.band_row_begin = 0;
+  cc.band_row_end = (uint32_t)tiles_y;
+  cc.band_pad_rows = (uint32_t)tiles_y;
+  cc.flags = (cfg->flags | GS_FLAG_BAND_CULL) & ~(GS_FLAG_BAND_INTERLEAVED | GS_FLAG_NO_REBALANCE |
+                                                   GS_FLAG_GATHER_COPY | GS_FLAG_PROFILE);
+  int rc = GS_OK;
+  for (size_t k = 0; k < g->mem.size(); ++k) {
+    Member& m = g->mem[k];
+    cc.device = m.device;
+    const gs_renderer* share = nullptr;  // one scene copy per device
+    for (size_t j = 0; j <= k && !share; ++j)
+      if (g->mem[j].device == m.device && !g->mem[j].slot.empty()) share = g->mem[j].slot[0];
+    for (int s = 0; s < g->F; ++s) {
+      gs_config c2 = cc;
+      if (k == 0 && s == 0 && g->profile) c2.flags |= GS_FLAG_PROFILE;
+      gs_renderer* c = nullptr;
+      if ((rc = gsr::create(gs, n, &c2, share, &c)) != GS_OK) return fail(rc);
+      m.slot.push_back(c);
+      if (!share) share = c;
+    }
+    if ((rc = set_dev(m.device)) != GS_OK) return fail(rc);
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&m.comm_stream, hipStreamNonBlocking)) != hipSuccess)
+      return fail(gsr::hip_fail(e, "hipStreamCreate(comm)"));
+    if ((e = hipMalloc(&m.d_send, (size_t)g->F * g->slot_cap)) != hipSuccess)
+      return fail(gsr::hip_fail(e, "hipMalloc(all-gather send)"));
+    if ((e = hipMalloc(&m.d_recv, (size_t)g->F * g->world * g->slot_cap)) != hipSuccess)
+      return fail(gsr::hip_fail(e, "hipMalloc(all-gather recv)"));
+    if ((e = hipMemset(m.d_recv, 0, (size_t)g->F * g->world * g->slot_cap)) != hipSuccess)
+      return fail(gsr::hip_fail(e, "hipMemset(all-gather recv)"));
+    m.ev_render.assign((size_t)g->F, nullptr);
+    m.ev_gathered.assign((size_t)g->F, nullptr);
+    for (int s = 0; s < g->F; ++s) {
+      if ((e = hipEventCreateWithFlags(&m.ev_render[s], hipEventDisableTiming)) != hipSuccess ||
+          (e = hipEventCreateWithFlags(&m.ev_gathered[s], hipEventDisableTiming)) != hipSuccess)
+        return fail(gsr::hip_fail(e, "hipEventCreate"));
+    }
+  }
+  if ((rc = set_dev(g->mem[0].device)) != GS_OK) return fail(rc);
+  {
+    hipError_t e;
+    g->ev_foot.assign((size_t)g->F, nullptr);
+    g->ev_g0.assign((size_t)g->F, nullptr);
+    g->ev_g1.assign((size_t)g->F, nullptr);
+    for (int s = 0; s < g->F; ++s) {
+      if ((e = hipEventCreateWithFlags(&g->ev_foot[s], hipEventDisableTiming)) != hipSuccess ||
+          (e = hipEventCreate(&g->ev_g0[s])) != hipSuccess || (e = hipEventCreate(&g->ev_g1[s])) != hipSuccess)
+        return fail(gsr::hip_fail(e, "hipEventCreate"));
+    }
+    if ((e = hipHostMalloc((void**)&g->h_foot, (size_t)g->F * g->world * g->foot_words * 4,
+                           hipHostMallocDefault)) != hipSuccess)
+      return fail(gsr::hip_fail(e, "hipHostMalloc(footers)"));
+    std::memset(g->h_foot, 0, (size_t)g->F * g->world * g->foot_words * 4);
+  }
+
+  // communicators
+  if (g->rccl) {
+    if ((rc = rccl_check()) != GS_OK) return fail(rc);
+    if (mp) {
+      ncclUniqueId uid;
+      static_assert(sizeof(uid) == sizeof(id->bytes), "ncclUniqueId is 128 bytes");
+      std::memcpy(&uid, id->bytes, sizeof(uid));
+      if ((rc = set_dev(g->mem[0].device)) != GS_OK) return fail(rc);
+      ncclResult_t nr = rccl().CommInitRank(&g->mem[0].comm, world, uid, rank);
+      if (nr != ncclSuccess) return fail(nccl_fail(nr, "ncclCommInitRank"));
+    } else {
+      std::vector<ncclComm_t> comms(devs.size());
+      ncclResult_t nr = rccl().CommInitAll(comms.data(), (int)devs.size(), devs.data());
+      if (nr != ncclSuccess) return fail(nccl_fail(nr, "ncclCommInitAll"));
+      for (size_t k = 0; k < devs.size(); ++k) g->mem[k].comm = comms[k];
+    }
+  }
+
+  {
+    gs_renderer* c0 = g->mem[0].slot[0];
+    g->stats.n_gaussians = n;
+    g->stats.n_tiles = (uint32_t)g->T;
+    g->stats.tiles_x = (uint32_t)g->tiles_x;
+    g->stats.tiles_y = (uint32_t)g->tiles_y;
+    g->stats.band_y0 = 0;
+    g->stats.band_rows = (uint32_t)g->H;
+    g->stats.band_stride = 1;
+    g->stats.bin_global = (uint32_t)c0->bin_global;
+    g->hist.assign((size_t)g->T, 0u);
+  }
+  gs_renderer* h = new gs_renderer();
+  h->cfg = *cfg;
+  h->n = n;
+  h->device = g->mem[0].device;
+  h->grp = g;
+  *out = h;
+  return GS_OK;
+}
+
+void destroy(Group* g) {
+  if (!g) return;
+  release(g);
+  delete g;
+}
+
+int set_view(Group* g, const float* rm) {
+  std::memcpy(g->view, rm, sizeof(g->view));
+  return GS_OK;
+}
+
+int set_projection(Group* g, const float* rm) {
+  std::memcpy(g->proj, rm, sizeof(g->proj));
+  return GS_OK;
+}
+
+int set_focal(Group* g, float fov, float sd) {
+  g->fov = fov;
+  g->sd = sd;
+  return GS_OK;
+}
+
+int render_async(Group* g) { return enqueue(g); }
+
+int sync(Group* g) {
+  int rc = GS_OK;
+  for (Member& m : g->mem) {
+    if ((rc = set_dev(m.device)) != GS_OK) return rc;
+    GS_HIP(hipStreamSynchronize(m.comm_stream));
+    for (gs_renderer* c : m.slot) {
+      rc = gsr::finish_frame(c);  // (overflow is decided from the gathered footers)
+      if (rc != GS_OK && rc != GS_EOVERFLOW) return rc;
+    }
+  }
+  // the remaining frames' footers, oldest first
+  std::vector<int> order;
+  for (int i = 0; i < g->F; ++i)
+    if (g->sinfo[i].used && !g->sinfo[i].footers_read) order.push_back(i);
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return g->sinfo[a].frame < g->sinfo[b].frame; });
+  for (int i : order)
+    if ((rc = read_footers(g, i)) != GS_OK) return rc;
+  if (g->overflow_seen) {
+    g->overflow_seen = false;
+    set_error("pair list overflow: a band of a frame since the last sync binned more pairs than its capacity");
+    return GS_EOVERFLOW;
+  }
+  return GS_OK;
+}
+
+int render(Group* g) {
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    int rc = enqueue(g);
+    if (rc != GS_OK) return rc;
+    rc = sync(g);
+    if (rc != GS_EOVERFLOW) return rc;
+    // every rank saw the same footers: all of them render the frame again
+    if ((rc = ensure_capacity(g)) != GS_OK) return rc;
+  }
+  set_error("gs_render: capacity growth did not converge");
+  return GS_EOVERFLOW;
+}
+
+int get_stream(Group* g, void** s) {
+  *s = (void*)g->mem[0].comm_stream;
+  return GS_OK;
+}
+
+int read_bgr8(Group* g, uint8_t* dst, size_t bytes) {
+  const size_t need = (size_t)g->H * g->W * 3;
+  if (bytes < need) {
+    set_error("gs_read_bgr8: destination too small");
+    return GS_EINVAL;
+  }
+  int rc = sync(g);
+  if (rc != GS_OK) return rc;
+  if (g->last_slot < 0) {
+    set_error("gs_read_bgr8: no frame rendered yet");
+    return GS_EINVAL;
+  }
+  const SlotInfo& si = g->sinfo[g->last_slot];
+  const Member& m0 = g->mem[0];
+  if ((rc = set_dev(m0.device)) != GS_OK) return rc;
+  const uint8_t* recv = m0.d_recv + (size_t)g->last_slot * g->world * g->slot_cap;
+  for (int r = 0; r < g->world; ++r) {  // drop each band's padding
+    const int y0 = (int)si.bounds[r] * g->th, y1 = std::min(g->H, (int)si.bounds[r + 1] * g->th);
+    if (y1 > y0)
+      GS_HIP(hipMemcpy(dst + (size_t)y0 * g->W * 3, recv + (size_t)r * si.bytes, (size_t)(y1 - y0) * g->W * 3,
+                       hipMemcpyDeviceToHost));
+  }
+  return GS_OK;
+}
+
+int read_rgba32f(Group* g, float* dst, size_t n_floats, int layout) {
+  if (g->multi_process && g->world > 1) {
+    set_error("gs_read_rgba32f: a rank of a multi-process group holds only its band's RGBA f32 "
+              "(the all-gather moves BGR8)");
+    return GS_EINVAL;
+  }
+  if (layout != GS_LAYOUT_ROW_MAJOR && layout != GS_LAYOUT_REF_TILE_MAJOR) return GS_EINVAL;
+  const size_t W = (size_t)g->W, H = (size_t)g->H;
+  const size_t need = layout == GS_LAYOUT_ROW_MAJOR ? H * W * 4 : (size_t)g->T * g->tw * g->th * 4;
+  if (n_floats < need) {
+    set_error("gs_read_rgba32f: destination too small");
+    return GS_EINVAL;
+  }
+  int rc = sync(g);
+  if (rc != GS_OK) return rc;
+  if (g->last_slot < 0) {
+    set_error("gs_read_rgba32f: no frame rendered yet");
+    return GS_EINVAL;
+  }
+  std::vector<float> tmp;
+  float* rm = dst;
+  if (layout != GS_LAYOUT_ROW_MAJOR) {
+    tmp.resize(H * W * 4);
+    rm = tmp.data();
+  }
+  for (Member& m : g->mem) {
+    gs_renderer* c = m.slot[g->last_slot];
+    if ((rc = gsr::read_rgba32f(c, rm + (size_t)c->band_py0 * W * 4, (size_t)c->band_rows * W * 4,
+                                GS_LAYOUT_ROW_MAJOR)) != GS_OK)
+      return rc;
+  }
+  if (layout != GS_LAYOUT_ROW_MAJOR) gsr::retile(rm, H, W, g->tw, g->th, g->tiles_x, g->T, dst);
+  return GS_OK;
+}
+
+int read_tile_histogram(Group* g, uint32_t* dst, size_t n) {
+  std::lock_guard<std::mutex> lk(g->hist_mu);
+  if (n < g->hist.size()) {
+    set_error("gs_read_tile_histogram: destination too small");
+    return GS_EINVAL;
+  }
+  std::copy(g->hist.begin(), g->hist.end(), dst);
+  return GS_OK;
+}
+
+int get_stats(Group* g, gs_frame_stats* st) {
+  std::lock_guard<std::mutex> lk(g->hist_mu);
+  *st = g->stats;
+  uint64_t cap = ~0ull;
+  for (Member& m : g->mem)
+    for (gs_renderer* c : m.slot) cap = std::min<uint64_t>(cap, c->pair_cap);
+  st->pair_capacity = cap;
+  return GS_OK;
+}
+
+int read_bins(Group* g, uint64_t* tile_start, size_t n_start, uint32_t* list, size_t n_list) {
+  if (g->multi_process && g->world > 1) {
+    set_error("gs_read_bins: a rank of a multi-process group holds only its band's lists");
+    return GS_EINVAL;
+  }
+  int rc = sync(g);
+  if (rc != GS_OK) return rc;
+  if (g->last_slot < 0) {
+    set_error("gs_read_bins: no frame rendered yet");
+    return GS_EINVAL;
+  }
+  if (n_start < (size_t)g->T + 1) {
+    set_error("gs_read_bins: destination too small");
+    return GS_EINVAL;
+  }
+  uint64_t off = 0;
+  size_t t_base = 0;
+  for (Member& m : g->mem) {  // ranks in band order
+    gs_renderer* c = m.slot[g->last_slot];
+    const size_t nt = (size_t)c->n_tiles;
+    if (n_list < off + c->stats.n_pairs) {
+      set_error("gs_read_bins: destination too small");
+      return GS_EINVAL;
+    }
+    std::vector<uint64_t> ts(nt + 1);
+    if ((rc = gsr::read_bins(c, ts.data(), nt + 1, list + off, n_list - off)) != GS_OK) return rc;
+    for (size_t j = 0; j < nt; ++j) tile_start[t_base + j] = off + ts[j];
+    t_base += nt;
+    off += ts[nt];
+  }
+  tile_start[t_base] = off;
+  return GS_OK;
+}
+
+int read_projected(Group* g, float* dst, size_t n_floats) {
+  int rc = sync(g);
+  if (rc != GS_OK) return rc;
+  if (g->last_slot < 0) {
+    set_error("gs_read_projected: no frame rendered yet");
+    return GS_EINVAL;
+  }
+  if ((rc = set_dev(g->mem[0].device)) != GS_OK) return rc;
+  return gsr::read_projected(g->mem[0].slot[g->last_slot], dst, n_floats);
+}
+
+int kernel_times(Group* g, double* avg_ms, uint64_t* launches, int n) {
+  if (!g->profile) {
+    set_error("gs_kernel_times: group created without GS_FLAG_PROFILE");
+    return GS_EINVAL;
+  }
+  gs_renderer* c = g->mem[0].slot[0];
+  int rc = set_dev(c->device);
+  if (rc != GS_OK) return rc;
+  for (auto& s : c->ring)
+    if ((rc = gsr::profile_harvest(c, s)) != GS_OK) return rc;
+  for (int k = 0; k < n && k < GS_K_COUNT; ++k) {
+    if (k == GS_K_GATHER) {
+      avg_ms[k] = g->g_n ? g->g_ms / (double)g->g_n : 0.0;
+      if (launches) launches[k] = g->g_n;
+    } else {
+      avg_ms[k] = c->k_launches[k] ? c->k_ms[k] / (double)c->k_launches[k] : 0.0;
+      if (launches) launches[k] = c->k_launches[k];
+    }
+  }
+  return GS_OK;
+}
+
+int reset_kernel_times(Group* g) {
+  int rc = sync(g);
+  if (rc != GS_OK && rc != GS_EOVERFLOW) return rc;
+  gs_renderer* c = g->mem[0].slot[0];
+  if (c->profile) {
+    if ((rc = set_dev(c->device)) != GS_OK) return rc;
+    for (auto& s : c->ring)
+      if ((rc = gsr::profile_harvest(c, s)) != GS_OK) return rc;
+    for (int k = 0; k < GS_K_COUNT; ++k) {
+      c->k_ms[k] = 0.0;
+      c->k_launches[k] = 0;
+    }
+  }
+  g->g_ms = 0.0;
+  g->g_n = 0;
+  return GS_OK;
+}
+
+int set_profile_interval(Group* g, uint32_t every) {
+  g->profile_every = every;
+  for (Member& m : g->mem)
+    for (gs_renderer* c : m.slot) {
+      c->profile_every = every;
+      c->frame_seq = 0;
+    }
+  return GS_OK;
+}
+
+int bands(Group* g, uint32_t* bounds, size_t n) {
+  const std::vector<uint32_t>& b = g->last_slot >= 0 ? g->sinfo[g->last_slot].bounds : g->bounds;
+  if (n < b.size()) {
+    set_error("gs_group_bands: destination too small");
+    return GS_EINVAL;
+  }
+  std::copy(b.begin(), b.end(), bounds);
+  return GS_OK;
+}
+
+}  // namespace gsg
+
+extern "C" int gs_comm_id_create(gs_comm_id* out) {
+  if (!out) return GS_EINVAL;
+  int rc = gsg::rccl_check();
+  if (rc != GS_OK) return rc;
+  ncclUniqueId uid;
+  ncclResult_t r = gsg::rccl().GetUniqueId(&uid);
+  if (r != ncclSuccess) {
+    set_error(std::string("ncclGetUniqueId: ") + gsg::rccl().GetErrorString(r));
+    return GS_EDEVICE;
+  }
+  std::memcpy(out->bytes, &uid, sizeof(out->bytes));
+  return GS_OK;
+}

@@ -770,6 +770,7 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
     uint32_t href = 0;  // the reference list length: the histogram, straight to host memory
     for (int w = 0; w < 16; ++w) href += whsum[w][lane];
     if (ok) b.host_counters[16 + t] = href;
+    if (ok && b.footer) b.footer[16 + t] = href;
     unsigned long long rsum = ok ? href : 0u;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) rsum += __shfl_xor(rsum, d, 64);
@@ -907,6 +908,8 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
       for (int k = 12; k < 16; ++k) b.counters[k] = 0;
       b.tile_start[T] = (uint32_t)(ts < 0xFFFFFFFFull ? ts : 0xFFFFFFFFull);
       for (int k = 0; k < 16; ++k) b.host_counters[k] = b.counters[k];
+      if (b.footer)
+        for (int k = 0; k < 16; ++k) b.footer[k] = b.counters[k];
     }
   }
 }

@@ -100,6 +100,9 @@ struct Buffers {
   // outputs
   float4* rgba;             // band_rows x width, row-major
   uint8_t* bgr;             // band rows (padded) x width x 3
+  uint32_t* footer;         // row-band group: counters[16] + reference list lengths[n_tiles]
+                            //   of this frame, next to its BGR8 band in the all-gather slot
+                            //   (written by the chunked scan; nullptr = none)
 };
 
 constexpr int GS_STAGE_EVENTS = 6;  // profile events: before project .. after blend

@@ -17,96 +17,19 @@
 #include <vector>
 
 #include "../../include/gsplat.h"
+#include "gs_internal.hpp"
 #include "gs_kernels.hpp"
 #include "host/gs_host.hpp"
 
 using gsh::set_error;
 
-namespace {
-
-constexpr int kProfileRing = 64;
-
-struct ProfileSlot {
-  hipEvent_t ev[gsk::GS_STAGE_EVENTS];
-  bool pending = false;
-};
-
-}  // namespace
-
-struct gs_renderer {
-  gs_config cfg{};
-  int device = 0;
-  size_t n = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-
-  // frame inputs (row-major as on the reference's wire)
-  float view_rm[16];
-  float proj_rm[16];
-  float fov = 0.6981317f;  // glm::radians(40.f) (splat.cpp:170)
-  float scale_div = 0.1f;  // lambda1 / 10 with lambda1 = 1 (InterfaceServer.hpp:238)
-
-  std::vector<uint32_t> perm;  // device index -> input index
-
-  // geometry
-  int tiles_x = 0, tiles_y = 0, band_ty0 = 0, band_stride = 1, band_nrows = 0, band_py0 = 0,
-      band_rows = 0;
-  int band_rows_padded = 0, n_tiles = 0;
-  uint64_t pair_cap = 0;
-
-  // device memory
-  void* d_scene = nullptr;      // 4 x float4 x n
-  void* d_gauss = nullptr;      // rec (48 B) + tail, rect, crect (8 B each) + depth key (4 B) per Gaussian
-  void* d_zero = nullptr;       // counters[16] + tile_count[n_tiles] (memset every frame)
-  void* d_tiles = nullptr;      // tile_start[n_tiles+1], tile_cursor, big_tiles
-  void* d_pairs = nullptr;      // pairs, pairs_alt, list
-  void* d_out = nullptr;        // rgba f32 + bgr8
-  void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
-  int bin_global = 0, chunk_size = 0, n_chunks = 0;
-  bool pair_cull = false;       // chunked binning into the alpha-box tiles only
-  size_t zero_bytes = 0;
-  size_t bgr_bytes = 0;
-  gsk::Buffers buf{};
-
-  // host mirrors
-  uint32_t* h_counters = nullptr;  // mapped pinned mirror of d_zero: counters[16] + tile_count[T]
-  std::vector<uint32_t> hist_snapshot;
-  std::mutex hist_mu;
-  bool frame_pending = false;
-  uint8_t* own_bgr = nullptr;     // the renderer's BGR8 band buffer
-  uint8_t* bgr_target = nullptr;  // gs_set_bgr8_target: frames write their BGR8 here instead
-  uint8_t* last_bgr = nullptr;    // where the last enqueued frame wrote its BGR8
-  bool have_frame = false;
-  gs_frame_stats stats{};
-  // the parameters of the last enqueued frame: the debug readbacks
-  // (gs_read_projected, gs_read_bins) reproduce THAT frame, not the current
-  // camera (a gs_set_view after the frame changes nothing they return)
-  gsk::FrameParams last_fp{};
-  bool have_fp = false;
-
-  // profiling
-  bool profile = false;
-  uint32_t profile_every = 1;  // stage events on every n-th frame
-  uint64_t frame_seq = 0;
-  ProfileSlot ring[kProfileRing];
-  int ring_head = 0;
-  double k_ms[GS_K_COUNT] = {0};
-  uint64_t k_launches[GS_K_COUNT] = {0};
-};
-
-namespace {
+namespace gsr {
 
 int hip_fail(hipError_t e, const char* what) {
   set_error(std::string(what) + ": " + hipGetErrorString(e));
   if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return GS_EOOM;
   return GS_EDEVICE;
 }
-
-#define GS_HIP(call)                                  \
-  do {                                                \
-    hipError_t e_ = (call);                           \
-    if (e_ != hipSuccess) return hip_fail(e_, #call); \
-  } while (0)
 
 int select_device(gs_renderer* r) {
   GS_HIP(hipSetDevice(r->device));
@@ -194,7 +117,8 @@ void release(gs_renderer* r) {
   if (!r) return;
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
-  for (void* p : {r->d_scene, r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk})
+  if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk})
     if (p) (void)hipFree(p);
   free_pairs(r);
   if (r->h_counters) (void)hipHostFree(r->h_counters);
@@ -288,7 +212,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
 int profile_harvest(gs_renderer* r, ProfileSlot& s) {
   if (!s.pending) return GS_OK;
   GS_HIP(hipEventSynchronize(s.ev[gsk::GS_STAGE_EVENTS - 1]));
-  for (int k = 0; k < GS_K_COUNT; ++k) {
+  for (int k = 0; k < kStages; ++k) {
     float ms = 0.0f;
     GS_HIP(hipEventElapsedTime(&ms, s.ev[k], s.ev[k + 1]));
     r->k_ms[k] += ms;
@@ -336,9 +260,14 @@ int enqueue_frame(gs_renderer* r) {
   GS_HIP(hipGetLastError());
   // the chunked scan writes the counters and list lengths into the mapped host
   // mirror itself; the other paths copy them (adjacent: one small D2H copy)
-  if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
+  if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0) {
     GS_HIP(hipMemcpyAsync(r->h_counters, r->d_zero, (16 + (size_t)r->n_tiles) * 4,
                           hipMemcpyDeviceToHost, s));
+    // (the chunked scan writes the group footer itself)
+    if (r->buf.footer)
+      GS_HIP(hipMemcpyAsync(r->buf.footer, r->d_zero, (16 + (size_t)r->n_tiles) * 4,
+                            hipMemcpyDeviceToDevice, s));
+  }
   r->frame_pending = true;
   return GS_OK;
 }
@@ -364,7 +293,7 @@ int finish_frame(gs_renderer* r) {
   r->stats.n_big_tiles = c[0];
   // the scan of EVERY frame ORs its overflow into the sticky word (several
   // frames may have run since the last sync; counters[3] is only the last one's)
-  volatile uint32_t* sticky = r->h_counters + 16 + r->n_tiles;
+  volatile uint32_t* sticky = r->h_counters + 16 + r->t_cap;
   const bool ovf = c[3] != 0 || *sticky != 0;
   *sticky = 0;
   if (ovf) {
@@ -380,42 +309,8 @@ int finish_frame(gs_renderer* r) {
   return GS_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int gs_abi_version(void) { return GSPLAT_ABI_VERSION; }
-
-const char* gs_last_error(void) { return gsh::last_error(); }
-
-int gs_device_count(int* count) {
-  if (!count) return GS_EINVAL;
-  int c = 0;
-  hipError_t e = hipGetDeviceCount(&c);
-  if (e != hipSuccess) {
-    *count = 0;
-    return hip_fail(e, "hipGetDeviceCount");
-  }
-  *count = c;
-  return GS_OK;
-}
-
-int gs_config_init(gs_config* cfg) {
-  if (!cfg) return GS_EINVAL;
-  std::memset(cfg, 0, sizeof(*cfg));
-  // tile_config.hpp:5-15: 1280x720, 40x36 tiles of 32x20; codelets.cpp:622
-  cfg->width = 1280;
-  cfg->height = 720;
-  cfg->tile_width = 32;
-  cfg->tile_height = 20;
-  cfg->guard_band = 15.0f;
-  cfg->device = -1;
-  cfg->band_index = 0;
-  cfg->band_count = 1;
-  return GS_OK;
-}
-
-int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_renderer** out) {
+int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_renderer* share,
+           gs_renderer** out) {
   if (!out || !cfg || (n > 0 && !g)) {
     set_error("gs_create: null argument");
     return GS_EINVAL;
@@ -490,7 +385,9 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
     r->band_rows = std::max(0, std::min((int)cfg->height, ty1 * th_px) - r->band_py0);
   }
   r->band_rows_padded = rpb * th_px;
+  r->rows_cap = rpb;
   r->n_tiles = r->tiles_x * r->band_nrows;
+  r->t_cap = r->n_tiles;
   r->stats.n_tiles = (uint32_t)r->n_tiles;
   r->stats.tiles_x = (uint32_t)r->tiles_x;
   r->stats.tiles_y = (uint32_t)r->band_nrows;
@@ -504,31 +401,40 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   r->stream = r->own_stream;
 
   // scene: SoA of the 64-B records, in device order (3D Morton order of the
-  // means unless GS_FLAG_INPUT_ORDER), plus the permutation both ways
+  // means unless GS_FLAG_INPUT_ORDER), plus the permutation both ways.  A
+  // renderer of a group shares the first one's copy on the same device.
   const size_t nn = std::max<size_t>(n, 1);
-  r->perm = morton_order(g, n, (cfg->flags & GS_FLAG_INPUT_ORDER) != 0);
-  if ((e = hipMalloc(&r->d_scene, nn * (64 + 8))) != hipSuccess)
-    return fail(hip_fail(e, "hipMalloc(scene)"));
-  {
-    std::vector<float> soa(nn * 16, 0.0f);
-    std::vector<uint32_t> pi(nn * 2, 0u);
-    for (size_t i = 0; i < n; ++i) {
-      const uint32_t o = r->perm[i];
-      const float* s = reinterpret_cast<const float*>(&g[o]);
-      for (int k = 0; k < 4; ++k) {
-        soa[(0 * nn + i) * 4 + k] = s[0 + k];
-        soa[(1 * nn + i) * 4 + k] = s[4 + k];
-        soa[(2 * nn + i) * 4 + k] = s[8 + k];
-        soa[(3 * nn + i) * 4 + k] = s[12 + k];
+  if (share && share->device == dev && share->n == n && share->d_scene) {
+    r->perm = share->perm;
+    r->d_scene = share->d_scene;
+    r->owns_scene = false;
+  } else {
+    r->perm = morton_order(g, n, (cfg->flags & GS_FLAG_INPUT_ORDER) != 0);
+    if ((e = hipMalloc(&r->d_scene, nn * (64 + 8))) != hipSuccess)
+      return fail(hip_fail(e, "hipMalloc(scene)"));
+    {
+      // staged in pinned host memory (one DMA at full PCIe rate)
+      float* soa = nullptr;
+      if ((e = hipHostMalloc((void**)&soa, nn * (64 + 8), hipHostMallocDefault)) != hipSuccess)
+        return fail(hip_fail(e, "hipHostMalloc(scene staging)"));
+      std::memset(soa, 0, nn * (64 + 8));
+      uint32_t* pi = (uint32_t*)(soa + nn * 16);
+      for (size_t i = 0; i < n; ++i) {
+        const uint32_t o = r->perm[i];
+        const float* s = reinterpret_cast<const float*>(&g[o]);
+        for (int k = 0; k < 4; ++k) {
+          soa[(0 * nn + i) * 4 + k] = s[0 + k];
+          soa[(1 * nn + i) * 4 + k] = s[4 + k];
+          soa[(2 * nn + i) * 4 + k] = s[8 + k];
+          soa[(3 * nn + i) * 4 + k] = s[12 + k];
+        }
+        pi[i] = o;
+        pi[nn + o] = (uint32_t)i;
       }
-      pi[i] = o;
-      pi[nn + o] = (uint32_t)i;
+      e = hipMemcpy(r->d_scene, soa, nn * (64 + 8), hipMemcpyHostToDevice);
+      (void)hipHostFree(soa);
+      if (e != hipSuccess) return fail(hip_fail(e, "hipMemcpy(scene)"));
     }
-    if ((e = hipMemcpy(r->d_scene, soa.data(), nn * 64, hipMemcpyHostToDevice)) != hipSuccess)
-      return fail(hip_fail(e, "hipMemcpy(scene)"));
-    if ((e = hipMemcpy((char*)r->d_scene + nn * 64, pi.data(), nn * 8, hipMemcpyHostToDevice)) !=
-        hipSuccess)
-      return fail(hip_fail(e, "hipMemcpy(permutation)"));
   }
   const float4* sc = (const float4*)r->d_scene;
   r->buf.mean = sc;
@@ -627,101 +533,49 @@ int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_rendere
   return GS_OK;
 }
 
-void gs_destroy(gs_renderer* r) {
+
+void destroy(gs_renderer* r) {
   if (!r) return;
   release(r);
   delete r;
 }
 
-int gs_set_view(gs_renderer* r, const float rowmajor[16]) {
-  if (!r || !rowmajor) return GS_EINVAL;
-  std::memcpy(r->view_rm, rowmajor, sizeof(r->view_rm));
-  return GS_OK;
-}
-
-int gs_set_projection(gs_renderer* r, const float rowmajor[16]) {
-  if (!r || !rowmajor) return GS_EINVAL;
-  std::memcpy(r->proj_rm, rowmajor, sizeof(r->proj_rm));
-  return GS_OK;
-}
-
-int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor) {
-  if (!r) return GS_EINVAL;
-  r->fov = fov_rad;
-  r->scale_div = scale_divisor;
-  return GS_OK;
-}
-
-int gs_set_stream(gs_renderer* r, void* hip_stream) {
-  if (!r) return GS_EINVAL;
-  if (r->frame_pending) {
-    set_error("gs_set_stream: a frame is in flight");
+int set_band_rows(gs_renderer* r, int ty0, int ty1, int pad_rows) {
+  if (ty0 < 0 || ty1 > r->tiles_y || ty1 <= ty0 || pad_rows < ty1 - ty0 || pad_rows > r->rows_cap ||
+      (ty1 - ty0) * r->tiles_x > r->t_cap) {
+    set_error("set_band_rows: band outside the renderer's tile rows");
     return GS_EINVAL;
   }
-  r->stream = hip_stream ? (hipStream_t)hip_stream : r->own_stream;
+  const int th_px = (int)r->cfg.tile_height;
+  r->band_ty0 = ty0;
+  r->band_stride = 1;
+  r->band_nrows = ty1 - ty0;
+  r->band_py0 = ty0 * th_px;
+  r->band_rows = std::max(0, std::min((int)r->cfg.height, ty1 * th_px) - r->band_py0);
+  r->band_rows_padded = pad_rows * th_px;
+  r->n_tiles = r->tiles_x * r->band_nrows;
+  r->bgr_bytes = (size_t)r->cfg.width * r->band_rows_padded * 3;
+  r->stats.n_tiles = (uint32_t)r->n_tiles;
+  r->stats.tiles_y = (uint32_t)r->band_nrows;
+  r->stats.band_stride = 1;
+  r->stats.band_y0 = (uint32_t)r->band_py0;
+  r->stats.band_rows = (uint32_t)r->band_rows;
   return GS_OK;
 }
 
-int gs_get_stream(gs_renderer* r, void** hip_stream) {
-  if (!r || !hip_stream) return GS_EINVAL;
-  *hip_stream = (void*)r->stream;
-  return GS_OK;
-}
-
-int gs_render_async(gs_renderer* r) {
-  if (!r) return GS_EINVAL;
-  int rc = select_device(r);
-  if (rc != GS_OK) return rc;
-  return enqueue_frame(r);
-}
-
-int gs_sync(gs_renderer* r) {
-  if (!r) return GS_EINVAL;
-  int rc = select_device(r);
-  if (rc != GS_OK) return rc;
-  return finish_frame(r);
-}
-
-int gs_render(gs_renderer* r) {
-  if (!r) return GS_EINVAL;
-  int rc = select_device(r);
-  if (rc != GS_OK) return rc;
-  for (int attempt = 0; attempt < 8; ++attempt) {
-    rc = enqueue_frame(r);
-    if (rc != GS_OK) return rc;
-    rc = finish_frame(r);
-    if (rc != GS_EOVERFLOW) return rc;
-    // grow the pair capacity (the reference silently drops on overflow)
-    const uint64_t need = r->stats.n_pairs_binned + r->stats.n_pairs_binned / 4 + 1024;
-    const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(need, 2 * r->pair_cap), 0xFFFFFFF0ull);
-    if (need > 0xFFFFFFF0ull) {
-      set_error("gs_render: pair count exceeds 2^32");
-      return GS_EOVERFLOW;
-    }
-    if (hipStreamSynchronize(r->stream) != hipSuccess) return GS_EDEVICE;
-    rc = alloc_pairs(r, cap);
-    if (rc != GS_OK) return rc;
+int grow_pairs(gs_renderer* r, bool force) {
+  const uint64_t need = r->stats.n_pairs_binned + r->stats.n_pairs_binned / 4 + 1024;
+  if (need > 0xFFFFFFF0ull) {
+    set_error("gs_render: pair count exceeds 2^32");
+    return GS_EOVERFLOW;
   }
-  set_error("gs_render: capacity growth did not converge");
-  return GS_EOVERFLOW;
+  if (!force && r->pair_cap >= need) return GS_OK;
+  const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(need, 2 * r->pair_cap), 0xFFFFFFF0ull);
+  GS_HIP(hipStreamSynchronize(r->stream));
+  return alloc_pairs(r, cap);
 }
 
-int gs_read_bgr8(gs_renderer* r, uint8_t* dst, size_t bytes) {
-  if (!r || !dst) return GS_EINVAL;
-  const size_t need = (size_t)r->band_rows * r->cfg.width * 3;
-  if (bytes < need) {
-    set_error("gs_read_bgr8: destination too small");
-    return GS_EINVAL;
-  }
-  int rc = select_device(r);
-  if (rc != GS_OK) return rc;
-  if ((rc = finish_frame(r)) != GS_OK) return rc;
-  GS_HIP(hipMemcpy(dst, r->last_bgr, need, hipMemcpyDeviceToHost));
-  return GS_OK;
-}
-
-int gs_read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
-  if (!r || !dst) return GS_EINVAL;
+int read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
   if (r->cfg.flags & GS_FLAG_NO_RGBA32F) {
     set_error("gs_read_rgba32f: renderer created with GS_FLAG_NO_RGBA32F");
     return GS_EINVAL;
@@ -740,7 +594,6 @@ int gs_read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
     return GS_OK;
   }
   if (layout != GS_LAYOUT_REF_TILE_MAJOR) return GS_EINVAL;
-  // the IPU layout (ipu_rasteriser.cpp:164-214 + codelets.cpp:174-176)
   const size_t tw = r->cfg.tile_width, th = r->cfg.tile_height;
   const size_t need = (size_t)r->n_tiles * tw * th * 4;
   if (n_floats < need) {
@@ -749,9 +602,16 @@ int gs_read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
   }
   std::vector<float> rm(rows * W * 4);
   GS_HIP(hipMemcpy(rm.data(), r->buf.rgba, rm.size() * 4, hipMemcpyDeviceToHost));
-  std::memset(dst, 0, need * 4);
-  for (int t = 0; t < r->n_tiles; ++t) {
-    const size_t tx = t % r->tiles_x, ty = t / r->tiles_x;
+  retile(rm.data(), rows, W, tw, th, r->tiles_x, r->n_tiles, dst);
+  return GS_OK;
+}
+
+// the IPU layout (ipu_rasteriser.cpp:164-214 + codelets.cpp:174-176)
+void retile(const float* rm, size_t rows, size_t W, size_t tw, size_t th, int tiles_x, int n_tiles,
+            float* dst) {
+  std::memset(dst, 0, (size_t)n_tiles * tw * th * 16);
+  for (int t = 0; t < n_tiles; ++t) {
+    const size_t tx = t % tiles_x, ty = t / tiles_x;
     for (size_t ly = 0; ly < th; ++ly) {
       const size_t y = ty * th + ly;
       if (y >= rows) break;
@@ -762,30 +622,9 @@ int gs_read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
       }
     }
   }
-  return GS_OK;
 }
 
-int gs_read_tile_histogram(gs_renderer* r, uint32_t* dst, size_t n) {
-  if (!r || !dst) return GS_EINVAL;
-  std::lock_guard<std::mutex> lk(r->hist_mu);
-  if (n < r->hist_snapshot.size()) {
-    set_error("gs_read_tile_histogram: destination too small");
-    return GS_EINVAL;
-  }
-  std::copy(r->hist_snapshot.begin(), r->hist_snapshot.end(), dst);
-  return GS_OK;
-}
-
-int gs_get_stats(gs_renderer* r, gs_frame_stats* st) {
-  if (!r || !st) return GS_EINVAL;
-  *st = r->stats;
-  st->pair_capacity = r->pair_cap;
-  return GS_OK;
-}
-
-int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list,
-                 size_t n_list) {
-  if (!r || !tile_start || (!list && n_list)) return GS_EINVAL;
+int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list, size_t n_list) {
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
@@ -805,20 +644,31 @@ int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t*
     // the BGR8 target, the stats and the histogram snapshot are untouched.
     gsk::FrameParams fp = r->last_fp;
     fp.pair_cull = 0;
+    gsk::Buffers bb = r->buf;
+    bb.footer = nullptr;  // (a group's all-gather slot belongs to the frame)
     for (int attempt = 0; attempt < 8; ++attempt) {
       fp.pair_cap = r->pair_cap;
+      bb.pairs = r->buf.pairs;
+      bb.pairs_alt = r->buf.pairs_alt;
+      bb.list = r->buf.list;
+      bb.big_item = r->buf.big_item;
+      bb.bk_spl = r->buf.bk_spl;
+      bb.bk_start = r->buf.bk_start;
+      bb.bk_cnt = r->buf.bk_cnt;
+      bb.bk_list = r->buf.bk_list;
+      bb.bk_off = r->buf.bk_off;
       fp.big_separate = 0;  // the tile sort radix-sorts big lists itself
       if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
         GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, r->stream));
-      gsk::launch_project(fp, r->buf, r->stream);
-      gsk::launch_scan(fp, r->buf, r->stream);
-      gsk::launch_emit(fp, r->buf, r->stream);
-      gsk::launch_sort(fp, r->buf, r->stream);
+      gsk::launch_project(fp, bb, r->stream);
+      gsk::launch_scan(fp, bb, r->stream);
+      gsk::launch_emit(fp, bb, r->stream);
+      gsk::launch_sort(fp, bb, r->stream);
       GS_HIP(hipGetLastError());
       if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
         GS_HIP(hipMemcpyAsync(r->h_counters, r->d_zero, (16 + T) * 4, hipMemcpyDeviceToHost, r->stream));
       GS_HIP(hipStreamSynchronize(r->stream));
-      volatile uint32_t* sticky = r->h_counters + 16 + r->n_tiles;
+      volatile uint32_t* sticky = r->h_counters + 16 + r->t_cap;
       *sticky = 0;
       const uint32_t* c = r->h_counters;
       const uint64_t P = (uint64_t)c[5] | ((uint64_t)c[6] << 32);
@@ -842,8 +692,7 @@ int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t*
   return GS_OK;
 }
 
-int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
-  if (!r || !dst) return GS_EINVAL;
+int read_projected(gs_renderer* r, float* dst, size_t n_floats) {
   if (n_floats < r->n * 12) {
     set_error("gs_read_projected: destination too small");
     return GS_EINVAL;
@@ -869,8 +718,6 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     gsk::launch_project(fp, r->buf, r->stream);
     GS_HIP(hipGetLastError());
     GS_HIP(hipStreamSynchronize(r->stream));
-  }
-  if (r->n) {
     GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 48, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(tail.data(), r->buf.rec_tail, r->n * 8, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(rect.data(), r->buf.rect, r->n * 8, hipMemcpyDeviceToHost));
@@ -895,15 +742,211 @@ int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
   return GS_OK;
 }
 
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+int gs_abi_version(void) { return GSPLAT_ABI_VERSION; }
+
+const char* gs_last_error(void) { return gsh::last_error(); }
+
+int gs_device_count(int* count) {
+  if (!count) return GS_EINVAL;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *count = c;
+  return GS_OK;
+}
+
+int gs_config_init(gs_config* cfg) {
+  if (!cfg) return GS_EINVAL;
+  std::memset(cfg, 0, sizeof(*cfg));
+  // tile_config.hpp:5-15: 1280x720, 40x36 tiles of 32x20; codelets.cpp:622
+  cfg->width = 1280;
+  cfg->height = 720;
+  cfg->tile_width = 32;
+  cfg->tile_height = 20;
+  cfg->guard_band = 15.0f;
+  cfg->device = -1;
+  cfg->band_index = 0;
+  cfg->band_count = 1;
+  for (int k = 0; k < GS_MAX_GPUS; ++k) cfg->device_ids[k] = k;
+  return GS_OK;
+}
+
+int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_renderer** out) {
+  if (cfg && cfg->num_gpus > 0) return gsg::create(g, n, cfg, nullptr, 0, 1, out);
+  return gsr::create(g, n, cfg, nullptr, out);
+}
+
+int gs_create_rank(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_comm_id* id,
+                   int rank, int world, gs_renderer** out) {
+  if (!id) {
+    set_error("gs_create_rank: null communicator id");
+    return GS_EINVAL;
+  }
+  return gsg::create(g, n, cfg, id, rank, world, out);
+}
+
+void gs_destroy(gs_renderer* r) {
+  if (!r) return;
+  if (r->grp) {
+    gsg::destroy(r->grp);
+    delete r;
+    return;
+  }
+  gsr::destroy(r);
+}
+
+int gs_set_view(gs_renderer* r, const float rowmajor[16]) {
+  if (!r || !rowmajor) return GS_EINVAL;
+  if (r->grp) return gsg::set_view(r->grp, rowmajor);
+  std::memcpy(r->view_rm, rowmajor, sizeof(r->view_rm));
+  return GS_OK;
+}
+
+int gs_set_projection(gs_renderer* r, const float rowmajor[16]) {
+  if (!r || !rowmajor) return GS_EINVAL;
+  if (r->grp) return gsg::set_projection(r->grp, rowmajor);
+  std::memcpy(r->proj_rm, rowmajor, sizeof(r->proj_rm));
+  return GS_OK;
+}
+
+int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor) {
+  if (!r) return GS_EINVAL;
+  if (r->grp) return gsg::set_focal(r->grp, fov_rad, scale_divisor);
+  r->fov = fov_rad;
+  r->scale_div = scale_divisor;
+  return GS_OK;
+}
+
+int gs_set_stream(gs_renderer* r, void* hip_stream) {
+  if (!r) return GS_EINVAL;
+  if (r->grp) {
+    set_error("gs_set_stream: a row-band group runs its frames on its own streams");
+    return GS_EINVAL;
+  }
+  if (r->frame_pending) {
+    set_error("gs_set_stream: a frame is in flight");
+    return GS_EINVAL;
+  }
+  r->stream = hip_stream ? (hipStream_t)hip_stream : r->own_stream;
+  return GS_OK;
+}
+
+int gs_get_stream(gs_renderer* r, void** hip_stream) {
+  if (!r || !hip_stream) return GS_EINVAL;
+  if (r->grp) return gsg::get_stream(r->grp, hip_stream);
+  *hip_stream = (void*)r->stream;
+  return GS_OK;
+}
+
+int gs_render_async(gs_renderer* r) {
+  if (!r) return GS_EINVAL;
+  if (r->grp) return gsg::render_async(r->grp);
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  return enqueue_frame(r);
+}
+
+int gs_sync(gs_renderer* r) {
+  if (!r) return GS_EINVAL;
+  if (r->grp) return gsg::sync(r->grp);
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  return finish_frame(r);
+}
+
+int gs_render(gs_renderer* r) {
+  if (!r) return GS_EINVAL;
+  if (r->grp) return gsg::render(r->grp);
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    rc = enqueue_frame(r);
+    if (rc != GS_OK) return rc;
+    rc = finish_frame(r);
+    if (rc != GS_EOVERFLOW) return rc;
+    // grow the pair capacity (the reference silently drops on overflow)
+    if ((rc = grow_pairs(r, true)) != GS_OK) return rc;
+  }
+  set_error("gs_render: capacity growth did not converge");
+  return GS_EOVERFLOW;
+}
+
+int gs_read_bgr8(gs_renderer* r, uint8_t* dst, size_t bytes) {
+  if (!r || !dst) return GS_EINVAL;
+  if (r->grp) return gsg::read_bgr8(r->grp, dst, bytes);
+  const size_t need = (size_t)r->band_rows * r->cfg.width * 3;
+  if (bytes < need) {
+    set_error("gs_read_bgr8: destination too small");
+    return GS_EINVAL;
+  }
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if ((rc = finish_frame(r)) != GS_OK) return rc;
+  GS_HIP(hipMemcpy(dst, r->last_bgr, need, hipMemcpyDeviceToHost));
+  return GS_OK;
+}
+
+int gs_read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
+  if (!r || !dst) return GS_EINVAL;
+  if (r->grp) return gsg::read_rgba32f(r->grp, dst, n_floats, layout);
+  return gsr::read_rgba32f(r, dst, n_floats, layout);
+}
+
+int gs_read_tile_histogram(gs_renderer* r, uint32_t* dst, size_t n) {
+  if (!r || !dst) return GS_EINVAL;
+  if (r->grp) return gsg::read_tile_histogram(r->grp, dst, n);
+  std::lock_guard<std::mutex> lk(r->hist_mu);
+  if (n < r->hist_snapshot.size()) {
+    set_error("gs_read_tile_histogram: destination too small");
+    return GS_EINVAL;
+  }
+  std::copy(r->hist_snapshot.begin(), r->hist_snapshot.end(), dst);
+  return GS_OK;
+}
+
+int gs_get_stats(gs_renderer* r, gs_frame_stats* st) {
+  if (!r || !st) return GS_EINVAL;
+  if (r->grp) return gsg::get_stats(r->grp, st);
+  *st = r->stats;
+  st->pair_capacity = r->pair_cap;
+  return GS_OK;
+}
+
+int gs_read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list,
+                 size_t n_list) {
+  if (!r || !tile_start || (!list && n_list)) return GS_EINVAL;
+  if (r->grp) return gsg::read_bins(r->grp, tile_start, n_start, list, n_list);
+  return gsr::read_bins(r, tile_start, n_start, list, n_list);
+}
+
+int gs_read_projected(gs_renderer* r, float* dst, size_t n_floats) {
+  if (!r || !dst) return GS_EINVAL;
+  if (r->grp) return gsg::read_projected(r->grp, dst, n_floats);
+  return gsr::read_projected(r, dst, n_floats);
+}
+
 int gs_bgr8_device(gs_renderer* r, void** dev_ptr, size_t* bytes) {
   if (!r || !dev_ptr || !bytes) return GS_EINVAL;
+  if (r->grp) {
+    set_error("gs_bgr8_device: a row-band group gathers its frame itself (gs_read_bgr8)");
+    return GS_EINVAL;
+  }
   *dev_ptr = r->own_bgr;
   *bytes = r->bgr_bytes;
   return GS_OK;
 }
 
 int gs_copy_bgr8_device(gs_renderer* r, void* dst_dev, size_t bytes) {
-  if (!r || !dst_dev || bytes < r->bgr_bytes) return GS_EINVAL;
+  if (!r || !dst_dev || r->grp || bytes < r->bgr_bytes) return GS_EINVAL;
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   GS_HIP(hipMemcpyAsync(dst_dev, r->last_bgr, r->bgr_bytes, hipMemcpyDeviceToDevice, r->stream));
@@ -912,6 +955,10 @@ int gs_copy_bgr8_device(gs_renderer* r, void* dst_dev, size_t bytes) {
 
 int gs_set_bgr8_target(gs_renderer* r, void* dst_dev, size_t bytes) {
   if (!r) return GS_EINVAL;
+  if (r->grp) {
+    set_error("gs_set_bgr8_target: a row-band group writes its bands into its own all-gather buffers");
+    return GS_EINVAL;
+  }
   if (dst_dev && bytes < r->bgr_bytes) {
     set_error("gs_set_bgr8_target: destination smaller than the padded band");
     return GS_EINVAL;
@@ -922,6 +969,7 @@ int gs_set_bgr8_target(gs_renderer* r, void* dst_dev, size_t bytes) {
 
 int gs_kernel_times(gs_renderer* r, double* avg_ms, uint64_t* launches, int n) {
   if (!r || !avg_ms) return GS_EINVAL;
+  if (r->grp) return gsg::kernel_times(r->grp, avg_ms, launches, n);
   if (!r->profile) {
     set_error("gs_kernel_times: renderer created without GS_FLAG_PROFILE");
     return GS_EINVAL;
@@ -939,6 +987,7 @@ int gs_kernel_times(gs_renderer* r, double* avg_ms, uint64_t* launches, int n) {
 
 int gs_set_profile_interval(gs_renderer* r, uint32_t every) {
   if (!r || every == 0) return GS_EINVAL;
+  if (r->grp) return gsg::set_profile_interval(r->grp, every);
   r->profile_every = every;
   r->frame_seq = 0;
   return GS_OK;
@@ -946,6 +995,7 @@ int gs_set_profile_interval(gs_renderer* r, uint32_t every) {
 
 int gs_reset_kernel_times(gs_renderer* r) {
   if (!r) return GS_EINVAL;
+  if (r->grp) return gsg::reset_kernel_times(r->grp);
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   for (auto& s : r->ring)
@@ -954,6 +1004,24 @@ int gs_reset_kernel_times(gs_renderer* r) {
     r->k_ms[k] = 0.0;
     r->k_launches[k] = 0;
   }
+  return GS_OK;
+}
+
+int gs_group_bands(gs_renderer* r, uint32_t* bounds, size_t n) {
+  if (!r || !bounds) return GS_EINVAL;
+  if (!r->grp) {
+    set_error("gs_group_bands: not a row-band group");
+    return GS_EINVAL;
+  }
+  return gsg::bands(r->grp, bounds, n);
+}
+
+int gs_balanced_bands(const double* row_work, uint32_t rows, uint32_t world, uint32_t* bounds) {
+  if (!row_work || !bounds || world == 0 || rows < world) {
+    set_error("gs_balanced_bands: need rows >= world >= 1");
+    return GS_EINVAL;
+  }
+  gsg::balanced_bands(row_work, (int)rows, (int)world, bounds);
   return GS_OK;
 }
 

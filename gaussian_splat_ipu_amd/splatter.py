@@ -22,7 +22,9 @@ import numpy as np
 from . import camera
 from ._lib import (
     GS_FLAG_BAND_CULL,
+    GS_FLAG_GATHER_COPY,
     GS_FLAG_NO_PAIR_CULL,
+    GS_FLAG_NO_REBALANCE,
     GS_FLAG_BAND_INTERLEAVED,
     GS_FLAG_BIN_GLOBAL,
     GS_FLAG_INPUT_ORDER,
@@ -32,6 +34,7 @@ from ._lib import (
     GS_LAYOUT_REF_TILE_MAJOR,
     GS_LAYOUT_ROW_MAJOR,
     KERNEL_NAMES,
+    CommId,
     Config,
     FrameStats,
     Gaussian3D,
@@ -49,7 +52,19 @@ def device_count() -> int:
     return c.value if rc == 0 else 0
 
 
+def comm_id_create() -> bytes:
+    """Rank 0 of a one-process-per-GPU group: a fresh ncclUniqueId (128 bytes)
+    to hand to every rank's GpuSplatter(comm_id=...)."""
+    cid = CommId()
+    check(lib().gs_comm_id_create(C.byref(cid)), "gs_comm_id_create")
+    return bytes(cid.bytes)
+
+
 class GpuSplatter:
+    """One renderer (a band of one device), or -- with ``num_gpus`` or
+    ``comm_id`` -- a row-band group: the tile rows split over several GPUs and
+    gathered by one all-gather per frame inside execute() (gs_group.hip)."""
+
     def __init__(
         self,
         gaussians,
@@ -70,6 +85,14 @@ class GpuSplatter:
         pair_cull: bool = True,
         band_rows=None,
         band_pad_rows: int = 0,
+        num_gpus: int = 0,
+        device_ids=None,
+        frames_in_flight: int = 0,
+        rebalance: bool = True,
+        gather_copy: bool = False,
+        comm_id: bytes | None = None,
+        rank: int = 0,
+        world: int = 1,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -98,11 +121,26 @@ class GpuSplatter:
             | (GS_FLAG_BAND_INTERLEAVED if band_interleaved else 0)
             | (GS_FLAG_BAND_CULL if band_cull else 0)
             | (0 if pair_cull else GS_FLAG_NO_PAIR_CULL)
+            | (0 if rebalance else GS_FLAG_NO_REBALANCE)
+            | (GS_FLAG_GATHER_COPY if gather_copy else 0)
         )
+        cfg.num_gpus = int(num_gpus)
+        if device_ids is not None:
+            for k, d in enumerate(device_ids):
+                cfg.device_ids[k] = int(d)
+        cfg.frames_in_flight = int(frames_in_flight)
         self.cfg = cfg
+        self.group = num_gpus > 0 or comm_id is not None
+        self.world = world if comm_id is not None else max(1, int(num_gpus))
         h = C.c_void_p()
         gp = g.ctypes.data_as(C.POINTER(Gaussian3D)) if self.n else None
-        check(lib().gs_create(gp, self.n, C.byref(cfg), C.byref(h)), "gs_create")
+        if comm_id is not None:
+            cid = CommId()
+            C.memmove(cid.bytes, bytes(comm_id), 128)
+            check(lib().gs_create_rank(gp, self.n, C.byref(cfg), C.byref(cid), int(rank), int(world), C.byref(h)),
+                  "gs_create_rank")
+        else:
+            check(lib().gs_create(gp, self.n, C.byref(cfg), C.byref(h)), "gs_create")
         self._h = h
         st = self.stats()
         self.n_tiles = st["n_tiles"]
@@ -239,6 +277,12 @@ class GpuSplatter:
 
     def copy_bgr8_device(self, dst_ptr: int, nbytes: int) -> None:
         check(lib().gs_copy_bgr8_device(self._h, C.c_void_p(dst_ptr), nbytes))
+
+    def bands(self):
+        """Group: the split of the last frame, [(ty0, ty1), ...] tile rows per band."""
+        b = (C.c_uint32 * (self.world + 1))()
+        check(lib().gs_group_bands(self._h, b, self.world + 1))
+        return [(b[i], b[i + 1]) for i in range(self.world)]
 
     def kernel_times(self) -> dict:
         avg = (C.c_double * GS_K_COUNT)()

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 5
+#define GSPLAT_ABI_VERSION 6
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -70,7 +70,21 @@ typedef struct gs_config {
    * the BGR8 band is padded to this many tile rows (>= the band's), so every
    * rank of an all-gather contributes the same number of bytes.  0 = none. */
   uint32_t band_row_begin, band_row_end, band_pad_rows;
+  /* ABI 6: row-band group (SURVEY §8 b/e: "multi-GPU fan-out is internal to
+   * gs_render").  num_gpus >= 1 makes gs_create return ONE handle over
+   * num_gpus devices of this process (device_ids[0..num_gpus)): the tile rows
+   * are split into num_gpus contiguous bands, one per device, re-balanced from
+   * the tile histograms of earlier frames, and every frame ends with one
+   * all-gather of the BGR8 bands (RCCL, ncclCommInitAll over the devices).
+   * The band fields above are then ignored.  num_gpus = 0: one renderer (the
+   * band fields apply).  frames_in_flight (group only, 0 = 1): frames a group
+   * keeps in flight under gs_render_async, each on its own HIP stream. */
+  uint32_t num_gpus;
+  int32_t device_ids[16];
+  uint32_t frames_in_flight;
 } gs_config;
+
+#define GS_MAX_GPUS 16
 
 #define GS_FLAG_NO_RGBA32F 1u  /* skip the RGBA f32 framebuffer store (BGR8 only) */
 #define GS_FLAG_PROFILE 2u     /* record HIP events around every kernel     */
@@ -93,6 +107,13 @@ typedef struct gs_config {
                                   tiles its alpha >= 1/255 box meets (the
                                   frame is bit-identical; the histogram and
                                   gs_read_bins keep the reference lists) */
+#define GS_FLAG_NO_REBALANCE 128u /* group: keep the first split (equal tile-row
+                                  bands) instead of re-balancing it from the
+                                  histograms of earlier frames */
+#define GS_FLAG_GATHER_COPY 256u /* group, one process: gather the bands with
+                                  device-to-device copies instead of RCCL
+                                  (automatic when device_ids repeat a device:
+                                  several bands emulated on one GPU) */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */
@@ -132,7 +153,10 @@ enum {
   GS_K_EMIT = 2,
   GS_K_SORT = 3,
   GS_K_BLEND = 4,
-  GS_K_COUNT = 5
+  GS_K_GATHER = 5,  /* group: the frame's all-gather on the communication
+                       stream, from the local band's completion to the
+                       gathered frame (includes waiting for the slowest rank) */
+  GS_K_COUNT = 6
 };
 
 typedef struct gs_renderer gs_renderer;
@@ -152,6 +176,30 @@ int gs_config_init(gs_config* cfg);
 int gs_create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, gs_renderer** out);
 /* Replaces IpuSplatter::~IpuSplatter. */
 void gs_destroy(gs_renderer* r);
+
+/* ABI 6: one process per GPU.  The row-band group of gs_create (num_gpus) as
+ * one rank of `world` processes: this process renders band `rank` on
+ * cfg->device and every frame ends with one ncclAllGather over a communicator
+ * built from `id` (ncclCommInitRank).  Rank 0 creates the id
+ * (gs_comm_id_create) and the caller hands its bytes to the other ranks (e.g.
+ * a torch.distributed broadcast).  Every rank must call gs_render /
+ * gs_render_async for every frame (the all-gather is collective); camera
+ * inputs must be the same on every rank.  gs_read_bgr8 and
+ * gs_read_tile_histogram return the whole frame on every rank. */
+typedef struct gs_comm_id {
+  unsigned char bytes[128]; /* ncclUniqueId */
+} gs_comm_id;
+int gs_comm_id_create(gs_comm_id* out);
+int gs_create_rank(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_comm_id* id,
+                   int rank, int world, gs_renderer** out);
+/* Group: the split of the last enqueued frame as world + 1 tile-row bounds
+ * (band r = tile rows [bounds[r], bounds[r + 1])). */
+int gs_group_bands(gs_renderer* r, uint32_t* bounds, size_t n);
+/* The group's split rule (host only, no device): `world` contiguous bands of
+ * nearly equal work over `rows` tile rows, every band at least one row;
+ * bounds = world + 1 entries.  Deterministic, so every rank derives the same
+ * split from the same gathered histograms. */
+int gs_balanced_bands(const double* row_work, uint32_t rows, uint32_t world, uint32_t* bounds);
 
 /* ------------------------------------------------------------ per-frame inputs */
 /* Replaces IpuSplatter::updateModelView (ipu_rasteriser.cpp:86-93): the
@@ -249,6 +297,19 @@ int gs_ply_synthetic(const gs_synth_params* sp, gs_ply** out);
  * raw log-scale, raw rotation, gid = i + 1.  bb_out = min[3], max[3] of the
  * centred points (may be NULL). */
 int gs_scene_prepare(const gs_ply* p, gs_gaussian3d* out, size_t n, float* bb_out);
+
+/* The render server's `--device cpu` path (src/splat/cpu_rasteriser.cpp:9-92,
+ * splat.cpp:250-256): the reference's CPU POINT splatter, not a Gaussian
+ * rasteriser and not a fallback of gs_render.  Projects every point with
+ * projection * view (row-major wire matrices), adds `value` (the reference:
+ * 25) to the three channels of its pixel of the W x H BGR8 image (saturating;
+ * the caller zeroes the image per frame, splat.cpp:247), counts the points
+ * that land in the image (*splatted) and, if tile_hist is not NULL, per tile
+ * of the (W / tile_w) x (H / tile_h) grid (buildTileHistogram).  nthreads <= 0:
+ * all hardware threads. */
+int gs_cpu_point_splat(const float* xyz, size_t n, const float* view_rm, const float* proj_rm,
+                       uint32_t width, uint32_t height, uint32_t tile_w, uint32_t tile_h, uint8_t value,
+                       uint8_t* bgr, uint32_t* tile_hist, uint32_t* splatted, int nthreads);
 
 /* ------------------------------------------------------------ camera (glm, column-major) */
 int gs_mat4_mul(const float* a, const float* b, float* out);

@@ -47,7 +47,7 @@ def test_abi_version_and_config_defaults(built):
     from gaussian_splat_ipu_amd import _lib
 
     L = _lib.lib()
-    assert L.gs_abi_version() == 5
+    assert L.gs_abi_version() == 6
     cfg = _lib.Config()
     assert L.gs_config_init(ctypes.byref(cfg)) == 0
     # tile_config.hpp:5-15 and codelets.cpp:622
@@ -87,7 +87,8 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
         "  splat::gs_check(gs_config_init(&c), \"init\");\n"
         "  splat::GpuSplatter* p = nullptr;  // the class is instantiable\n"
         "  (void)p;\n"
-        "  std::printf(\"%d %u\\n\", gs_abi_version(), c.tile_width);\n"
+        "  std::printf(\"%d %u %zu %zu %zu\\n\", gs_abi_version(), c.tile_width, sizeof(gs_config),\n"
+        "              sizeof(gs_frame_stats), sizeof(gs_comm_id));\n"
         "  return 0;\n"
         "}\n"
     )
@@ -96,4 +97,35 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
                     "-L", libdir, "-lgsplat", f"-Wl,-rpath,{libdir}"], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    assert int(out[0]) == 5
+    assert int(out[0]) == 6
+    # the ctypes mirrors have the C layouts
+    assert int(out[2]) == ctypes.sizeof(_lib.Config)
+    assert int(out[3]) == ctypes.sizeof(_lib.FrameStats)
+    assert int(out[4]) == ctypes.sizeof(_lib.CommId) == 128
+
+
+def test_balanced_bands_matches_the_python_rule(built):
+    """gs_balanced_bands (the row-band group's split rule, gs_group.hip) is
+    dist.balanced_bands: every rank must derive the same split."""
+    import numpy as np
+
+    from gaussian_splat_ipu_amd import _lib, dist
+
+    L = _lib.lib()
+    rng = np.random.default_rng(3)
+    cases = [(np.ones(68), 8), (np.zeros(9), 3), (np.arange(1, 11, dtype=np.float64), 10)]
+    for _ in range(200):
+        rows = int(rng.integers(1, 140))
+        world = int(rng.integers(1, min(rows, 16) + 1))
+        w = rng.exponential(1.0, rows) * (rng.random(rows) < 0.7)
+        cases.append((w, world))
+    for w, world in cases:
+        w = np.ascontiguousarray(w, np.float64)
+        b = (ctypes.c_uint32 * (world + 1))()
+        assert L.gs_balanced_bands(w.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), w.size, world, b) == 0
+        want = dist.balanced_bands(w, world)
+        got = [(b[i], b[i + 1]) for i in range(world)]
+        assert got == [(int(a), int(c)) for a, c in want], (w, world)
+    b = (ctypes.c_uint32 * 4)()
+    one = np.ones(2)
+    assert L.gs_balanced_bands(one.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 2, 3, b) == _lib.GS_EINVAL

@@ -1,6 +1,9 @@
 """Summarise rocprofv3 output of tools/profile.sh into per-kernel averages.
 
-    python tools/pmc_summary.py gpurun_out/prof [--config 1000000@1920x1080/t16/w1] [--json out.json]
+    python tools/pmc_summary.py gpurun_out/prof [--config KEY] [--json out.json]
+
+KEY is the bench line's config.pmc_key (workload, split, band); by default it
+is read from the bench lines the profiled runs printed (<dir>/*.log).
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half of the bytes of a
@@ -49,9 +52,18 @@ def load_stats(d):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--config", default="1000000@1920x1080/t16/w1")
+    ap.add_argument("--config", default=None)
     ap.add_argument("--json")
     a = ap.parse_args()
+    if a.config is None:
+        keys = set()
+        for f in glob.glob(os.path.join(a.dir, "*.log")) + glob.glob(os.path.join(os.path.dirname(a.dir.rstrip("/")), "*.log")):
+            for line in open(f, errors="replace"):
+                if line.startswith("{") and '"pmc_key"' in line:
+                    keys.add(json.loads(line)["config"]["pmc_key"])
+        if len(keys) != 1:
+            raise SystemExit(f"cannot tell the workload key from the bench logs: {sorted(keys)}")
+        a.config = keys.pop()
     ctr = load_counters(a.dir)
     st = load_stats(a.dir)
     kernels = {}
