@@ -1,16 +1,26 @@
-// splat_main.cpp -- the render server's headless frame loop on the C ABI
-// (reference: src/main/splat.cpp:24-329).
+// splat_main.cpp -- the render server on the C ABI (SURVEY §8 f1 + f3;
+// reference: src/main/splat.cpp:24-329).
 //
-//   splat --input scene.ply [--device gpu] [--log-level info] [--ui-port 0]
-//         [--width 1280 --height 720 --tile-width 32 --tile-height 20]
+//   splat --input scene.ply [--device cpu|gpu] [--log-level info] [--ui-port 0]
+//         [--gpus N] [--width 1280 --height 720 --tile-width 32 --tile-height 20]
 //         [--frames 1] [--scale-div 0.1] [--out test.png]
 //
 // Same flags and flow as the reference: load the PLY, centre + negate z,
-// build the Gaussians, set up the headless camera, render, log
-// "Splat time: {} points/sec: {}" per frame (splat.cpp:272,318) and write
-// test.png (splat.cpp:326).  --device gpu replaces --device ipu; the
-// reference's --device cpu point splatter and the remote UI (--ui-port) are
-// not part of this build and are rejected with a clear message.
+// build the Gaussians, set up the camera (lookAtBoundingBox, frustum fitted to
+// the eye-space bounds, first view mvpStart), then the frame loop:
+//   --device cpu  the reference's CPU point splatter (gs_cpu_point_splat,
+//                 cpu_rasteriser.cpp:9-92), the reference's default device;
+//   --device gpu  the Gaussian frame path on the MI355X (gs_render; "ipu" is
+//                 accepted as an alias), --gpus N: N devices as one row-band
+//                 group (one all-gather per frame inside gs_render).
+// Without --ui-port the loop runs --frames frames (the reference: exactly one,
+// splat.cpp:322) and logs "Splat time: {} points/sec: {}" (:318).  With
+// --ui-port (built with REMOTE_UI=1) it serves one remote-UI client
+// (remote_ui.hpp): after every frame the histogram and a preview go out on an
+// AsyncTask thread, the UI state is consumed, the projection is refitted to
+// the state's fov and the view rebuilt from its rotations and X/Y/Z
+// (splat.cpp:280-315), until the client sends "stop".  test.png is the last
+// rendered frame (splat.cpp:326).
 #include <zlib.h>
 
 #include <chrono>
@@ -18,25 +28,29 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../../include/gsplat.h"
 #include "../../../include/gsplat.hpp"
+#if GSPLAT_REMOTE_UI
+#include "remote_ui.hpp"
+#endif
 
 namespace {
 
 struct Args {
-  std::string input, device = "gpu", log_level = "info", out = "test.png";
-  int ui_port = 0, frames = 1;
+  std::string input, device = "cpu", log_level = "info", out = "test.png";
+  int ui_port = 0, frames = 1, gpus = 0;
   uint32_t width = 1280, height = 720, tw = 32, th = 20;
-  float scale_div = 0.1f;  // lambda1 / 10 (InterfaceServer.hpp:238, splat.cpp:262)
+  float scale_div = -1.0f;  // default: lambda1 / 10 = 0.1 (InterfaceServer.hpp:238, splat.cpp:262)
 };
 
 void usage() {
   std::printf(
-      "splat --input <file.ply|file.xyz> [--device gpu] [--log-level info] [--ui-port 0]\n"
-      "      [--width 1280] [--height 720] [--tile-width 32] [--tile-height 20]\n"
+      "splat --input <file.ply|file.xyz> [--device cpu|gpu] [--log-level info] [--ui-port 0]\n"
+      "      [--gpus N] [--width 1280] [--height 720] [--tile-width 32] [--tile-height 20]\n"
       "      [--frames 1] [--scale-div 0.1] [--out test.png]\n");
 }
 
@@ -61,6 +75,8 @@ bool parse(int argc, char** argv, Args& a) {
       a.log_level = val();
     } else if (k == "--ui-port") {
       a.ui_port = std::atoi(val());
+    } else if (k == "--gpus") {
+      a.gpus = std::atoi(val());
     } else if (k == "--width") {
       a.width = (uint32_t)std::atoi(val());
     } else if (k == "--height") {
@@ -146,6 +162,61 @@ bool write_png(const std::string& path, const uint8_t* bgr, uint32_t w, uint32_t
   return ok;
 }
 
+float radians(float deg) { return deg * 0.01745329251994329576923690768489f; }  // glm::radians
+
+struct Mat4 {
+  float m[16];  // glm column-major
+};
+
+Mat4 transposed(const Mat4& a) {
+  Mat4 r;
+  splat::gs_check(gs_mat4_transpose(a.m, r.m), "transpose");
+  return r;
+}
+
+// The render-server's GPU device: one renderer, or a row-band group over
+// --gpus devices, created on first use (a --device cpu run needs no GPU).
+class GpuDevice {
+ public:
+  GpuDevice(const std::vector<gs_gaussian3d>& g, const Args& a) {
+    gs_config cfg;
+    splat::gs_check(gs_config_init(&cfg), "gs_config_init");
+    cfg.width = a.width;
+    cfg.height = a.height;
+    cfg.tile_width = a.tw;
+    cfg.tile_height = a.th;
+    if (a.gpus > 0) {
+      cfg.num_gpus = (uint32_t)a.gpus;
+      for (int k = 0; k < a.gpus && k < GS_MAX_GPUS; ++k) cfg.device_ids[k] = k;
+    }
+    splat::gs_check(gs_create(g.data(), g.size(), &cfg, &r_), "gs_create");
+  }
+  ~GpuDevice() { gs_destroy(r_); }
+  GpuDevice(const GpuDevice&) = delete;
+  GpuDevice& operator=(const GpuDevice&) = delete;
+
+  // splat.cpp:259-264: updateModelView, updateProjection, updateFocalLengths,
+  // execute, getFrameBuffer; getIPUHistogram (:222)
+  void frame(const Mat4& view, const Mat4& proj, float fov, float scale_div, std::vector<uint8_t>& bgr,
+             std::vector<uint32_t>& hist) {
+    splat::gs_check(gs_set_view(r_, transposed(view).m), "gs_set_view");
+    splat::gs_check(gs_set_projection(r_, transposed(proj).m), "gs_set_projection");
+    splat::gs_check(gs_set_focal(r_, fov, scale_div), "gs_set_focal");
+    splat::gs_check(gs_render(r_), "gs_render");
+    splat::gs_check(gs_read_bgr8(r_, bgr.data(), bgr.size()), "gs_read_bgr8");
+    gs_frame_stats st;
+    splat::gs_check(gs_get_stats(r_, &st), "gs_get_stats");
+    hist.assign(st.n_tiles, 0u);
+    splat::gs_check(gs_read_tile_histogram(r_, hist.data(), hist.size()), "gs_read_tile_histogram");
+    n_rendered = st.n_rendered;
+    n_pairs = st.n_pairs;
+  }
+  uint64_t n_rendered = 0, n_pairs = 0;
+
+ private:
+  gs_renderer* r_ = nullptr;
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -154,15 +225,12 @@ int main(int argc, char** argv) {
     usage();
     return EXIT_FAILURE;
   }
+#if !GSPLAT_REMOTE_UI
   if (a.ui_port != 0) {
-    std::fprintf(stderr, "Exiting after: remote UI (--ui-port) is not part of this build.\n");
+    std::fprintf(stderr, "Exiting after: this splat was built without the remote UI (make REMOTE_UI=1).\n");
     return EXIT_FAILURE;
   }
-  if (a.device != "gpu") {
-    std::fprintf(stderr, "Exiting after: --device %s is not supported (use --device gpu).\n",
-                 a.device.c_str());
-    return EXIT_FAILURE;
-  }
+#endif
   try {
     gs_ply* ply = nullptr;
     splat::gs_check(gs_ply_load(a.input.c_str(), &ply), "load");
@@ -173,31 +241,121 @@ int main(int argc, char** argv) {
     gs_ply_free(ply);
     if (log_on(a, "info")) {
       std::printf("[info] Total point count: %lld\n", (long long)n);
-      std::printf("[info] Point bounds (centred, z negated): (%g, %g, %g) -> (%g, %g, %g)\n", bb[0],
-                  bb[1], bb[2], bb[3], bb[4], bb[5]);
+      std::printf("[info] Point bounds (centred, z negated): (%g, %g, %g) -> (%g, %g, %g)\n", bb[0], bb[1],
+                  bb[2], bb[3], bb[4], bb[5]);
     }
-    splat::GpuFramebuffer fb{a.width, a.height, a.tw, a.th};
-    splat::GpuSplatter splatter(g, fb);
-    float view_rm[16], proj_rm[16];
-    const float fov = 40.0f * 0.01745329251994329576923690768489f;  // glm::radians(40.f)
-    splat::gs_check(gs_cam_headless(bb, a.width, a.height, fov, view_rm, proj_rm), "camera");
-    splat::gs_check(gs_set_view(splatter.handle(), view_rm), "view");
-    splat::gs_check(gs_set_projection(splatter.handle(), proj_rm), "projection");
-    splatter.updateFocalLengths(fov, a.scale_div);
-    std::vector<uint8_t> bgr;
-    for (int f = 0; f < a.frames; ++f) {
+    std::vector<float> xyz((size_t)n * 3);  // the points of the CPU path (pts[i].p)
+    for (int64_t i = 0; i < n; ++i)
+      for (int k = 0; k < 3; ++k) xyz[(size_t)i * 3 + k] = g[(size_t)i].mean[k];
+
+    const float aspect = a.width / (float)a.height;  // splat.cpp:107
+    // splat.cpp:186-195: modelView, eye-space bounds, fitted projection
+    Mat4 modelView, projection, dynamicView;
+    const float up[3] = {0.f, 1.f, 1.f};
+    splat::gs_check(gs_cam_look_at_bbox(bb, bb + 3, up, 1.f, modelView.m), "lookAtBoundingBox");
+    float bbCamMin[4], bbCamMax[4];
+    {
+      const float pmin[4] = {bb[0], bb[1], bb[2], 1.f}, pmax[4] = {bb[3], bb[4], bb[5], 1.f};
+      gs_mat4_mul_vec4(modelView.m, pmin, bbCamMin);
+      gs_mat4_mul_vec4(modelView.m, pmax, bbCamMax);
+    }
+#if GSPLAT_REMOTE_UI
+    using State = gsui::InterfaceServer::State;
+#else
+    struct State {
+      float envRotationDegrees = 0.f, envRotationDegrees2 = 0.f, X = 640.f, Y = 360.f, Z = 1.f, lambda1 = 1.f,
+            fov = 90.f;
+      std::string device = "cpu";
+      bool stop = false;
+    };
+#endif
+    State state;
+    state.fov = radians(40.f);  // splat.cpp:175
+    state.device = a.device;
+    if (a.scale_div > 0.f) state.lambda1 = a.scale_div * 10.f;
+#if GSPLAT_REMOTE_UI
+    std::unique_ptr<gsui::InterfaceServer> ui;
+    if (a.ui_port) {
+      ui.reset(new gsui::InterfaceServer(a.ui_port));
+      if (!ui->start(state)) throw std::runtime_error("remote UI server could not start");
+      ui->updateFov(state.fov);
+    }
+#endif
+    splat::gs_check(gs_cam_fit_frustum(bbCamMin, bbCamMax, state.fov, aspect, projection.m), "fitFrustum");
+    splat::gs_check(gs_cam_mvp_start(dynamicView.m), "mvpStart");  // splat.cpp:235-244
+
+    std::unique_ptr<GpuDevice> gpu;
+    const size_t px = (size_t)a.width * a.height;
+    std::vector<uint8_t> image(px * 3, 0), imageBuffered(px * 3, 0);
+    std::vector<uint32_t> hist, histBuffered;
+#if GSPLAT_REMOTE_UI
+    gsui::AsyncTask hostProcessing;
+#endif
+    double secondsElapsed = 0.0;
+    int frame = 0;
+    for (;;) {
       const auto t0 = std::chrono::steady_clock::now();
-      splatter.execute();
-      splatter.getFrameBuffer(bgr);
-      const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (log_on(a, "info")) {
-        const gs_frame_stats st = splatter.stats();
-        std::printf("[info] Splat time: %g points/sec: %g\n", secs, (double)n / secs);
-        std::printf("[info] Splatted point count: %llu (tile pairs %llu)\n",
-                    (unsigned long long)st.n_rendered, (unsigned long long)st.n_pairs);
+      std::fill(image.begin(), image.end(), (uint8_t)0);  // *imagePtr = 0 (splat.cpp:247)
+      uint32_t count = 0;
+      const float scaleDiv = state.lambda1 / 10.f;
+      if (state.device == "cpu") {
+        hist.assign((size_t)(a.width / a.tw) * (a.height / a.th), 0u);
+        splat::gs_check(gs_cpu_point_splat(xyz.data(), (size_t)n, transposed(dynamicView).m, transposed(projection).m,
+                                           a.width, a.height, a.tw, a.th, 25, image.data(), hist.data(), &count, 0),
+                        "splatPoints");
+      } else if (state.device == "gpu" || state.device == "ipu") {
+        if (!gpu) gpu.reset(new GpuDevice(g, a));
+        gpu->frame(dynamicView, projection, state.fov, scaleDiv, image, hist);
+        count = (uint32_t)gpu->n_rendered;
+      } else if (log_on(a, "warn")) {
+        std::printf("[warn] unknown device '%s': nothing rendered\n", state.device.c_str());
       }
+      const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      secondsElapsed += secs;
+      ++frame;
+#if GSPLAT_REMOTE_UI
+      if (ui) {
+        if (secondsElapsed > 3.0 && log_on(a, "info"))
+          std::printf("[info] Splat time: %g points/sec: %g\n", secs, (double)n / secs);
+        // splat.cpp:280-315
+        hostProcessing.waitForCompletion();
+        std::swap(image, imageBuffered);
+        std::swap(hist, histBuffered);
+        hostProcessing.run([&] {
+          ui->sendHistogram(histBuffered);
+          ui->sendPreviewImage(imageBuffered.data(), (int)a.width, (int)a.height);
+        });
+        state = ui->consumeState();
+        splat::gs_check(gs_cam_fit_frustum(bbCamMin, bbCamMax, state.fov, aspect, projection.m), "fitFrustum");
+        if (secondsElapsed >= 3.0) {
+          if (log_on(a, "info"))
+            std::printf("[info] envRotationDegrees: %f envRotationDegrees2: %f lambda1: %f fov: %f\n",
+                        state.envRotationDegrees, state.envRotationDegrees2, state.lambda1, state.fov);
+          secondsElapsed = 0.0;
+        }
+        Mat4 id, t;
+        for (int i = 0; i < 16; ++i) id.m[i] = (i % 5 == 0) ? 1.f : 0.f;
+        const float ax[3] = {1.f, 0.f, 0.f}, ay[3] = {0.f, 1.f, 0.f};
+        splat::gs_check(gs_cam_rotate(id.m, radians(state.envRotationDegrees), ax, t.m), "rotate");
+        splat::gs_check(gs_mat4_mul(modelView.m, t.m, dynamicView.m), "modelView * rotate");
+        splat::gs_check(gs_cam_rotate(dynamicView.m, radians(state.envRotationDegrees2), ay, t.m), "rotate");
+        const float tr[3] = {state.X / 50.f, state.Y / 50.f, -state.Z / 20.f + 20.f};
+        splat::gs_check(gs_cam_translate(t.m, tr, dynamicView.m), "translate");
+        if (state.stop) break;
+        continue;
+      }
+#endif
+      if (log_on(a, "info")) {
+        std::printf("[info] Splat time: %g points/sec: %g\n", secs, (double)n / secs);
+        std::printf("[info] Splatted point count: %u\n", count);
+      }
+      if (frame >= a.frames) break;
     }
-    if (!write_png(a.out, bgr.data(), a.width, a.height)) {
+#if GSPLAT_REMOTE_UI
+    hostProcessing.waitForCompletion();
+    if (ui) std::swap(image, imageBuffered);  // the last rendered frame
+#endif
+    if (!write_png(a.out, image.data(), a.width, a.height)) {
       std::fprintf(stderr, "could not write %s\n", a.out.c_str());
       return EXIT_FAILURE;
     }

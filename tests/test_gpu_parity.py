@@ -498,8 +498,13 @@ def test_render_server_cli(built, tmp_path):
     view, proj = camera.headless(bb, 1280, 720)
     ref = O.render(g, O.make_frame(view, proj, 1280, 720, 32, 20, camera.FOV_DEFAULT, 0.1))
     np.testing.assert_array_equal(raw[:, :, ::-1], ref["bgr"])
-    bad = subprocess.run([exe, "--input", PC12, "--ui-port", "5000"], capture_output=True, text=True)
-    assert bad.returncode != 0 and "remote UI" in bad.stderr
+    # the same frame through a row-band group (--gpus 1: gs_create with
+    # num_gpus, one RCCL all-gather per frame inside gs_render)
+    out2 = tmp_path / "test2.png"
+    r = subprocess.run([exe, "--input", PC12, "--device", "gpu", "--gpus", "1", "--out", str(out2)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert out2.read_bytes() == data
 
 
 @pytest.mark.parametrize("half_width,log_scale,planes", [
