@@ -1198,14 +1198,14 @@ __device__ __forceinline__ bool write_tied_list(const Buffers& b, uint32_t s, ui
 // rolled network, one copy for every E (the hot unrolled networks stay
 // compact in the instruction cache: a copy per E inside them doubled the
 // kernel's code and cost the isolated sort 13 us).
-__device__ __forceinline__ void wave_sort_tile_input(const Buffers& b, uint32_t s, uint32_t L,
-                                                               int lane) {
+__device__ __forceinline__ void wave_sort_tile_input(const Buffers& b, const unsigned long long* src,
+                                                     uint32_t s, uint32_t L, int lane) {
   constexpr int E = 4;  // L <= kSortRegCap = 256
   unsigned long long v[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const uint32_t i = (uint32_t)(lane * E + e);
-    v[e] = i < L ? rekey_input(b, b.pairs[s + i]) : ~0ull;
+    v[e] = i < L ? rekey_input(b, src[i]) : ~0ull;
   }
   for (int k = 2; k <= 64 * E; k <<= 1) wave_merge<E>(v, lane, 0, k, k >> 1);
 #pragma unroll
@@ -1215,16 +1215,17 @@ __device__ __forceinline__ void wave_sort_tile_input(const Buffers& b, uint32_t 
   }
 }
 
-// Returns false (nothing written; the sorted keys are left in slice[0, L))
-// when the list has equal depths.
+// Sorts the keys src[0, L) and writes the list at list[s, s + L).  Returns
+// false (nothing written; the sorted keys are left in slice[0, L)) when the
+// list has equal depths.
 template <int E>
-__device__ __forceinline__ bool wave_sort_tile(const Buffers& b, uint32_t s, uint32_t L, int lane,
-                                               unsigned long long* slice) {
+__device__ __forceinline__ bool wave_sort_tile(const Buffers& b, const unsigned long long* src, uint32_t s,
+                                               uint32_t L, int lane, unsigned long long* slice) {
   unsigned long long v[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const uint32_t i = (uint32_t)(lane * E + e);
-    v[e] = i < L ? b.pairs[s + i] : ~0ull;
+    v[e] = i < L ? src[i] : ~0ull;
   }
   wave_bitonic<E>(v, lane);
   // key i - 1 of key i: this lane's previous register, or lane - 1's last
@@ -1507,6 +1508,29 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
   radix_sort_seg<NT, KPL, false>(b, s, L, hist, base, wcnt);
 }
 
+// One wave sorts a list of L <= kSortRegCap keys src[0, L) in registers and
+// writes it at list[s, s + L) (equal depths: see write_tied_list).
+__device__ __forceinline__ void wave_sort_list(const Buffers& b, const unsigned long long* src, uint32_t s,
+                                               uint32_t L, int lane, unsigned long long* slice) {
+  bool done;
+  if (L <= 64u)
+    done = wave_sort_tile<1>(b, src, s, L, lane, slice);
+  else if (L <= 128u)
+    done = wave_sort_tile<2>(b, src, s, L, lane, slice);
+  else
+    done = wave_sort_tile<4>(b, src, s, L, lane, slice);
+  if (!done) {  // equal depths (wave-uniform)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool longrun = write_tied_list(b, s, L, slice, (uint32_t)lane, 64u);
+    if (ballot64(longrun) != 0ull) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // after the stores above
+      wave_sort_tile_input(b, src, s, L, lane);
+    }
+  }
+}
+
 // Big, medium and small lists in one launch, longest first: workgroups
 // [0, n_big) radix-sort one big list each (> kSortLdsCap); the next n_medium
 // each sort one medium list (kSortRegCap < L <= kSortLdsCap, merge_sort_tile);
@@ -1555,23 +1579,7 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   // equal depths
   static_assert(NW * kSortRegCap <= kWords / 2, "small-list slices fit the merge buffer");
   unsigned long long* const slice = keys + wave * kSortRegCap;
-  bool done;
-  if (L <= 64u)
-    done = wave_sort_tile<1>(b, s, L, lane, slice);
-  else if (L <= 128u)
-    done = wave_sort_tile<2>(b, s, L, lane, slice);
-  else
-    done = wave_sort_tile<4>(b, s, L, lane, slice);
-  if (!done) {  // equal depths (wave-uniform)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const bool longrun = write_tied_list(b, s, L, slice, (uint32_t)lane, 64u);
-    if (ballot64(longrun) != 0ull) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // after the stores above
-      wave_sort_tile_input(b, s, L, lane);
-    }
-  }
+  wave_sort_list(b, b.pairs + s, s, L, lane, slice);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {

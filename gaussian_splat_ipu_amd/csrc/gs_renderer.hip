@@ -89,7 +89,7 @@ std::vector<uint32_t> morton_order(const gs_gaussian3d* g, size_t n, bool keep) 
 int alloc_pairs(gs_renderer* r, uint64_t cap) {
   free_pairs(r);
   // + one u32 per 2048-key work item a big list can have, and the big-list
-  // sample sort's bucket tables (one bucket per ~1024 keys)
+  // sample sort's bucket tables (one bucket per ~1024 keys, gs_kernels.hip kBktAvg)
   const size_t n_items = (size_t)(cap / 2048) + (size_t)r->n_tiles + 1;
   const size_t n_bk = (size_t)(cap / 1024) + (size_t)r->n_tiles + 1;
   const size_t bytes = (size_t)cap * (8 + 8 + 4) + n_bk * 8 + n_items * 4 + n_bk * 12 +
@@ -178,6 +178,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
   fp.pair_cap = r->pair_cap;
+
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
   fp.bin_global = r->bin_global;
@@ -648,6 +649,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
     bb.footer = nullptr;  // (a group's all-gather slot belongs to the frame)
     for (int attempt = 0; attempt < 8; ++attempt) {
       fp.pair_cap = r->pair_cap;
+
       bb.pairs = r->buf.pairs;
       bb.pairs_alt = r->buf.pairs_alt;
       bb.list = r->buf.list;
