@@ -66,6 +66,7 @@ struct gs_renderer {
   void* d_pairs = nullptr;      // pairs, pairs_alt, list
   void* d_out = nullptr;        // rgba f32 + bgr8
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
+  void* d_lazy = nullptr;       // lazy big lists (16x16 tiles): per-tile tables + saved blend waves
   int bin_global = 0, chunk_size = 0, n_chunks = 0;
   bool pair_cull = false;       // chunked binning into the alpha-box tiles only
   size_t zero_bytes = 0;

@@ -871,6 +871,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
       if (cl == 0) b.small_tiles[pq[0] + (uint32_t)__popcll(m0 & lt)] = (uint32_t)t;
       if (cl == 1) b.medium_tiles[pq[1] + (uint32_t)__popcll(m1 & lt)] = (uint32_t)t;
       if (cl == 2) b.big_tiles[pq[2] + (uint32_t)__popcll(m2 & lt)] = (uint32_t)t;
+      if (b.tile_big) b.tile_big[t] = cl == 2 ? pq[2] + (uint32_t)__popcll(m2 & lt) : 0xFFFFFFFFu;
     }
   }
   if (g == 0) {  // frame counters (every counter of the frame is reset here)
@@ -1602,6 +1603,8 @@ constexpr int kBigSeg = 2048;
 // sample sort of the big lists: buckets of ~kBktAvg keys, at most kBktMax
 // per list (their splitters are staged in LDS)
 constexpr uint32_t kBktAvg = 1024, kBktMax = 2048;
+// lazy big lists: the sorted prefix holds ~this many keys (see gs_big_select_kernel)
+constexpr uint32_t kLazyPrefix = 1536;
 __device__ __forceinline__ uint32_t big_buckets(uint32_t L) {
   return min(kBktMax, (L + kBktAvg - 1u) / kBktAvg);
 }
@@ -1620,9 +1623,17 @@ __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buf
     if (j < n_big) {
       uint32_t s, L;
       tile_segment(fp, b, (int)b.big_tiles[j], s, L);
-      c = (L + kBigSeg - 1) / kBigSeg;
-      nb = big_buckets(L);
-      maxl = max(maxl, L);
+      // pass 1 (lazy frames): only the lists whose blend outlived the prefix
+      const bool use = fp.big_pass == 0 || b.big_flag[j] != 0u;
+      c = use ? (L + kBigSeg - 1) / kBigSeg : 0u;
+      nb = use ? big_buckets(L) : 0u;
+      maxl = use ? max(maxl, L) : maxl;
+      if (fp.lazy && fp.big_pass == 0) {
+        b.big_flag[j] = 0u;
+        b.big_cnt[j] = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b.cont_flag[4 * j + q] = 0u;
+      }
     }
     uint32_t inc = c, inc_b = nb;
     for (int d = 1; d < 64; d <<= 1) {
@@ -1690,22 +1701,113 @@ __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffe
   __shared__ unsigned long long keys[kSortLdsCap];
   const uint32_t n_big = b.counters[0];
   const uint32_t tid = threadIdx.x;
+  const bool bound = fp.lazy && fp.big_pass == 0;
   for (uint32_t j = blockIdx.x; j < n_big; j += gridDim.x) {
+    if (fp.big_pass == 1 && b.big_flag[j] == 0u) continue;  // (uniform)
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t B = big_buckets(L), bo = b.bk_off[j];
-    const uint32_t S = min((uint32_t)kSortLdsCap, 16u * B);  // sample size
+    const uint32_t S = bound ? min((uint32_t)kSortLdsCap, L) : min((uint32_t)kSortLdsCap, 16u * B);  // sample size
     for (uint32_t k = tid; k < S; k += 256u) {
       const uint32_t p = (uint32_t)(((2ull * k + 1ull) * L) / (2ull * S));
       keys[k] = b.pairs[s + p];
     }
     __syncthreads();
     merge_sort_tile<256, 2, kOutLds, kSrcLds>(b, 0u, S, keys);
+    if (bound) {
+      // the prefix: keys of lower depth than the sample's kLazyPrefix / L
+      // quantile (~kLazyPrefix keys; more than kSortLdsCap sends the whole
+      // list to the continuation)
+      if (tid == 0u) {
+        const uint32_t q = (uint32_t)(((unsigned long long)kLazyPrefix * S) / L);
+        b.big_thr[j] = (uint32_t)(keys[min(q, S - 1u)] >> 32);
+      }
+      __syncthreads();
+      continue;
+    }
     for (uint32_t t = tid; t < B; t += 256u) {
       if (t + 1u < B) b.bk_spl[bo + t] = keys[((unsigned long long)(t + 1u) * S) / B - 1u];
       b.bk_cnt[bo + t] = 0u;
       b.bk_list[bo + t] = j;
     }
+    __syncthreads();
+  }
+}
+
+// ---- lazy big lists (FrameParams::lazy): the blend rarely needs more than
+// the nearest ~2 k keys of a big list -- a tile's pixels saturate (the
+// reference's `break`) after a few hundred records in front (config 5: 6.5 %
+// of the big-list keys are ever composited).  So before the blend only each
+// list's prefix of keys below a depth bound is sorted (split: the bound from
+// the sample; select: the keys below it; psort: one workgroup sorts them into
+// the list).  A blend wave that reaches the end of the prefix with live pixels
+// saves their state and flags the list; after the blend the flagged lists are
+// sorted in full by the sample sort (big_pass 1) and the saved waves continue
+// from the prefix's end (blend_cont).  Every key below the bound precedes
+// every other in the total order (ties share a depth, so they share a side),
+// so each pixel composites exactly the list's records in order: the frame is
+// the same bit for bit.
+// one workgroup per 2048-key work item (pass 0: every big list): append the
+// item's keys below the list's bound to the list's prefix (pairs_alt[s, ...))
+__global__ __launch_bounds__(256) void gs_big_select_kernel(FrameParams fp, Buffers b) {
+  __shared__ uint32_t s_par[5];
+  __shared__ uint32_t s_n, s_base;
+  const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
+  const uint32_t tid = threadIdx.x;
+  constexpr int Q = kBigSeg / 256;
+  for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
+    if (tid == 0) {
+      uint32_t j, c;
+      big_item(b, n_big, k, j, c);
+      uint32_t s, L;
+      tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+      s_par[0] = s;
+      s_par[1] = L;
+      s_par[2] = c;
+      s_par[3] = b.big_thr[j];
+      s_par[4] = j;
+      s_n = 0u;
+    }
+    __syncthreads();
+    const uint32_t s = s_par[0], L = s_par[1], c = s_par[2], thr = s_par[3], j = s_par[4];
+    unsigned long long key[Q];
+    uint32_t rk[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
+      key[q] = i < L ? b.pairs[s + i] : ~0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
+      rk[q] = (i < L && (uint32_t)(key[q] >> 32) < thr) ? atomicAdd(&s_n, 1u) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    if (tid == 0) s_base = s_n ? atomicAdd(&b.big_cnt[j], s_n) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t pos = s_base + rk[q];
+      if (rk[q] != 0xFFFFFFFFu && pos < (uint32_t)kSortLdsCap) b.pairs_alt[s + pos] = key[q];
+    }
+    __syncthreads();
+  }
+}
+
+// one workgroup per big list (grid-stride): sort its prefix into list[s, s + n)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_psort_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long keys[kSortLdsCap];
+  const uint32_t n_big = b.counters[0];
+  for (uint32_t j = blockIdx.x; j < n_big; j += gridDim.x) {
+    uint32_t s, L;
+    tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+    const uint32_t n = b.big_cnt[j];
+    const bool ok = n > 0u && n <= (uint32_t)kSortLdsCap;  // else: all of it in the continuation
+    if (ok && !merge_sort_tile<256, 2, kOutDevice, kSrcAlt>(b, s, n, keys)) {
+      __syncthreads();  // a long run of equal depths: again with input-index keys
+      merge_sort_tile<256, 2, kOutInput, kSrcAltRekey>(b, s, n, keys);
+    }
+    if (threadIdx.x == 0) b.big_len[j] = ok ? n : 0u;
     __syncthreads();
   }
 }
@@ -1802,6 +1904,7 @@ __global__ __launch_bounds__(256) void gs_big_bscan_kernel(FrameParams fp, Buffe
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * 4u;
   for (uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6); j < n_big; j += nw) {
+    if (fp.big_pass == 1 && b.big_flag[j] == 0u) continue;  // (wave-uniform)
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t B = big_buckets(L), bo = b.bk_off[j];
@@ -1986,13 +2089,22 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
   if (slot >= fp.n_tiles) return;
+  // lazy big lists: jb = the tile's big-list slot.  The continuation's waves
+  // are (slot, chunk) of the flagged lists whose state was saved.
+  uint32_t jb = 0xFFFFFFFFu;
+  if (fp.blend_cont) {
+    if ((uint32_t)slot >= b.counters[0] || b.cont_flag[4 * slot + chunk] == 0u) return;
+    jb = (uint32_t)slot;
+  }
   // row bands: longest lists first (the sort queues: big, medium, then small
   // and empty tiles), so the heaviest tiles' waves start at once instead of
   // where the tile order puts them (8 bands: blend 35.7 -> 29.3 us).  The
   // full frame keeps the tile order (neighbouring tiles share records in L2:
   // 75.1 against 76.1 us in queue order).
   int tile = slot;
-  if (fp.blend_lpt) {
+  if (fp.blend_cont) {
+    tile = (int)b.big_tiles[jb];
+  } else if (fp.blend_lpt) {
     const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
     tile = (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
   }
@@ -2041,7 +2153,25 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
 
   uint32_t s, L;
   tile_segment(fp, b, tile, s, L);
-  const uint32_t* __restrict__ list = b.list + s;
+  // lazy big list: this pass composites the sorted prefix [0, big_len), the
+  // continuation the rest [big_len, L) from the saved state
+  uint32_t k0 = 0u, Lfull = L;
+  if (fp.lazy && !fp.blend_cont) jb = b.tile_big[tile];
+  if (jb != 0xFFFFFFFFu) {
+    const uint32_t np = min(b.big_len[jb], L);
+    if (fp.blend_cont) {
+      k0 = np;
+      float* sv = b.cont_state + (size_t)(4 * jb + chunk) * 6 * 64 + lane;
+      q.T = sv[0];
+      q.c01 = f32x2{sv[64], sv[128]};
+      q.c23 = f32x2{sv[192], sv[256]};
+      q.done = sv[320] != 0.0f;
+    } else {
+      L = np;
+    }
+  }
+  const uint32_t* __restrict__ list = b.list + s + k0;
+  L -= k0;
 
   // wave-private staging of one batch of 64 records (48 B each) in LDS
   __shared__ float4 s_rec[GS_BLEND_WPG][3][64];
@@ -2148,6 +2278,21 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
   }
+  if (jb != 0xFFFFFFFFu && !fp.blend_cont && L < Lfull && ballot64(!q.done) != 0ull) {
+    // the prefix ended with live pixels: save the wave's state, flag the list
+    float* sv = b.cont_state + (size_t)(4 * jb + chunk) * 6 * 64 + lane;
+    sv[0] = q.T;
+    sv[64] = q.c01.x;
+    sv[128] = q.c01.y;
+    sv[192] = q.c23.x;
+    sv[256] = q.c23.y;
+    sv[320] = q.done ? 1.0f : 0.0f;
+    if (lane == 0) {
+      b.cont_flag[4 * jb + chunk] = 1u;
+      b.big_flag[jb] = 1u;
+    }
+    return;  // the continuation stores these pixels
+  }
   if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
 
@@ -2196,19 +2341,29 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   gs_emit_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
 }
 
+// the sample sort's bucket passes (every big list, or the flagged ones)
+void launch_big_buckets(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  const unsigned grid = 4096;
+  gs_big_count_kernel<<<grid, 256, 0, s>>>(fp, b);
+  gs_big_bscan_kernel<<<256, 256, 0, s>>>(fp, b);
+  gs_big_scatter_kernel<<<grid, 256, 0, s>>>(fp, b);
+  gs_big_bsort_kernel<<<grid, 256, 0, s>>>(fp, b);
+}
+
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
   if (fp.big_separate) {
     // work items = 2048-key segments of the big lists; the passes run until a
     // run covers the longest list the pair buffer can hold (passes after a
     // list's last one skip it)
-    const unsigned grid = 4096;
     gs_big_prefix_kernel<<<1, 1024, 0, s>>>(fp, b);
     gs_big_split_kernel<<<1024, 256, 0, s>>>(fp, b);
-    gs_big_count_kernel<<<grid, 256, 0, s>>>(fp, b);
-    gs_big_bscan_kernel<<<256, 256, 0, s>>>(fp, b);
-    gs_big_scatter_kernel<<<grid, 256, 0, s>>>(fp, b);
-    gs_big_bsort_kernel<<<grid, 256, 0, s>>>(fp, b);
+    if (fp.lazy) {  // only the prefixes now; the rest after the blend (launch_blend)
+      gs_big_select_kernel<<<4096, 256, 0, s>>>(fp, b);
+      gs_big_psort_kernel<<<2048, 256, 0, s>>>(fp, b);
+    } else {
+      launch_big_buckets(fp, b, s);
+    }
   }
   // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
@@ -2225,6 +2380,17 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     gs_blend_kernel<8><<<grid, block, 0, s>>>(fp, b);
   else
     gs_blend_kernel<0><<<grid, block, 0, s>>>(fp, b);
+  if (fp.lazy) {
+    // the big lists whose blend outlived the prefix: sorted in full, then
+    // their saved waves continue (nothing to do when none was flagged)
+    FrameParams f1 = fp;
+    f1.big_pass = 1;
+    gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f1, b);
+    gs_big_split_kernel<<<1024, 256, 0, s>>>(f1, b);
+    launch_big_buckets(f1, b, s);
+    f1.blend_cont = 1;
+    gs_blend_kernel<4><<<grid, block, 0, s>>>(f1, b);
+  }
 }
 
 }  // namespace gsk

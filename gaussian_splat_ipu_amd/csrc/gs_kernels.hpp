@@ -43,6 +43,10 @@ struct FrameParams {
   int pair_cull;      // bin only the tiles the alpha box meets (crect); the
                       // reference list lengths are counted alongside
   int big_separate;   // big lists sorted by gs_sort_big_kernel (launched before the tile sort)
+  int lazy;           // big lists: only their nearest keys are sorted before the blend; the
+                      //   blocks whose pixels outlive that prefix continue after a full sort
+  int big_pass;       // big-list kernels: 0 = every big list, 1 = the lists flagged by the blend
+  int blend_cont;     // blend: 1 = the continuation of the flagged big-list blocks
   int pow2;           // tile size, band stride and fxy[1] are powers of two: the
                       // projection divides by them with exact multiplies / shifts
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)
@@ -100,6 +104,14 @@ struct Buffers {
   // outputs
   float4* rgba;             // band_rows x width, row-major
   uint8_t* bgr;             // band rows (padded) x width x 3
+  // lazy big lists (FrameParams::lazy); all per tile / per big-list slot
+  uint32_t* tile_big;       // [n_tiles] big-list slot of a tile (~0: not a big list)
+  uint32_t* big_len;        // [n_tiles] keys sorted before the blend (the prefix)
+  uint32_t* big_thr;        // [n_tiles] the prefix's depth bound (keys of lower depth)
+  uint32_t* big_cnt;        // [n_tiles] keys below the bound
+  uint32_t* big_flag;       // [n_tiles] 1: a pixel outlived the prefix (continuation)
+  uint32_t* cont_flag;      // [n_tiles * 4] per slot and blend wave: its state is saved
+  float* cont_state;        // [n_tiles * 4 * 6 * 64] T, colour, done of the saved waves
   uint32_t* footer;         // row-band group: counters[16] + reference list lengths[n_tiles]
                             //   of this frame, next to its BGR8 band in the all-gather slot
                             //   (written by the chunked scan; nullptr = none)

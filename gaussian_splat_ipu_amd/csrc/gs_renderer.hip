@@ -118,7 +118,7 @@ void release(gs_renderer* r) {
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
-  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk})
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy})
     if (p) (void)hipFree(p);
   free_pairs(r);
   if (r->h_counters) (void)hipHostFree(r->h_counters);
@@ -178,7 +178,6 @@ gsk::FrameParams make_params(const gs_renderer* r) {
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
   fp.pair_cap = r->pair_cap;
-
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
   fp.bin_global = r->bin_global;
@@ -190,6 +189,15 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // big lists (a hint read from the mapped counters: either choice sorts
   // every list, the other launch handles them otherwise)
   fp.big_separate = (r->h_counters && ((volatile const uint32_t*)r->h_counters)[0] > 0) ? 1 : 0;
+  // lazy big lists: sort only the lists' nearest keys before the blend
+  // (GSPLAT_LAZY=0 sorts every big list in full first)
+  {
+    static const bool lazy_env = !(std::getenv("GSPLAT_LAZY") && std::strcmp(std::getenv("GSPLAT_LAZY"), "0") == 0);
+    fp.lazy = (fp.big_separate && lazy_env && r->d_lazy && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 &&
+               !r->bin_global && r->n_chunks > 0) ? 1 : 0;
+  }
+  fp.big_pass = 0;
+  fp.blend_cont = 0;
   {
     auto log2_exact = [](double v, int& sh) -> bool {  // v == 2^sh, sh in [-126, 126]
       int e = 0;
@@ -500,6 +508,24 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   }
   r->stats.bin_global = (uint32_t)r->bin_global;
 
+  // lazy big lists (gs_kernels.hip, kLazyPrefix): with the chunked binning
+  // and 16x16 tiles (four 8x8 blend waves per tile); per tile 9 u32 + the
+  // saved state of 4 waves (6 x 64 floats each)
+  if (!r->bin_global && r->n_chunks > 0 && cfg->tile_width == 16 && cfg->tile_height == 16) {
+    const size_t TT = (size_t)r->t_cap;
+    if ((e = hipMalloc(&r->d_lazy, TT * (9 * 4 + 4 * 6 * 64 * 4))) != hipSuccess)
+      return fail(hip_fail(e, "hipMalloc(lazy big lists)"));
+    uint32_t* u = (uint32_t*)r->d_lazy;
+    r->buf.tile_big = u;
+    r->buf.big_len = u + TT;
+    r->buf.big_thr = u + 2 * TT;
+    r->buf.big_cnt = u + 3 * TT;
+    r->buf.big_flag = u + 4 * TT;
+    r->buf.cont_flag = u + 5 * TT;  // 4 per slot: [5 T, 9 T)
+    r->buf.cont_state = (float*)(u + 9 * TT);
+    if ((e = hipMemset(r->d_lazy, 0, TT * 9 * 4)) != hipSuccess) return fail(hip_fail(e, "hipMemset(lazy)"));
+  }
+
   uint64_t cap = cfg->pair_capacity;
   if (cap == 0) cap = std::max<uint64_t>(1u << 20, 8ull * n);
   cap = std::min<uint64_t>(cap, 0xFFFFFFF0ull);
@@ -649,7 +675,6 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
     bb.footer = nullptr;  // (a group's all-gather slot belongs to the frame)
     for (int attempt = 0; attempt < 8; ++attempt) {
       fp.pair_cap = r->pair_cap;
-
       bb.pairs = r->buf.pairs;
       bb.pairs_alt = r->buf.pairs_alt;
       bb.list = r->buf.list;
@@ -660,6 +685,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
       bb.bk_list = r->buf.bk_list;
       bb.bk_off = r->buf.bk_off;
       fp.big_separate = 0;  // the tile sort radix-sorts big lists itself
+      fp.lazy = 0;
       if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
         GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, r->stream));
       gsk::launch_project(fp, bb, r->stream);
