@@ -299,10 +299,12 @@ def test_lazy_big_lists_continuation(built, op_lo, op_hi):
     W, H = 1920, 1080
     view, proj = camera.headless(bb, W, H)
     s = _splatter(g, view, proj, W, H, 16)
-    s.execute()
-    s.execute()  # with the big-list hint: lazy prefixes + continuation
     f = O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0)
     ref = O.render(g, f)
+    s.execute()
+    s.execute()  # with the big-list hint: lazy prefixes + continuation
     assert s.stats()["n_big_tiles"] > 10
+    _check_frame(s, g, f, ref, lists=False)
+    s.execute()  # the lists that continued are now sorted in full up front
     _check_frame(s, g, f, ref, lists=False)
     s.close()
