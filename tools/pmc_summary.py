@@ -57,7 +57,7 @@ def main():
     a = ap.parse_args()
     if a.config is None:
         keys = set()
-        for f in glob.glob(os.path.join(a.dir, "*.log")) + glob.glob(os.path.join(os.path.dirname(a.dir.rstrip("/")), "*.log")):
+        for f in glob.glob(os.path.join(a.dir, "*.log")):
             for line in open(f, errors="replace"):
                 if line.startswith("{") and '"pmc_key"' in line:
                     keys.add(json.loads(line)["config"]["pmc_key"])

@@ -1,10 +1,11 @@
 #!/bin/bash
-# rocprofv3 passes on the headline bench: kernel trace + stats, then PMC
-# counters in separate passes (never combined with other trace domains).
-#   PASSES="stats fetch write sq1 sq2" (default all)  STEPS=20
+# rocprofv3 passes on the bench: kernel trace + stats, then PMC counters in
+# separate passes (never combined with other trace domains).
+#   NAME=c3 BENCH_ARGS="--inflight 1" PASSES="stats fetch write sq1 sq2" STEPS=20
+# Outputs: gpurun_out/prof_$NAME/<pass>/..., gpurun_out/prof_$NAME/<pass>.log
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=gpurun_out/prof_${NAME:-c3}
 mkdir -p $OUT
 BENCH="bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-}"
 run() {  # run <name> <timeout> <rocprof args...>
@@ -12,7 +13,7 @@ run() {  # run <name> <timeout> <rocprof args...>
   echo "== $name"
   timeout -k 10 "$t" rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $BENCH > $OUT/$name.log 2>&1
   local rc=$?
-  echo "== $name rc=$rc"; grep -h '"metric"' $OUT/$name.log | cut -c1-200
+  echo "== $name rc=$rc"; grep -h '"metric"' $OUT/$name.log | cut -c1-160
   if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; exit $rc; fi
 }
 for p in ${PASSES:-stats fetch write sq1 sq2}; do
