@@ -20,8 +20,11 @@
 //
 // Frames in flight: F band renderers per device take frames round-robin, each
 // on its own stream; the all-gathers run in frame order on one communication
-// stream per device.  Enqueueing frame k waits (host) for the footers of frame
-// k - F, which bounds the pipeline at F frames and feeds the re-balancing.
+// stream per device.  gs_render_async never waits: the split is re-balanced
+// every kRebalanceEvery frames from the footers of the frame half that many
+// frames back (copied to the host when it was enqueued), the same frame on
+// every rank; gs_sync (and so a blocking gs_render) re-balances from the last
+// frame.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -46,6 +49,7 @@ namespace {
 
 constexpr double kTileCost = 64.0;   // fixed work per tile of a row (dist.row_work)
 constexpr double kRebalanceGain = 0.97;  // switch splits only if the slowest band gains > 3 %
+constexpr uint64_t kRebalanceEvery = 8;  // frames between re-balancing decisions
 constexpr int kMaxInFlight = 8;
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -123,7 +127,6 @@ struct Member {
 
 struct SlotInfo {
   bool used = false;
-  bool footers_read = false;
   bool gather_timed = false;
   uint64_t frame = 0;
   std::vector<uint32_t> bounds;  // world + 1 tile-row bounds of the frame
@@ -146,13 +149,15 @@ struct Group {
   std::vector<Member> mem;
   std::vector<uint32_t> bounds;  // split of the next frame
   std::vector<SlotInfo> sinfo;
-  uint32_t* h_foot = nullptr;    // pinned: F x world x foot_words
-  std::vector<hipEvent_t> ev_foot, ev_g0, ev_g1;  // on mem[0].comm_stream
+  uint32_t* h_snap = nullptr;    // pinned: world x foot_words, a frame's footers for re-balancing
+  uint32_t* h_last = nullptr;    // pinned: world x foot_words, the last frame's (read at sync)
+  hipEvent_t ev_snap = nullptr;  // the snapshot's copy is done (mem[0].comm_stream)
+  bool snap_pending = false;
+  std::vector<uint32_t> snap_bounds;
+  std::vector<hipEvent_t> ev_g0, ev_g1;  // per slot, on mem[0].comm_stream
   uint64_t frame = 0;
   int last_slot = -1;
-  uint64_t newest_read = 0;
-  bool have_read = false;
-  bool overflow_seen = false;
+  bool last_read = false;
   float view[16], proj[16];
   float fov = 0.6981317f, sd = 0.1f;
   // the last frame whose footers were read
@@ -208,62 +213,32 @@ int nccl_fail(ncclResult_t r, const char* what) {
     if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
   } while (0)
 
-// Footers of the frame in slot i (its all-gather is complete once ev_foot[i]
-// fired): overflow, the whole frame's histogram and stats, and -- for the
-// newest frame read -- the next split.
-int read_footers(Group* g, int i) {
-  SlotInfo& si = g->sinfo[i];
-  if (!si.used || si.footers_read) return GS_OK;
-  int rc = set_dev(g->mem[0].device);
-  if (rc != GS_OK) return rc;
-  GS_HIP(hipEventSynchronize(g->ev_foot[i]));
-  si.footers_read = true;
-  if (si.gather_timed) {
-    float ms = 0.0f;
-    GS_HIP(hipEventElapsedTime(&ms, g->ev_g0[i], g->ev_g1[i]));
-    g->g_ms += ms;
-    g->g_n += 1;
-    si.gather_timed = false;
-  }
+// The footers of one gathered frame (world x foot_words at h, the frame's
+// split `bounds`): the whole frame's histogram and, with `stats`, its stats
+// (kept for gs_get_stats / gs_read_tile_histogram); with `split`, the next
+// split.  Returns whether a band overflowed.
+bool parse_footers(Group* g, const uint32_t* h, const std::vector<uint32_t>& bounds, bool stats, bool split) {
   const bool chunked = !g->mem[0].slot[0]->bin_global && g->mem[0].slot[0]->n_chunks > 0;
   bool ovf = false;
   uint64_t P = 0, Pb = 0, V = 0, nbig = 0;
   std::vector<uint32_t> hist((size_t)g->T, 0u);
   for (int r = 0; r < g->world; ++r) {
-    const uint32_t* f = g->h_foot + ((size_t)i * g->world + r) * g->foot_words;
+    const uint32_t* f = h + (size_t)r * g->foot_words;
     ovf = ovf || f[3] != 0;
     const uint64_t pb = (uint64_t)f[5] | ((uint64_t)f[6] << 32);
     Pb += pb;
     P += chunked ? ((uint64_t)f[10] | ((uint64_t)f[11] << 32)) : pb;
     V = std::max<uint64_t>(V, f[2]);
     nbig += f[0];
-    const size_t t0 = (size_t)si.bounds[r] * g->tiles_x, t1 = (size_t)si.bounds[r + 1] * g->tiles_x;
+    const size_t t0 = (size_t)bounds[r] * g->tiles_x, t1 = (size_t)bounds[r + 1] * g->tiles_x;
     std::memcpy(hist.data() + t0, f + 16, (t1 - t0) * 4);
   }
-  if (ovf) g->overflow_seen = true;
-  if (g->have_read && si.frame < g->newest_read) return GS_OK;
-  g->have_read = true;
-  g->newest_read = si.frame;
-  uint32_t mx = 0;
-  for (uint32_t v : hist) mx = std::max(mx, v);
-  {
-    std::lock_guard<std::mutex> lk(g->hist_mu);
-    g->hist.swap(hist);
-    g->stats.n_rendered = V;
-    g->stats.n_pairs = P;
-    g->stats.n_pairs_binned = Pb;
-    g->stats.max_list = mx;
-    g->stats.n_big_tiles = (uint32_t)nbig;
-  }
-  if (g->rebalance && g->world > 1 && !ovf) {
+  if (split && g->rebalance && g->world > 1 && !ovf) {
     std::vector<double> w((size_t)g->tiles_y, 0.0);
-    {
-      std::lock_guard<std::mutex> lk(g->hist_mu);
-      for (int y = 0; y < g->tiles_y; ++y) {
-        double s = 0.0;
-        for (int x = 0; x < g->tiles_x; ++x) s += g->hist[(size_t)y * g->tiles_x + x];
-        w[y] = s + kTileCost * g->tiles_x;
-      }
+    for (int y = 0; y < g->tiles_y; ++y) {
+      double sum = 0.0;
+      for (int x = 0; x < g->tiles_x; ++x) sum += hist[(size_t)y * g->tiles_x + x];
+      w[y] = sum + kTileCost * g->tiles_x;
     }
     std::vector<uint32_t> nb((size_t)g->world + 1);
     balanced_bands(w.data(), g->tiles_y, g->world, nb.data());
@@ -272,14 +247,53 @@ int read_footers(Group* g, int i) {
       g->rebalances += 1;
     }
   }
+  if (stats) {
+    uint32_t mx = 0;
+    for (uint32_t v : hist) mx = std::max(mx, v);
+    std::lock_guard<std::mutex> lk(g->hist_mu);
+    g->hist.swap(hist);
+    g->stats.n_rendered = V;
+    g->stats.n_pairs = P;
+    g->stats.n_pairs_binned = Pb;
+    g->stats.max_list = mx;
+    g->stats.n_big_tiles = (uint32_t)nbig;
+  }
+  return ovf;
+}
+
+// every band's footer of the frame in slot i -> h (one strided copy on s)
+int copy_footers(Group* g, int i, uint32_t* h, hipStream_t s, bool async) {
+  const SlotInfo& si = g->sinfo[i];
+  const uint8_t* src = g->mem[0].d_recv + (size_t)i * g->world * g->slot_cap + si.bgr_part;
+  const size_t width = (16 + (size_t)si.pad_rows * g->tiles_x) * 4;
+  if (async)
+    GS_HIP(hipMemcpy2DAsync(h, g->foot_words * 4, src, si.bytes, width, (size_t)g->world, hipMemcpyDeviceToHost, s));
+  else
+    GS_HIP(hipMemcpy2D(h, g->foot_words * 4, src, si.bytes, width, (size_t)g->world, hipMemcpyDeviceToHost));
   return GS_OK;
 }
 
 int enqueue(Group* g) {
   const int i = (int)(g->frame % (uint64_t)g->F);
   SlotInfo& si = g->sinfo[i];
-  int rc = read_footers(g, i);  // frame k - F: bounds the pipeline, feeds the split
+  int rc = set_dev(g->mem[0].device);
   if (rc != GS_OK) return rc;
+  // re-balance from the snapshot of frame k - kRebalanceEvery / 2 (long done)
+  if (g->frame % kRebalanceEvery == 0 && g->snap_pending) {
+    GS_HIP(hipEventSynchronize(g->ev_snap));
+    g->snap_pending = false;
+    parse_footers(g, g->h_snap, g->snap_bounds, false, true);
+  }
+  // the gather timing of the frame this slot held (profiling only)
+  if (si.gather_timed) {
+    if (hipEventQuery(g->ev_g1[i]) == hipSuccess) {
+      float ms = 0.0f;
+      GS_HIP(hipEventElapsedTime(&ms, g->ev_g0[i], g->ev_g1[i]));
+      g->g_ms += ms;
+      g->g_n += 1;
+    }
+    si.gather_timed = false;
+  }
   int pad = 0;
   for (int r = 0; r < g->world; ++r) pad = std::max(pad, (int)(g->bounds[r + 1] - g->bounds[r]));
   const size_t bgr_part = align256((size_t)pad * g->th * g->W * 3);
@@ -335,24 +349,25 @@ int enqueue(Group* g) {
     if ((rc = set_dev(m.device)) != GS_OK) return rc;
     GS_HIP(hipEventRecord(m.ev_gathered[i], m.comm_stream));
   }
-  // every band's footer to the host (one strided copy), for frame k + F
   Member& m0 = g->mem[0];
   if ((rc = set_dev(m0.device)) != GS_OK) return rc;
   if (timed) GS_HIP(hipEventRecord(g->ev_g1[i], m0.comm_stream));
-  GS_HIP(hipMemcpy2DAsync(g->h_foot + (size_t)i * g->world * g->foot_words, g->foot_words * 4,
-                          m0.d_recv + (size_t)i * g->world * g->slot_cap + bgr_part, bytes,
-                          (16 + (size_t)pad * g->tiles_x) * 4, (size_t)g->world, hipMemcpyDeviceToHost,
-                          m0.comm_stream));
-  GS_HIP(hipEventRecord(g->ev_foot[i], m0.comm_stream));
   si.used = true;
-  si.footers_read = false;
   si.gather_timed = timed;
   si.frame = g->frame;
   si.bounds = g->bounds;
   si.pad_rows = pad;
   si.bgr_part = bgr_part;
   si.bytes = bytes;
+  // the footers of this frame for the re-balancing kRebalanceEvery / 2 frames on
+  if (g->rebalance && g->world > 1 && g->frame % kRebalanceEvery == kRebalanceEvery / 2) {
+    if ((rc = copy_footers(g, i, g->h_snap, m0.comm_stream, true)) != GS_OK) return rc;
+    GS_HIP(hipEventRecord(g->ev_snap, m0.comm_stream));
+    g->snap_bounds = g->bounds;
+    g->snap_pending = true;
+  }
   g->last_slot = i;
+  g->last_read = false;
   g->frame += 1;
   return GS_OK;
 }
@@ -394,10 +409,12 @@ void release(Group* g) {
     if (m.comm_stream) (void)hipStreamDestroy(m.comm_stream);
   }
   if (!g->mem.empty()) (void)hipSetDevice(g->mem[0].device);
-  for (auto* v : {&g->ev_foot, &g->ev_g0, &g->ev_g1})
+  for (auto* v : {&g->ev_g0, &g->ev_g1})
     for (hipEvent_t e : *v)
       if (e) (void)hipEventDestroy(e);
-  if (g->h_foot) (void)hipHostFree(g->h_foot);
+  if (g->ev_snap) (void)hipEventDestroy(g->ev_snap);
+  if (g->h_snap) (void)hipHostFree(g->h_snap);
+  if (g->h_last) (void)hipHostFree(g->h_last);
   g->mem.clear();
 }
 
@@ -525,18 +542,20 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
   if ((rc = set_dev(g->mem[0].device)) != GS_OK) return fail(rc);
   {
     hipError_t e;
-    g->ev_foot.assign((size_t)g->F, nullptr);
     g->ev_g0.assign((size_t)g->F, nullptr);
     g->ev_g1.assign((size_t)g->F, nullptr);
     for (int s = 0; s < g->F; ++s) {
-      if ((e = hipEventCreateWithFlags(&g->ev_foot[s], hipEventDisableTiming)) != hipSuccess ||
-          (e = hipEventCreate(&g->ev_g0[s])) != hipSuccess || (e = hipEventCreate(&g->ev_g1[s])) != hipSuccess)
+      if ((e = hipEventCreate(&g->ev_g0[s])) != hipSuccess || (e = hipEventCreate(&g->ev_g1[s])) != hipSuccess)
         return fail(gsr::hip_fail(e, "hipEventCreate"));
     }
-    if ((e = hipHostMalloc((void**)&g->h_foot, (size_t)g->F * g->world * g->foot_words * 4,
-                           hipHostMallocDefault)) != hipSuccess)
+    if ((e = hipEventCreateWithFlags(&g->ev_snap, hipEventDisableTiming)) != hipSuccess)
+      return fail(gsr::hip_fail(e, "hipEventCreate"));
+    const size_t fb = (size_t)g->world * g->foot_words * 4;
+    if ((e = hipHostMalloc((void**)&g->h_snap, fb, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&g->h_last, fb, hipHostMallocDefault)) != hipSuccess)
       return fail(gsr::hip_fail(e, "hipHostMalloc(footers)"));
-    std::memset(g->h_foot, 0, (size_t)g->F * g->world * g->foot_words * 4);
+    std::memset(g->h_snap, 0, fb);
+    std::memset(g->h_last, 0, fb);
   }
 
   // communicators
@@ -602,25 +621,39 @@ int set_focal(Group* g, float fov, float sd) {
 
 int render_async(Group* g) { return enqueue(g); }
 
+// Waits for every frame, then reads the last frame's footers (its stats and
+// histogram).  Overflow: the last frame's footers (the same on every rank) or
+// an earlier frame of this process's bands since the last sync.
 int sync(Group* g) {
   int rc = GS_OK;
+  bool local_ovf = false;
   for (Member& m : g->mem) {
     if ((rc = set_dev(m.device)) != GS_OK) return rc;
     GS_HIP(hipStreamSynchronize(m.comm_stream));
     for (gs_renderer* c : m.slot) {
-      rc = gsr::finish_frame(c);  // (overflow is decided from the gathered footers)
-      if (rc != GS_OK && rc != GS_EOVERFLOW) return rc;
+      rc = gsr::finish_frame(c);
+      if (rc == GS_EOVERFLOW) local_ovf = true;
+      else if (rc != GS_OK) return rc;
     }
   }
-  // the remaining frames' footers, oldest first
-  std::vector<int> order;
-  for (int i = 0; i < g->F; ++i)
-    if (g->sinfo[i].used && !g->sinfo[i].footers_read) order.push_back(i);
-  std::sort(order.begin(), order.end(), [&](int a, int b) { return g->sinfo[a].frame < g->sinfo[b].frame; });
-  for (int i : order)
-    if ((rc = read_footers(g, i)) != GS_OK) return rc;
-  if (g->overflow_seen) {
-    g->overflow_seen = false;
+  bool ovf = false;
+  if (g->last_slot >= 0 && !g->last_read) {
+    if ((rc = set_dev(g->mem[0].device)) != GS_OK) return rc;
+    if ((rc = copy_footers(g, g->last_slot, g->h_last, nullptr, false)) != GS_OK) return rc;
+    // (a blocking frame also re-balances the split from itself: every rank
+    // calls gs_sync after the same frames)
+    ovf = parse_footers(g, g->h_last, g->sinfo[g->last_slot].bounds, true, true);
+    g->last_read = true;
+    SlotInfo& si = g->sinfo[g->last_slot];
+    if (si.gather_timed) {
+      float ms = 0.0f;
+      GS_HIP(hipEventElapsedTime(&ms, g->ev_g0[g->last_slot], g->ev_g1[g->last_slot]));
+      g->g_ms += ms;
+      g->g_n += 1;
+      si.gather_timed = false;
+    }
+  }
+  if (ovf || local_ovf) {
     set_error("pair list overflow: a band of a frame since the last sync binned more pairs than its capacity");
     return GS_EOVERFLOW;
   }
