@@ -191,11 +191,12 @@ def main():
     split = a.split if a.split > 1 else world
     if group:
         if world > 1 or a.gather:
-            cid = comm_id_create() if rank == 0 else None
             if world > 1:
-                box = [cid]
-                dist.broadcast_object_list(box, src=0)
-                cid = box[0]
+                from gaussian_splat_ipu_amd import dist as gdist
+
+                cid = gdist.share_comm_id(rank, comm_id_create)
+            else:
+                cid = comm_id_create()
             R = [GpuSplatter(g, fb, device=local, comm_id=cid, rank=rank, world=world, frames_in_flight=F,
                              profile=True, rebalance=not a.no_rebalance)]
         else:  # --split S: S bands emulated on this GPU

@@ -105,3 +105,17 @@ def assemble_bands(gathered: np.ndarray, fb: TiledFramebuffer, bands, channels: 
         y1 = min(fb.height, t1 * fb.tile_height)
         parts.append(g[r, : max(0, y1 - y0)])
     return np.concatenate(parts, 0)
+
+
+def share_comm_id(rank: int, make_id) -> bytes:
+    """The row-band group's RCCL id on every rank of an initialised
+    torch.distributed group (any backend; bench.py uses gloo): rank 0 calls
+    make_id() (splatter.comm_id_create), the others receive its 128 bytes."""
+    import torch.distributed as tdist
+
+    box = [make_id() if rank == 0 else None]
+    tdist.broadcast_object_list(box, src=0)
+    cid = box[0]
+    if not isinstance(cid, (bytes, bytearray)) or len(cid) != 128:
+        raise RuntimeError("share_comm_id: rank 0 sent no 128-byte RCCL id")
+    return bytes(cid)

@@ -116,3 +116,43 @@ def test_balanced_bands_partition():
         assert max(loads) <= w.sum() / world + 2.0 * w.max() + 1e-9
     with pytest.raises(ValueError):
         gdist.balanced_bands(np.ones(3), 4)
+
+
+def _id_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gaussian_splat_ipu_amd import dist as gdist
+
+        made = []
+
+        def make():
+            made.append(rank)
+            return bytes(range(128))
+
+        cid = gdist.share_comm_id(rank, make)
+        q.put((rank, cid == bytes(range(128)), made))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_share_comm_id_world_3():
+    """bench.py's RCCL-id hand-off for the row-band group (gs_create_rank):
+    only rank 0 makes the id, every rank receives the same 128 bytes."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_id_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = sorted(q.get(timeout=10) for _ in range(3))
+    assert all(ok for _, ok, _ in got)
+    assert [m for _, _, m in got] == [[0], [], []]
