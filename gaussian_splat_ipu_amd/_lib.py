@@ -24,6 +24,7 @@ GS_FLAG_BAND_CULL = 32
 GS_FLAG_NO_PAIR_CULL = 64
 GS_FLAG_NO_REBALANCE = 128
 GS_FLAG_GATHER_COPY = 256
+GS_FLAG_LATTICE = 512
 GS_MAX_GPUS = 16
 GS_LAYOUT_ROW_MAJOR = 0
 GS_LAYOUT_REF_TILE_MAJOR = 1
@@ -117,6 +118,23 @@ class FrameStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class LatticeStats(C.Structure):
+    _fields_ = [
+        ("frames", C.c_uint64),
+        ("total_slots", C.c_uint64),
+        ("dropped", C.c_uint64),
+        ("send_failed", C.c_uint64),
+        ("zbuf_overrun", C.c_uint64),
+        ("records_per_tile", C.c_uint32),
+        ("extra_records", C.c_uint32),
+        ("slots_per_tile", C.c_uint32),
+        ("channel_slots", C.c_uint32),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class SynthParams(C.Structure):
     _fields_ = [
         ("n", C.c_uint64),
@@ -148,6 +166,8 @@ _SIGS = {
                                  C.c_int, C.c_int, C.POINTER(_P)]),
     "gs_group_bands": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_size_t]),
     "gs_balanced_bands": (C.c_int, [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "gs_get_lattice_stats": (C.c_int, [_P, C.POINTER(LatticeStats)]),
+    "gs_read_lattice_slots": (C.c_int, [_P, _FP, C.c_size_t]),
     "gs_set_view": (C.c_int, [_P, _FP]),
     "gs_set_projection": (C.c_int, [_P, _FP]),
     "gs_set_focal": (C.c_int, [_P, C.c_float, C.c_float]),

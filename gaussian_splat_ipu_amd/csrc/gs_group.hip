@@ -429,6 +429,10 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
   *out = nullptr;
   const bool mp = id != nullptr;
   const int G = mp ? world : (int)cfg->num_gpus;
+  if (cfg->flags & GS_FLAG_LATTICE) {
+    set_error("gs_create: the lattice emulator (GS_FLAG_LATTICE) runs on one device, not in a row-band group");
+    return GS_EINVAL;
+  }
   if (G < 1 || (!mp && G > GS_MAX_GPUS) || (mp && (rank < 0 || rank >= world)) || cfg->tile_height == 0 ||
       cfg->tile_width == 0 || cfg->width == 0 || cfg->height == 0) {
     set_error("gs_create: invalid row-band group (num_gpus / rank / world)");

@@ -67,6 +67,13 @@ struct gs_renderer {
   void* d_out = nullptr;        // rgba f32 + bgr8
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
   void* d_lazy = nullptr;       // lazy big lists (16x16 tiles): per-tile tables + saved blend waves
+  // GS_FLAG_LATTICE: the lattice-migration emulator's state (gs_lattice.hip)
+  void* d_lat = nullptr;
+  bool lattice = false;
+  gsk::LatticeBufs lat{};
+  int lat_gpt = 0, lat_rem = 0;  // initial records per tile, extra records of the last tile
+  size_t lat_slots = 0;          // vertsIn slots over all tiles
+  uint64_t lat_frames = 0;       // frames stepped (the exchange parity)
   int bin_global = 0, chunk_size = 0, n_chunks = 0;
   bool pair_cull = false;       // chunked binning into the alpha-box tiles only
   size_t zero_bytes = 0;

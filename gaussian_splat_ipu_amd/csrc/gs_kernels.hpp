@@ -132,4 +132,35 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s);
 
+// ---- the lattice-migration emulator (gs_lattice.hip, GS_FLAG_LATTICE)
+constexpr int kLatChan = 75;        // records per channel (edge_builder.cpp:18, ipu_rasteriser.cpp:307-308)
+constexpr int kLatExtra = 600;      // extra vertsIn slots per tile (ipu_rasteriser.cpp:309)
+constexpr int kLatMaxSlots = 2048;  // vertsIn slots of one tile the kernel's LDS holds
+
+struct LatticeParams {
+  float mvp[16];
+  float tanfov, focal_x, focal_y, guard_thr, scale_div;
+  float W, H, tw, th;
+  float across;       // TiledFramebuffer::numTilesAcross (a float)
+  int width, height, tile_w, tile_h, tiles_x, n_tiles;
+  int gpt, rem;       // records per tile of the initial distribution, extra records of the last tile
+  int parity;         // this frame writes out-channel set `parity`, reads the other
+  int write_rgba;
+  int bgr_pitch;
+};
+
+struct LatticeBufs {
+  float4* slots;      // vertsIn: every tile's slots (tile t from t * (gpt + 600)), 4 float4 (Gaussian3D) each
+  float4* chan;       // out-channels [2][T][4 directions][75 slots][4]
+  float4* zbuf;       // z-buffer (persistent): 3 float4 per entry: colour | cov a b c, z | mean x y
+  float4* zscratch;   // the sort's permutation scratch (same size)
+  uint32_t* splatted; // [T] the reference's splatted counter (kept while a tile renders nothing)
+  uint32_t* tile_stat;  // [T][4] render list, dropped, failed sends, z-buffer overruns (last frame)
+  float4* rgba;       // row-major W x H
+  uint8_t* bgr;
+  uint32_t* host_counters;  // mapped: counters[16] + splatted[T]
+};
+
+void launch_lattice(const LatticeParams& lp, const LatticeBufs& lb, hipStream_t s);
+
 }  // namespace gsk

@@ -118,7 +118,7 @@ void release(gs_renderer* r) {
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
-  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy})
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat})
     if (p) (void)hipFree(p);
   free_pairs(r);
   if (r->h_counters) (void)hipHostFree(r->h_counters);
@@ -231,6 +231,50 @@ int profile_harvest(gs_renderer* r, ProfileSlot& s) {
   return GS_OK;
 }
 
+// GS_FLAG_LATTICE: one step of the emulated lattice (compute set + exchange,
+// ipu_rasteriser.cpp:393-399); its kernel time is reported as the blend stage
+int enqueue_lattice(gs_renderer* r, const gsk::FrameParams& fp, ProfileSlot* slot) {
+  hipStream_t s = r->stream;
+  gsk::LatticeParams lp{};
+  std::memcpy(lp.mvp, fp.mvp, sizeof(lp.mvp));
+  lp.tanfov = fp.tanfov;
+  lp.focal_x = fp.focal_x;
+  lp.focal_y = fp.focal_y;
+  lp.guard_thr = fp.guard_thr;
+  lp.scale_div = fp.scale_div;
+  lp.W = fp.W;
+  lp.H = fp.H;
+  lp.tw = fp.tw;
+  lp.th = fp.th;
+  lp.across = (float)r->tiles_x;
+  lp.width = fp.width;
+  lp.height = fp.height;
+  lp.tile_w = fp.tile_w;
+  lp.tile_h = fp.tile_h;
+  lp.tiles_x = r->tiles_x;
+  lp.n_tiles = r->tiles_x * r->tiles_y;
+  lp.gpt = r->lat_gpt;
+  lp.rem = r->lat_rem;
+  lp.parity = (int)(r->lat_frames & 1);
+  lp.write_rgba = fp.write_rgba;
+  lp.bgr_pitch = fp.bgr_pitch;
+  gsk::LatticeBufs lb = r->lat;
+  lb.rgba = r->buf.rgba;
+  lb.bgr = r->buf.bgr;
+  lb.host_counters = r->buf.host_counters;
+  if (slot)
+    for (int k = 0; k < gsk::GS_STAGE_EVENTS - 1; ++k) GS_HIP(hipEventRecord(slot->ev[k], s));
+  gsk::launch_lattice(lp, lb, s);
+  if (slot) {
+    GS_HIP(hipEventRecord(slot->ev[gsk::GS_STAGE_EVENTS - 1], s));
+    slot->pending = true;
+  }
+  GS_HIP(hipGetLastError());
+  r->lat_frames++;
+  r->frame_pending = true;
+  return GS_OK;
+}
+
 int enqueue_frame(gs_renderer* r) {
   // several frames may be in flight on the stream; the host mirrors always
   // hold the last one's counters after gs_sync
@@ -248,6 +292,7 @@ int enqueue_frame(gs_renderer* r) {
     int rc = profile_harvest(r, *slot);
     if (rc != GS_OK) return rc;
   }
+  if (r->lattice) return enqueue_lattice(r, fp, slot);
   // counters + tile_count: the chunked path rewrites all of them (colscan,
   // scan); the global-atomic path accumulates tile_count and needs zeros
   if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
@@ -318,6 +363,52 @@ int finish_frame(gs_renderer* r) {
   return GS_OK;
 }
 
+// GS_FLAG_LATTICE: the emulator's device state, with the reference's initial
+// distribution of the records over the tiles: calculateMapping /
+// applyTileMapping of the 64-float records (ipu_rasteriser.cpp:164-214,
+// 287-298) put record j on tile j / gpt, gpt = ceil(64 n / (tiles * 64)) in
+// float; every tile has gpt + 600 vertsIn slots (:307-309, 361-363), the last
+// one also the rem records past fullTiles * gpt.  Never-written memory
+// (padding, extra storage, channels, z-buffers) starts as zeros.
+int lattice_init(gs_renderer* r, const gs_gaussian3d* g, size_t n) {
+  const int T = r->tiles_x * r->tiles_y;
+  const float q = (float)((uint64_t)n * 64u) / ((float)T * 64.0f);
+  const int64_t gpt = (int64_t)std::ceil(q);
+  const int64_t rem = (int64_t)n - ((int64_t)n / gpt) * gpt;
+  if (gpt + rem + gsk::kLatExtra > gsk::kLatMaxSlots) {
+    set_error("gs_create: lattice mode holds at most " + std::to_string(gsk::kLatMaxSlots) +
+              " vertsIn slots per tile (" + std::to_string(gpt) + " records per tile + 600)");
+    return GS_EINVAL;
+  }
+  const size_t slots = (size_t)T * (size_t)(gpt + gsk::kLatExtra) + (size_t)rem;
+  const size_t chan = (size_t)2 * T * 4 * gsk::kLatChan * 4;  // float4
+  const size_t bytes = slots * 64 + chan * 16 + slots * 48 * 2 + (size_t)T * 4 * 5;
+  GS_HIP(hipMalloc(&r->d_lat, bytes));
+  GS_HIP(hipMemset(r->d_lat, 0, bytes));
+  char* p = (char*)r->d_lat;
+  r->lat.slots = (float4*)p;
+  p += slots * 64;
+  r->lat.chan = (float4*)p;
+  p += chan * 16;
+  r->lat.zbuf = (float4*)p;
+  p += slots * 48;
+  r->lat.zscratch = (float4*)p;
+  p += slots * 48;
+  r->lat.splatted = (uint32_t*)p;
+  r->lat.tile_stat = r->lat.splatted + T;
+  std::vector<float> img(slots * 16, 0.0f);
+  for (size_t j = 0; j < n; ++j) {
+    const size_t t = j / (size_t)gpt;
+    std::memcpy(&img[(t * (size_t)(gpt + gsk::kLatExtra) + (j - t * (size_t)gpt)) * 16], &g[j], 64);
+  }
+  GS_HIP(hipMemcpy(r->lat.slots, img.data(), slots * 64, hipMemcpyHostToDevice));
+  r->lat_gpt = (int)gpt;
+  r->lat_rem = (int)rem;
+  r->lat_slots = slots;
+  r->lattice = true;
+  return GS_OK;
+}
+
 int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_renderer* share,
            gs_renderer** out) {
   if (!out || !cfg || (n > 0 && !g)) {
@@ -331,8 +422,20 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     set_error("gs_create: invalid configuration");
     return GS_EINVAL;
   }
+  const bool lattice = (cfg->flags & GS_FLAG_LATTICE) != 0;
+  if (lattice && (cfg->width % cfg->tile_width || cfg->height % cfg->tile_height || cfg->band_count != 1 ||
+                  cfg->band_row_end > cfg->band_row_begin || (cfg->flags & GS_FLAG_BAND_INTERLEAVED) || n == 0 ||
+                  n >= (1u << 24))) {
+    set_error("gs_create: GS_FLAG_LATTICE needs a whole tile grid (width % tile_width == 0, height % "
+              "tile_height == 0), one band and 1 <= n < 2^24");
+    return GS_EINVAL;
+  }
   gs_renderer* r = new gs_renderer();
   r->cfg = *cfg;
+  if (lattice) {  // the guard band of the lattice is the tile's own diagonal (codelets.cpp:470)
+    r->cfg.guard_tile_width = 0;
+    r->cfg.guard_tile_height = 0;
+  }
   r->n = n;
   r->profile = (cfg->flags & GS_FLAG_PROFILE) != 0;
   r->pair_cull = (cfg->flags & GS_FLAG_NO_PAIR_CULL) == 0;
@@ -551,6 +654,10 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     return fail(hip_fail(e, "hipHostGetDevicePointer"));
   r->buf.host_sticky = r->buf.host_counters + 16 + T;
   r->hist_snapshot.assign((size_t)r->n_tiles, 0u);
+  if (lattice) {
+    const int rc2 = lattice_init(r, g, n);
+    if (rc2 != GS_OK) return fail(rc2);
+  }
   if (r->profile) {
     for (auto& s : r->ring)
       for (auto& ev : s.ev)
@@ -652,6 +759,10 @@ void retile(const float* rm, size_t rows, size_t W, size_t tw, size_t th, int ti
 }
 
 int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list, size_t n_list) {
+  if (r->lattice) {
+    set_error("gs_read_bins: a lattice renderer has no converged tile lists (gs_read_lattice_slots)");
+    return GS_EINVAL;
+  }
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
@@ -1032,6 +1143,50 @@ int gs_reset_kernel_times(gs_renderer* r) {
     r->k_ms[k] = 0.0;
     r->k_launches[k] = 0;
   }
+  return GS_OK;
+}
+
+int gs_get_lattice_stats(gs_renderer* r, gs_lattice_stats* st) {
+  if (!r || !st) return GS_EINVAL;
+  if (r->grp || !r->lattice) {
+    set_error("gs_get_lattice_stats: renderer created without GS_FLAG_LATTICE");
+    return GS_EINVAL;
+  }
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if ((rc = finish_frame(r)) != GS_OK) return rc;
+  std::memset(st, 0, sizeof(*st));
+  st->frames = r->lat_frames;
+  st->total_slots = r->lat_slots;
+  if (r->lat_frames) {
+    const uint32_t* c = r->h_counters;
+    st->dropped = c[12];
+    st->send_failed = c[13];
+    st->zbuf_overrun = c[14];
+  }
+  st->records_per_tile = (uint32_t)r->lat_gpt;
+  st->extra_records = (uint32_t)r->lat_rem;
+  st->slots_per_tile = (uint32_t)(r->lat_gpt + gsk::kLatExtra);
+  st->channel_slots = (uint32_t)gsk::kLatChan;
+  return GS_OK;
+}
+
+int gs_read_lattice_slots(gs_renderer* r, float* gids, size_t n) {
+  if (!r || !gids) return GS_EINVAL;
+  if (r->grp || !r->lattice) {
+    set_error("gs_read_lattice_slots: renderer created without GS_FLAG_LATTICE");
+    return GS_EINVAL;
+  }
+  if (n < r->lat_slots) {
+    set_error("gs_read_lattice_slots: destination too small");
+    return GS_EINVAL;
+  }
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if ((rc = finish_frame(r)) != GS_OK) return rc;
+  // the gid is the last float of every 64-B slot: one strided copy
+  GS_HIP(hipMemcpy2D(gids, sizeof(float), (const char*)r->lat.slots + 60, 64, sizeof(float), r->lat_slots,
+                     hipMemcpyDeviceToHost));
   return GS_OK;
 }
 

@@ -23,6 +23,7 @@ from . import camera
 from ._lib import (
     GS_FLAG_BAND_CULL,
     GS_FLAG_GATHER_COPY,
+    GS_FLAG_LATTICE,
     GS_FLAG_NO_PAIR_CULL,
     GS_FLAG_NO_REBALANCE,
     GS_FLAG_BAND_INTERLEAVED,
@@ -38,6 +39,7 @@ from ._lib import (
     Config,
     FrameStats,
     Gaussian3D,
+    LatticeStats,
     check,
     fptr,
     lib,
@@ -93,6 +95,7 @@ class GpuSplatter:
         comm_id: bytes | None = None,
         rank: int = 0,
         world: int = 1,
+        lattice: bool = False,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -123,6 +126,7 @@ class GpuSplatter:
             | (0 if pair_cull else GS_FLAG_NO_PAIR_CULL)
             | (0 if rebalance else GS_FLAG_NO_REBALANCE)
             | (GS_FLAG_GATHER_COPY if gather_copy else 0)
+            | (GS_FLAG_LATTICE if lattice else 0)
         )
         cfg.num_gpus = int(num_gpus)
         if device_ids is not None:
@@ -241,6 +245,20 @@ class GpuSplatter:
         st = FrameStats()
         check(lib().gs_get_stats(self._h, C.byref(st)))
         return st.as_dict()
+
+    def lattice_stats(self) -> dict:
+        """lattice=True: the emulated lattice after the last frame
+        (gs_get_lattice_stats)."""
+        st = LatticeStats()
+        check(lib().gs_get_lattice_stats(self._h, C.byref(st)))
+        return st.as_dict()
+
+    def lattice_slots(self) -> np.ndarray:
+        """lattice=True: the gid of every vertsIn slot, tile-major (0 = empty)."""
+        n = self.lattice_stats()["total_slots"]
+        out = np.empty(n, np.float32)
+        check(lib().gs_read_lattice_slots(self._h, fptr(out), out.size))
+        return out
 
     def get_bins(self):
         """(tile_start[T+1] uint64, list[P] uint32): depth-sorted per-tile lists."""

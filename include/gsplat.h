@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 6
+#define GSPLAT_ABI_VERSION 7
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -114,6 +114,22 @@ typedef struct gs_config {
                                   device-to-device copies instead of RCCL
                                   (automatic when device_ids repeat a device:
                                   several bands emulated on one GPU) */
+#define GS_FLAG_LATTICE 512u     /* ABI 7, SURVEY §8 f4: emulate the reference's
+                                  multi-frame lattice migration instead of the
+                                  converged single-frame binning.  Every
+                                  gs_render is one step of the IPU program --
+                                  the GSplat codelet of every tile and the
+                                  channel exchange (ipu_rasteriser.cpp:393-399,
+                                  codelets.cpp:143-641, edge_builder.cpp:35-84)
+                                  -- from the reference's initial distribution
+                                  of the records by index, so the frames are its
+                                  transient ones (75-record channels, y-first
+                                  routing, silent drops, the off-by-one
+                                  quicksort, the stale splatted counters).
+                                  Needs width % tile_width == 0, height %
+                                  tile_height == 0, one band, one device; the
+                                  guard band uses the tile's own diagonal;
+                                  gs_read_bins is unavailable. */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */
@@ -200,6 +216,26 @@ int gs_group_bands(gs_renderer* r, uint32_t* bounds, size_t n);
  * bounds = world + 1 entries.  Deterministic, so every rank derives the same
  * split from the same gathered histograms. */
 int gs_balanced_bands(const double* row_work, uint32_t rows, uint32_t world, uint32_t* bounds);
+
+/* GS_FLAG_LATTICE renderers: the emulated lattice after the last frame. */
+typedef struct gs_lattice_stats {
+  uint64_t frames;         /* frames stepped since gs_create                 */
+  uint64_t total_slots;    /* vertsIn slots over all tiles                   */
+  uint64_t dropped;        /* last frame: vertsIn inserts that found no empty
+                              slot (the reference drops them silently)      */
+  uint64_t send_failed;    /* last frame: channel inserts into a full channel */
+  uint64_t zbuf_overrun;   /* last frame: render-list entries past a tile's
+                              z-buffer (the reference reads past it; here
+                              they are empty records)                        */
+  uint32_t records_per_tile; /* gpt: the initial records per tile           */
+  uint32_t extra_records;    /* rem: the last tile's extra initial records  */
+  uint32_t slots_per_tile;   /* gpt + 600 (the last tile: + rem)            */
+  uint32_t channel_slots;    /* 75 records per channel                      */
+} gs_lattice_stats;
+int gs_get_lattice_stats(gs_renderer* r, gs_lattice_stats* st);
+/* The gid of every vertsIn slot (0 = empty), tile-major: tile t's slots start
+ * at t * slots_per_tile.  n >= total_slots. */
+int gs_read_lattice_slots(gs_renderer* r, float* gids, size_t n);
 
 /* ------------------------------------------------------------ per-frame inputs */
 /* Replaces IpuSplatter::updateModelView (ipu_rasteriser.cpp:86-93): the

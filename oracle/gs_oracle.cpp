@@ -546,3 +546,436 @@ uint32_t or_point_splat(const float* xyz, int64_t n, const float* view_rm, const
 }
 
 }  // extern "C"
+
+// ======================================================================= lattice
+// the reference's multi-frame migration of the Gaussians over
+// the 4-neighbour channel lattice, restated frame by frame: the GSplat codelet
+// of every IPU tile (codelets.cpp:143-641: compute :605-639, readInput
+// :507-586, renderInternal :437-505, renderTile :358-421, the quicksort
+// :295-356), the initial distribution of the records over the tiles
+// (ipu_rasteriser.cpp:164-214, 287-386) and the exchange of the out-channels
+// into the neighbours' in-channels (edge_builder.cpp:15-84).  The choices
+// where the reference reads memory it never wrote or converts out of range are
+// listed in gs_oracle.h (or_lattice_create).
+namespace {
+
+enum LDir { kLeft = 0, kRight = 1, kUp = 2, kDown = 3, kNone = 4 };  // ipu_geometry.hpp:94-100
+// channel: EdgeBuilder::addEdge allocates channelSize / 4 floats
+// (edge_builder.cpp:18) with channelSize = 300 * 64 (ipu_rasteriser.cpp:
+// 307-308); insert() walks it in 64-float slots: 75 records
+constexpr int kChan = 75;
+// extraStorageSize = 2 * channelSize floats of vertsIn (ipu_rasteriser.cpp:309,361-363)
+constexpr int kExtra = 600;
+
+struct LG3 { float f[16]; };  // Gaussian3D at the head of a 64-float slot (ipu_geometry.hpp:305-311)
+struct LG2 { float colour[4]; float cov[3]; float mean[2]; float z; };  // Gaussian2D (:232-236)
+struct LB { float x0, y0, x1, y1; };                                     // Bounds2f
+struct LDirs { bool up, right, down, left; };
+
+struct Lat {
+  int W, H, tw, th, tx, ty, T;
+  float across;  // TiledFramebuffer::numTilesAcross, a float (tile_config.hpp:135)
+  int64_t n, gpt, rem;
+  std::vector<LG3> vs;       // every tile's vertsIn slots
+  std::vector<LG3> chan[2];  // out-channels [parity][tile][direction][slot]
+  std::vector<LG2> zb;       // every tile's gaus2D z-buffer (persistent)
+  std::vector<uint32_t> splatted;
+  std::vector<float> rgba;   // row-major W x H
+  uint64_t frames = 0, dropped = 0, send_failed = 0, overrun = 0;
+  int64_t base(int t) const { return (int64_t)t * (gpt + kExtra); }
+  int vs_n(int t) const { return (int)(gpt + kExtra + (t == T - 1 ? rem : 0)); }
+  int z_n(int t) const { return t == T - 1 ? (int)(gpt + rem) : (int)(gpt + kExtra); }
+};
+
+// float -> unsigned of a negative / NaN / huge value is undefined in C++ (the
+// reference does it for tiles above the first row and means left of or above
+// the image); the emulator saturates
+uint32_t lat_u32(float v) {
+  if (!(v > 0.0f)) return 0u;
+  if (v >= 4294967296.0f) return 0xFFFFFFFFu;
+  return (uint32_t)v;
+}
+
+// TiledFramebuffer::getTileBounds (tile_config.hpp:57-71): float arithmetic
+LB lat_bounds(const Lat& L, uint32_t tid) {
+  const float div = std::floor((float)tid / L.across);
+  const float mod = (float)tid - div * L.across;
+  LB b;
+  b.x0 = std::floor(mod * (float)L.tw);
+  b.y0 = std::floor(div * (float)L.th);
+  b.x1 = b.x0 + (float)L.tw;
+  b.y1 = b.y0 + (float)L.th;
+  return b;
+}
+
+// Bounds2f::centroid (ipu_geometry.hpp:109-111)
+void lat_centroid(const LB& b, float& cx, float& cy) {
+  cx = (b.x1 + b.x0) * 0.5f;
+  cy = (b.y1 + b.y0) * 0.5f;
+}
+
+// TiledFramebuffer::getNearbyTile (tile_config.hpp:73-86): unsigned wrap for
+// left / right, float arithmetic for up / down
+uint32_t lat_nearby(const Lat& L, uint32_t tid, int from) {
+  switch (from) {
+    case kLeft: return tid - 1u;
+    case kRight: return tid + 1u;
+    case kUp: return lat_u32((float)tid - L.across);
+    case kDown: return lat_u32((float)tid + L.across);
+  }
+  return tid;
+}
+
+// Bounds2f::contains (ipu_geometry.hpp:163-165)
+bool lat_contains(const LB& b, float x, float y) {
+  return std::ceil(x) >= b.x0 && std::floor(x) < b.x1 && std::ceil(y) >= b.y0 && std::floor(y) < b.y1;
+}
+
+// TiledFramebuffer::pixCoordToTile (tile_config.hpp:43-54)
+float lat_pix_to_tile(const Lat& L, float row, float col) {
+  const float r = std::nearbyint(row), c = std::nearbyint(col);
+  const float tc = std::floor(c / (float)L.tw);
+  const float tr = std::floor(r / (float)L.th);
+  return tr * L.across + tc;
+}
+
+// manhattanDistance (tile_config.hpp:88-90) as float |.| (the centroids of even
+// tile sizes are integers, where an int abs() would agree)
+float lat_manhattan(float ax, float ay, float bx, float by) { return std::fabs(ax - bx) + std::fabs(ay - by); }
+
+// getBestDirection (tile_config.hpp:92-110): y first
+int lat_best_dir(float sx, float sy, float dx, float dy) {
+  if (lat_manhattan(sx, sy, dx, dy) == 0.0f) return kNone;
+  if (sy < dy) return kDown;
+  if (sy > dy) return kUp;
+  if (sx < dx) return kRight;
+  if (sx > dx) return kLeft;
+  return kNone;
+}
+
+// Bounds2f::clip's direction flags (ipu_geometry.hpp:133-139)
+LDirs lat_clip(const LB& bb, const LB& tb) {
+  LDirs d;
+  d.left = std::floor(bb.x0) < tb.x0;
+  d.up = std::floor(bb.y0) < tb.y0;
+  d.right = std::ceil(bb.x1) >= tb.x1;
+  d.down = std::ceil(bb.y1) >= tb.y1;
+  return d;
+}
+
+// EdgeBuilder::constructLattice (edge_builder.cpp:35-84): the out-channel the
+// exchange copies into in-channel `from` of tile t -- the neighbour's opposite
+// out-channel, or the tile's own one at the image border (self loop)
+void lat_source(const Lat& L, int t, int from, int& st, int& sd) {
+  const LB b = lat_bounds(L, (uint32_t)t);  // checkImageBoundaries (tile_config.hpp:116-126)
+  const bool bl = b.x0 < 1.0f, bu = b.y0 < 1.0f;
+  const bool br = b.x1 > (float)(L.W - 1), bd = b.y1 > (float)(L.H - 1);
+  st = t;
+  sd = from;
+  switch (from) {
+    case kRight: if (!br) { st = t + 1; sd = kLeft; } break;
+    case kLeft: if (!bl) { st = t - 1; sd = kRight; } break;
+    case kUp: if (!bu) { st = t - L.tx; sd = kDown; } break;
+    case kDown: if (!bd) { st = t + L.tx; sd = kUp; } break;
+  }
+}
+
+// insert (codelets.cpp:41-59): a slot with the same gid -> done; else the first
+// empty slot (gid == 0); false when there is none
+bool lat_insert(LG3* buf, int n, const LG3& g) {
+  int idx = n;
+  for (int i = 0; i < n; ++i) {
+    const float gid = buf[i].f[15];
+    if (gid == g.f[15]) return true;
+    if (gid == 0.0f && i < idx) idx = i;
+  }
+  if (idx >= n) return false;
+  buf[idx] = g;
+  return true;
+}
+
+// iterativeQuickSort / partition (codelets.cpp:303-344) on entries [l, h]
+// (Lomuto, pivot = last, `<=` to the left; an explicit stack of (l, h))
+void lat_quicksort(LG2* e, int l, int h) {
+  std::vector<int> st;
+  st.push_back(l);
+  st.push_back(h);
+  while (!st.empty()) {
+    h = st.back();
+    st.pop_back();
+    l = st.back();
+    st.pop_back();
+    const float pivot = e[h].z;
+    int i = l - 1;
+    for (int j = l; j <= h - 1; ++j)
+      if (e[j].z <= pivot) {
+        ++i;
+        std::swap(e[i], e[j]);
+      }
+    std::swap(e[i + 1], e[h]);
+    const int pi = i + 1;
+    if (pi - 1 > l) {
+      st.push_back(l);
+      st.push_back(pi - 1);
+    }
+    if (pi + 1 < h) {
+      st.push_back(pi + 1);
+      st.push_back(h);
+    }
+  }
+}
+
+struct LP {
+  float vx, vy, z, cov[3];
+  LB bb;
+  bool within;
+};
+
+// the per-record math both readInput and renderInternal do (codelets.cpp:
+// 460-470, 537-551, 576-578): the same functions as the single-frame path
+void lat_project(const LG3& g, const FrameC& c, float scale_div, LP& p) {
+  or_proj o;
+  project_one(g.f, c, scale_div, &o);
+  p.vx = o.mean2d[0];
+  p.vy = o.mean2d[1];
+  p.z = o.clip_z;
+  for (int k = 0; k < 3; ++k) p.cov[k] = o.cov2d[k];
+  const float r = o.radius;
+  p.bb = LB{p.vx - r, p.vy - r, p.vx + r, p.vy + r};
+  const float dx = p.bb.x1 - p.bb.x0, dy = p.bb.y1 - p.bb.y0;
+  p.within = std::sqrt(dx * dx + dy * dy) < c.guard_thr;
+}
+
+struct LCount {
+  uint64_t dropped = 0, send_failed = 0, overrun = 0;
+};
+
+// GSplat::compute of tile t (codelets.cpp:605-639)
+void lat_tile(Lat& L, const FrameC& c, float scale_div, int t, LCount& cnt) {
+  const int par = (int)(L.frames & 1);
+  LG3* out = &L.chan[par][(size_t)t * 4 * kChan];
+  for (int k = 0; k < 4 * kChan; ++k) out[k].f[15] = 0.0f;  // clearOutBuffers (:588-602)
+  const LB tb = lat_bounds(L, (uint32_t)t);
+  float tcx, tcy;
+  lat_centroid(tb, tcx, tcy);
+  LG3* vs = &L.vs[L.base(t)];
+  const int nvs = L.vs_n(t);
+  // sendOnce (:214-225)
+  auto send_once = [&](const LG3& g, int dir) -> bool {
+    if (dir == kNone) return false;
+    const bool ok = lat_insert(out + dir * kChan, kChan, g);
+    if (!ok) cnt.send_failed++;
+    return ok;
+  };
+  auto dest_centroid = [&](const LP& p, float& dx, float& dy) {
+    lat_centroid(lat_bounds(L, lat_u32(lat_pix_to_tile(L, p.vy, p.vx))), dx, dy);
+  };
+  // readInput of the four in-channels (:507-586), in the order of :630-633
+  const int order[4] = {kRight, kLeft, kUp, kDown};
+  for (const int from : order) {
+    int st, sd;
+    lat_source(L, t, from, st, sd);
+    const LG3* in = &L.chan[par ^ 1][((size_t)st * 4 + sd) * kChan];
+    float pcx, pcy;
+    lat_centroid(lat_bounds(L, lat_nearby(L, (uint32_t)t, from)), pcx, pcy);
+    for (int k = 0; k < kChan; ++k) {
+      const LG3 g = in[k];
+      if (g.f[15] <= 0.0f) continue;
+      LP p;
+      lat_project(g, c, scale_div, p);
+      auto keep = [&]() {
+        if (!lat_insert(vs, nvs, g)) cnt.dropped++;
+      };
+      if (lat_contains(tb, p.vx, p.vy)) {  // the anchor arrived
+        keep();
+        continue;
+      }
+      float dcx, dcy;
+      dest_centroid(p, dcx, dcy);
+      if (lat_manhattan(tcx, tcy, dcx, dcy) < lat_manhattan(pcx, pcy, dcx, dcy)) {  // in transit
+        send_once(g, lat_best_dir(tcx, tcy, dcx, dcy));
+        keep();
+        continue;
+      }
+      if (p.within) {  // spreading away from the anchor: protocol (:251-293)
+        const LDirs s = lat_clip(p.bb, tb);
+        if (from == kRight && s.left) {
+          bool ok = send_once(g, kLeft);
+          if (s.down) ok = ok && send_once(g, kDown);
+          if (s.up) ok = ok && send_once(g, kUp);
+        } else if (from == kLeft && s.right) {
+          bool ok = send_once(g, kRight);
+          if (s.down) ok = ok && send_once(g, kDown);
+          if (s.up) ok = ok && send_once(g, kUp);
+        } else if (from == kUp && s.down) {
+          send_once(g, kDown);
+        } else if (from == kDown && s.up) {
+          send_once(g, kUp);
+        } else if (s.up || s.right || s.down || s.left) {
+          bool ok = true;
+          if (s.up && from != kUp) ok = ok && send_once(g, kUp);
+          if (s.down && from != kDown) ok = ok && send_once(g, kDown);
+        }
+      }
+      keep();
+    }
+  }
+  // renderInternal (:437-505)
+  LG2* zb = &L.zb[L.base(t)];
+  const int nz = L.z_n(t);
+  int to_render = 0;
+  for (int i = 0; i < nvs; ++i) {
+    const LG3 g = vs[i];
+    if (g.f[15] <= 0.0f) continue;
+    LP p;
+    lat_project(g, c, scale_div, p);
+    LDirs dirs{false, false, false, false};  // (uninitialised in the reference outside the guard band)
+    if (p.within) dirs = lat_clip(p.bb, tb);
+    if (lat_contains(tb, p.vx, p.vy)) {
+      bool sent = true;  // send (:194-212)
+      if (dirs.right) sent = sent && send_once(g, kRight);
+      if (dirs.left) sent = sent && send_once(g, kLeft);
+      if (dirs.up) sent = sent && send_once(g, kUp);
+      if (dirs.down) sent = sent && send_once(g, kDown);
+    } else {  // evict and send one hop toward the anchor tile
+      float dcx, dcy;
+      dest_centroid(p, dcx, dcy);
+      const int dir = lat_best_dir(tcx, tcy, dcx, dcy);
+      vs[i].f[15] = 0.0f;
+      if (!send_once(g, dir)) vs[i] = g;  // guard against losing it
+    }
+    if (p.within && p.z < 0.0f) {
+      if (to_render < nz) {
+        LG2& e = zb[to_render];
+        for (int k = 0; k < 4; ++k) e.colour[k] = g.f[4 + k];
+        for (int k = 0; k < 3; ++k) e.cov[k] = p.cov[k];
+        e.mean[0] = p.vx;
+        e.mean[1] = p.vy;
+        e.z = p.z;
+      } else {
+        cnt.overrun++;  // insertAt past the z-buffer fails (:33-39)
+      }
+      to_render++;
+    }
+  }
+  // renderTile (:358-421): sortBuffer sorts [0, L] inclusive (the stale entry
+  // L included, the largest z of the L + 1 dropped) unless L >= z_n - 1
+  if (to_render >= 1 && to_render < nz - 1) lat_quicksort(zb, 0, to_render);
+  for (int ly = 0; ly < L.th; ++ly) {
+    for (int lx = 0; lx < L.tw; ++lx) {
+      const float pfx = tb.x0 + (float)lx, pfy = tb.y0 + (float)ly;
+      float T_ = 1.0f;
+      float C[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int gi = 0; gi < to_render; ++gi) {
+        LG2 e;
+        if (gi < nz) e = zb[gi];
+        else std::memset(&e, 0, sizeof(e));  // past the z-buffer: read as empty
+        // ComputeConicOpacity (ipu_geometry.hpp:278-286)
+        const float det = e.cov[0] * e.cov[2] - e.cov[1] * e.cov[1];
+        float k0 = 0.0f, k1 = 0.0f, k2 = 0.0f, op = 0.0f;
+        if (!(det == 0.0f)) {
+          const float inv = 1.0f / det;
+          k0 = e.cov[2] * inv;
+          k1 = -e.cov[1] * inv;
+          k2 = e.cov[0] * inv;
+          op = e.colour[3];
+        }
+        if (op == 0.0f) continue;
+        const float dx = e.mean[0] - pfx, dy = e.mean[1] - pfy;
+        const float power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
+        if (power > 0.0f) continue;
+        const float v = op * or_expf(power);
+        const float alpha = (v < 0.99f) ? v : 0.99f;
+        if (alpha < 1.0f / 255.0f) continue;
+        const float test_T = T_ * (1.0f - alpha);
+        if (test_T < 0.0001f) break;
+        for (int k = 0; k < 4; ++k) C[k] = C[k] + (e.colour[k] * alpha) * T_;
+        T_ = test_T;
+      }
+      float* o = &L.rgba[4 * ((size_t)(tb.y0 + (float)ly) * L.W + (size_t)(tb.x0 + (float)lx))];
+      for (int k = 0; k < 4; ++k) o[k] = 0.0f + C[k];  // colourFb black, then setPixel
+    }
+  }
+  if (to_render > 0) L.splatted[t] = (uint32_t)to_render;
+}
+
+}  // namespace
+
+struct or_lattice : Lat {};
+
+extern "C" {
+
+or_lattice* or_lattice_create(const float* g64, int64_t n, const or_frame* f) {
+  if (!g64 || !f || n < 1 || f->tile_w <= 0 || f->tile_h <= 0 || f->width % f->tile_w || f->height % f->tile_h)
+    return nullptr;
+  or_lattice* L = new or_lattice();
+  L->W = f->width;
+  L->H = f->height;
+  L->tw = f->tile_w;
+  L->th = f->tile_h;
+  L->tx = f->width / f->tile_w;
+  L->ty = f->height / f->tile_h;
+  L->T = L->tx * L->ty;
+  L->across = (float)L->tx;
+  L->n = n;
+  // calculateMapping (ipu_rasteriser.cpp:164-193) of the 64-float records:
+  // grainsPerTile = ceil(64 n / (numTiles * 64)) in float, fullTiles = floor(n / gpt)
+  const float q = (float)((uint64_t)n * 64u) / ((float)L->T * 64.0f);
+  L->gpt = (int64_t)std::ceil(q);
+  const int64_t full = n / L->gpt;
+  L->rem = n - full * L->gpt;
+  const size_t slots = (size_t)L->base(L->T - 1) + L->vs_n(L->T - 1);
+  L->vs.assign(slots, LG3{});
+  L->zb.assign(slots, LG2{});
+  for (int p = 0; p < 2; ++p) L->chan[p].assign((size_t)L->T * 4 * kChan, LG3{});
+  L->splatted.assign((size_t)L->T, 0u);
+  L->rgba.assign((size_t)L->W * L->H * 4, 0.0f);
+  // applyTileMapping (:199-214): record j on tile j / gpt
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t t = j / L->gpt;
+    std::memcpy(L->vs[(size_t)(L->base((int)t) + (j - t * L->gpt))].f, g64 + 16 * j, 64);
+  }
+  return L;
+}
+
+int or_lattice_step(or_lattice* L, const or_frame* f, int nthreads) {
+  if (!L || !f) return -1;
+  const FrameC c = make_frame(f);
+  const int nt = nthreads_or_default(nthreads);
+  uint64_t d = 0, s = 0, o = 0;
+#pragma omp parallel for schedule(dynamic, 8) num_threads(nt) reduction(+ : d, s, o)
+  for (int t = 0; t < L->T; ++t) {
+    LCount cnt;
+    lat_tile(*L, c, f->scale_div, t, cnt);
+    d += cnt.dropped;
+    s += cnt.send_failed;
+    o += cnt.overrun;
+  }
+  L->dropped = d;
+  L->send_failed = s;
+  L->overrun = o;
+  L->frames++;  // the exchange: this frame's out-channels are the next one's in-channels
+  return 0;
+}
+
+int64_t or_lattice_total_slots(const or_lattice* L) { return L ? (int64_t)L->vs.size() : 0; }
+
+void or_lattice_read(const or_lattice* L, float* rgba, uint32_t* hist, float* slot_gids, uint64_t* counters) {
+  if (!L) return;
+  if (rgba) std::memcpy(rgba, L->rgba.data(), L->rgba.size() * 4);
+  if (hist) std::memcpy(hist, L->splatted.data(), L->splatted.size() * 4);
+  if (slot_gids)
+    for (size_t i = 0; i < L->vs.size(); ++i) slot_gids[i] = L->vs[i].f[15];
+  if (counters) {
+    counters[0] = L->frames;
+    counters[1] = L->dropped;
+    counters[2] = L->send_failed;
+    counters[3] = L->overrun;
+    counters[4] = (uint64_t)L->gpt;
+    counters[5] = (uint64_t)L->rem;
+  }
+}
+
+void or_lattice_destroy(or_lattice* L) { delete L; }
+
+}  // extern "C"

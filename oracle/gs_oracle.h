@@ -108,6 +108,28 @@ uint32_t or_point_splat(const float* xyz, int64_t n, const float* view_rm, const
                         int32_t width, int32_t height, int32_t tile_w, int32_t tile_h,
                         uint8_t* image, uint32_t* hist, int nthreads);
 
+
+/* the lattice-migration emulator -- the reference's per-tile
+ * codelet and channel exchange, one call per frame (codelets.cpp:143-641,
+ * ipu_rasteriser.cpp:164-420, edge_builder.cpp:15-84).  Requires
+ * width % tile_w == 0 and height % tile_h == 0 (the reference's macros).
+ * Choices where the reference is undefined (unpinned): never-written memory
+ * (padding slots, extra storage, in-channels before the first exchange, the
+ * z-buffer) reads as zeros; `directions` outside the guard band are all false;
+ * float -> unsigned of negative / NaN tile indices saturates to 0; z-buffer
+ * reads past a tile's capacity (the last tile's is 600 entries shorter) are
+ * empty records; the six workers of a tile do not race.  NULL on bad input. */
+typedef struct or_lattice or_lattice;
+or_lattice* or_lattice_create(const float* g64, int64_t n, const or_frame* f);
+int or_lattice_step(or_lattice* L, const or_frame* f, int nthreads);
+int64_t or_lattice_total_slots(const or_lattice* L);
+/* rgba: width x height x 4 row-major; hist: the splatted counter per tile;
+ * slot_gids: gid of every vertsIn slot (tile t's slots from t * (gpt + 600));
+ * counters[6]: frames, dropped, send_failed, overrun (last frame), gpt, rem.
+ * Any pointer may be NULL. */
+void or_lattice_read(const or_lattice* L, float* rgba, uint32_t* hist, float* slot_gids, uint64_t* counters);
+void or_lattice_destroy(or_lattice* L);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,6 +100,14 @@ def lib():
         L.or_render.argtypes = [_FP, C.c_int64, C.POINTER(Frame), _FP, C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.POINTER(Stats), C.c_int]
         L.or_point_splat.restype = C.c_uint32
         L.or_point_splat.argtypes = [_FP, C.c_int64, _FP, _FP, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.c_int]
+        L.or_lattice_create.restype = C.c_void_p
+        L.or_lattice_create.argtypes = [_FP, C.c_int64, C.POINTER(Frame)]
+        L.or_lattice_step.restype = C.c_int
+        L.or_lattice_step.argtypes = [C.c_void_p, C.POINTER(Frame), C.c_int]
+        L.or_lattice_total_slots.restype = C.c_int64
+        L.or_lattice_total_slots.argtypes = [C.c_void_p]
+        L.or_lattice_read.argtypes = [C.c_void_p, _FP, C.POINTER(C.c_uint32), _FP, C.POINTER(C.c_uint64)]
+        L.or_lattice_destroy.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -195,3 +203,45 @@ def point_splat(xyz, view_rm, proj_rm, width, height, tile_w, tile_h, nthreads: 
         hist.ctypes.data_as(C.POINTER(C.c_uint32)), nthreads,
     )
     return img, hist, int(cnt)
+
+
+class Lattice:
+    """The reference's multi-frame lattice migration, one
+    step() per frame: or_lattice_* in gs_oracle.cpp."""
+
+    def __init__(self, g64, frame: Frame):
+        a = _g(g64)
+        self._keep = a
+        self.width, self.height = frame.width, frame.height
+        self.T = (frame.width // frame.tile_w) * (frame.height // frame.tile_h)
+        self.h = lib().or_lattice_create(a.ctypes.data_as(_FP), a.shape[0], C.byref(frame))
+        if not self.h:
+            raise ValueError("or_lattice_create: invalid lattice configuration")
+        self.total_slots = int(lib().or_lattice_total_slots(self.h))
+
+    def step(self, frame: Frame, nthreads: int = 0):
+        assert lib().or_lattice_step(self.h, C.byref(frame), nthreads) == 0
+
+    def read(self):
+        """dict(rgba (H, W, 4), hist (T,), slots (gid per vertsIn slot),
+        frames, dropped, send_failed, overrun, gpt, rem)."""
+        rgba = np.zeros((self.height, self.width, 4), np.float32)
+        hist = np.zeros(self.T, np.uint32)
+        slots = np.zeros(self.total_slots, np.float32)
+        cnt = np.zeros(6, np.uint64)
+        lib().or_lattice_read(self.h, rgba.ctypes.data_as(_FP), hist.ctypes.data_as(C.POINTER(C.c_uint32)),
+                              slots.ctypes.data_as(_FP), cnt.ctypes.data_as(C.POINTER(C.c_uint64)))
+        out = {"rgba": rgba, "hist": hist, "slots": slots}
+        out.update({k: int(v) for k, v in zip(("frames", "dropped", "send_failed", "overrun", "gpt", "rem"), cnt)})
+        return out
+
+    def close(self):
+        if self.h:
+            lib().or_lattice_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

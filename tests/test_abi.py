@@ -47,7 +47,7 @@ def test_abi_version_and_config_defaults(built):
     from gaussian_splat_ipu_amd import _lib
 
     L = _lib.lib()
-    assert L.gs_abi_version() == 6
+    assert L.gs_abi_version() == 7
     cfg = _lib.Config()
     assert L.gs_config_init(ctypes.byref(cfg)) == 0
     # tile_config.hpp:5-15 and codelets.cpp:622
@@ -68,6 +68,20 @@ def test_create_rejects_bad_config_without_touching_the_device(built):
     assert rc == _lib.GS_EINVAL
     assert "invalid configuration" in _lib.last_error()
     assert L.gs_render(None) == _lib.GS_EINVAL
+    # the lattice emulator needs a whole tile grid, one band, one device
+    import numpy as np
+
+    g = np.zeros(4, dtype=np.dtype((np.void, 64)))
+    gp = g.ctypes.data_as(ctypes.POINTER(_lib.Gaussian3D))
+    for w, h_, bc, ngpu in [(1920, 1080, 1, 0), (1280, 720, 2, 0), (1280, 720, 1, 2)]:
+        L.gs_config_init(ctypes.byref(cfg))
+        cfg.width, cfg.height, cfg.tile_width, cfg.tile_height = w, h_, 16, 16
+        cfg.band_count, cfg.num_gpus = bc, ngpu
+        cfg.flags = _lib.GS_FLAG_LATTICE
+        rc = L.gs_create(gp, 4, ctypes.byref(cfg), ctypes.byref(h))
+        assert rc == _lib.GS_EINVAL, (w, h_, bc, ngpu)
+        assert "lattice" in _lib.last_error().lower()
+    assert L.gs_get_lattice_stats(None, None) == _lib.GS_EINVAL
 
 
 def test_cpp_wrapper_compiles_and_links(built, tmp_path):
@@ -87,8 +101,8 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
         "  splat::gs_check(gs_config_init(&c), \"init\");\n"
         "  splat::GpuSplatter* p = nullptr;  // the class is instantiable\n"
         "  (void)p;\n"
-        "  std::printf(\"%d %u %zu %zu %zu\\n\", gs_abi_version(), c.tile_width, sizeof(gs_config),\n"
-        "              sizeof(gs_frame_stats), sizeof(gs_comm_id));\n"
+        "  std::printf(\"%d %u %zu %zu %zu %zu\\n\", gs_abi_version(), c.tile_width, sizeof(gs_config),\n"
+        "              sizeof(gs_frame_stats), sizeof(gs_comm_id), sizeof(gs_lattice_stats));\n"
         "  return 0;\n"
         "}\n"
     )
@@ -97,11 +111,12 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
                     "-L", libdir, "-lgsplat", f"-Wl,-rpath,{libdir}"], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    assert int(out[0]) == 6
+    assert int(out[0]) == 7
     # the ctypes mirrors have the C layouts
     assert int(out[2]) == ctypes.sizeof(_lib.Config)
     assert int(out[3]) == ctypes.sizeof(_lib.FrameStats)
     assert int(out[4]) == ctypes.sizeof(_lib.CommId) == 128
+    assert int(out[5]) == ctypes.sizeof(_lib.LatticeStats)
 
 
 def test_balanced_bands_matches_the_python_rule(built):
