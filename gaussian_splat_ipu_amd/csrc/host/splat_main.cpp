@@ -3,7 +3,7 @@
 //
 //   splat --input scene.ply [--device cpu|gpu] [--log-level info] [--ui-port 0]
 //         [--gpus N] [--width 1280 --height 720 --tile-width 32 --tile-height 20]
-//         [--frames 1] [--scale-div 0.1] [--out test.png]
+//         [--frames 1] [--scale-div 0.1] [--out test.png] [--lattice]
 //
 // Same flags and flow as the reference: load the PLY, centre + negate z,
 // build the Gaussians, set up the camera (lookAtBoundingBox, frustum fitted to
@@ -12,7 +12,10 @@
 //                 cpu_rasteriser.cpp:9-92), the reference's default device;
 //   --device gpu  the Gaussian frame path on the MI355X (gs_render; "ipu" is
 //                 accepted as an alias), --gpus N: N devices as one row-band
-//                 group (one all-gather per frame inside gs_render).
+//                 group (one all-gather per frame inside gs_render);
+//                 --lattice: every frame is one step of the emulated IPU
+//                 lattice (GS_FLAG_LATTICE), the reference's own transient
+//                 frames, instead of the converged single-frame binning.
 // Without --ui-port the loop runs --frames frames (the reference: exactly one,
 // splat.cpp:322) and logs "Splat time: {} points/sec: {}" (:318).  With
 // --ui-port (built with REMOTE_UI=1) it serves one remote-UI client
@@ -43,6 +46,7 @@ namespace {
 struct Args {
   std::string input, device = "cpu", log_level = "info", out = "test.png";
   int ui_port = 0, frames = 1, gpus = 0;
+  bool lattice = false;
   uint32_t width = 1280, height = 720, tw = 32, th = 20;
   float scale_div = -1.0f;  // default: lambda1 / 10 = 0.1 (InterfaceServer.hpp:238, splat.cpp:262)
 };
@@ -51,7 +55,7 @@ void usage() {
   std::printf(
       "splat --input <file.ply|file.xyz> [--device cpu|gpu] [--log-level info] [--ui-port 0]\n"
       "      [--gpus N] [--width 1280] [--height 720] [--tile-width 32] [--tile-height 20]\n"
-      "      [--frames 1] [--scale-div 0.1] [--out test.png]\n");
+      "      [--frames 1] [--scale-div 0.1] [--out test.png] [--lattice]\n");
 }
 
 bool parse(int argc, char** argv, Args& a) {
@@ -91,6 +95,8 @@ bool parse(int argc, char** argv, Args& a) {
       a.scale_div = (float)std::atof(val());
     } else if (k == "--out") {
       a.out = val();
+    } else if (k == "--lattice") {
+      a.lattice = true;
     } else if (k == "--no-amp") {
       // accepted for compatibility (splat.cpp:34-35), no effect
     } else {
@@ -189,6 +195,7 @@ class GpuDevice {
       cfg.num_gpus = (uint32_t)a.gpus;
       for (int k = 0; k < a.gpus && k < GS_MAX_GPUS; ++k) cfg.device_ids[k] = k;
     }
+    if (a.lattice) cfg.flags |= GS_FLAG_LATTICE;
     splat::gs_check(gs_create(g.data(), g.size(), &cfg, &r_), "gs_create");
   }
   ~GpuDevice() { gs_destroy(r_); }

@@ -124,3 +124,37 @@ def test_lattice_converges_to_the_gpu_frame_path(pc12):
     assert_same_bits(s.get_rgba(), ref.get_rgba(), "converged lattice vs frame path")
     h, rh = s.get_histogram(), ref.get_histogram()
     np.testing.assert_array_equal(h[rh > 0], rh[rh > 0])
+
+
+def test_render_server_lattice_mode(built, tmp_path):
+    """bin/splat --lattice: the render server's frames are the emulated IPU's
+    (every frame one lattice step); after 5 frames its test.png equals the
+    oracle lattice's fifth frame."""
+    import os
+    import struct
+    import subprocess
+    import zlib
+
+    from conftest import ROOT
+    from gaussian_splat_ipu_amd import camera, scene
+    from oracle import oracle as O
+
+    exe = os.path.join(ROOT, "gaussian_splat_ipu_amd", "bin", "splat")
+    out = tmp_path / "test.png"
+    r = subprocess.run([exe, "--input", PC12, "--device", "gpu", "--lattice", "--out", str(out), "--frames", "5"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    data = out.read_bytes()
+    w, h = struct.unpack(">II", data[16:24])
+    idat = data[data.index(b"IDAT") + 4:data.index(b"IEND") - 8]
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + w * 3)[:, 1:].reshape(h, w, 3)
+    g, bb = scene.prepare_scene(scene.load_ply(PC12))
+    view, proj = camera.headless(bb, 1280, 720)
+    f = O.make_frame(view, proj, 1280, 720, 32, 20, camera.FOV_DEFAULT, 0.1)
+    L = O.Lattice(g, f)
+    for _ in range(5):
+        L.step(f)
+    rgba = L.read()["rgba"]
+    bgr = np.zeros((h * w, 3), np.uint8)
+    O.lib().or_pack_bgr8(rgba.ctypes.data_as(O._FP), h * w, bgr.ctypes.data_as(O.C.POINTER(O.C.c_uint8)))
+    np.testing.assert_array_equal(raw[:, :, ::-1].reshape(-1, 3), bgr)
