@@ -36,6 +36,11 @@
 #ifndef GS_BLEND_PIXEL_MASKS
 #define GS_BLEND_PIXEL_MASKS 1
 #endif
+// blend: per-lane masks read back from a VGPR table of the ballots with
+// ds_bpermute (1) or selected from them with compare / select chains (0)
+#ifndef GS_BLEND_PERMUTE_MASKS
+#define GS_BLEND_PERMUTE_MASKS 1
+#endif
 
 namespace gsk {
 namespace {
@@ -366,8 +371,11 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
     // without reading their rectangles, so nothing else needs writing
     bool culled = false;
     if (i < fp.n) {
+      // both loads in one memory round trip (the test needs the mean unless
+      // the slot is empty)
       const float4 sg = b.scale_gid[i];
-      culled = !(sg.w <= 0.0f) && band_culled_fast<P2>(fp, b.mean[i], sg);
+      const float4 mean = b.mean[i];
+      culled = !(sg.w <= 0.0f) && band_culled_fast<P2>(fp, mean, sg);
     }
     if (__syncthreads_count(i < fp.n && !culled) == 0) {
       if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = 0u;
@@ -1846,6 +1854,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// v_writelane_b32 x2: lanes L and L + 1 of v take the wave-uniform words lo,
+// hi -- a ballot's two halves.  The s_nop gives the two wait states a VALU
+// read of an SGPR needs after the VALU compare that wrote it (the compiler
+// inserts them for its own code, not inside inline asm).
+template <int L>
+__device__ __forceinline__ uint32_t writelane2(uint32_t v, uint32_t lo, uint32_t hi) {
+  asm("s_nop 1\n\tv_writelane_b32 %0, %1, %3\n\tv_writelane_b32 %0, %2, %4"
+      : "+v"(v)
+      : "s"(lo), "s"(hi), "n"(L), "n"(L + 1));
+  return v;
+}
+
+// The ballots of spans [lo, lo + sp] over positions C = 0 .. N - 1, written
+// into lanes 2 (B + C) (low word) and 2 (B + C) + 1 (high word) of tab
+template <int B, int C, int N>
+struct BallotTab {
+  __device__ __forceinline__ static void run(uint32_t& tab, int lo, int sp) {
+    if constexpr (C < N) {
+      const unsigned long long bc = ballot64((uint32_t)(C - lo) <= (uint32_t)sp);
+      tab = writelane2<2 * (B + C)>(tab, (uint32_t)bc, (uint32_t)(bc >> 32));
+      BallotTab<B, C + 1, N>::run(tab, lo, sp);
+    }
+  }
+};
+
 // Per-pixel blend state: position, transmittance, accumulated colour, and
 // whether the pixel has saturated (the reference's `break`).
 struct Px {
@@ -2112,6 +2145,22 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
       const int xlo = rok ? (rx0 - bx) >> SH : 0x40000000, xsp = rok ? ((rx1 - bx) >> SH) - xlo : 0;
       const int ylo = rok ? (ry0 - by) >> SH : 0x40000000, ysp = rok ? ((ry1 - by) >> SH) - ylo : 0;
       const int mycol = (lx - q_x) >> SH, myrow = (ly - q_y) >> SH;
+#if GS_BLEND_PERMUTE_MASKS
+      // the ballots (wave-uniform) go into one VGPR, lanes 2c / 2c + 1 for
+      // column c and 2 (NC + w) / + 1 for row w; each lane then reads its
+      // column's and row's words back with ds_bpermute (4 crossbar reads
+      // instead of a select chain of 4 VALU per ballot)
+      static_assert(2 * (NC + NR) <= 64, "one VGPR holds every ballot");
+      uint32_t tab = 0u;
+      BallotTab<0, 0, NC>::run(tab, xlo, xsp);
+      BallotTab<NC, 0, NR>::run(tab, ylo, ysp);
+      const int ac = 8 * mycol, ar = 8 * (NC + myrow);  // byte addresses of the lanes' words
+      const uint32_t mcl = (uint32_t)__builtin_amdgcn_ds_bpermute(ac, (int)tab);
+      const uint32_t mch = (uint32_t)__builtin_amdgcn_ds_bpermute(ac + 4, (int)tab);
+      const uint32_t mrl = (uint32_t)__builtin_amdgcn_ds_bpermute(ar, (int)tab);
+      const uint32_t mrh = (uint32_t)__builtin_amdgcn_ds_bpermute(ar + 4, (int)tab);
+      m = ((unsigned long long)(mch & mrh) << 32) | (unsigned long long)(mcl & mrl);
+#else
       unsigned long long mc = 0ull, mr = 0ull;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -2124,6 +2173,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
         mr = (myrow == w) ? br : mr;
       }
       m = mc & mr;
+#endif
     } else {
       int cx = q_x, cy = q_y;
 #pragma unroll
