@@ -523,6 +523,11 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
       gs_renderer* c = nullptr;
       if ((rc = gsr::create(gs, n, &c2, share, &c)) != GS_OK) return fail(rc);
       m.slot.push_back(c);
+      if (c->bin_global) {  // see gsr::create: not inside row bands
+        set_error("gs_create: the row-band group needs the chunked binning (at most 81 920 tiles in the "
+                  "frame and ~16.7 M Gaussians)");
+        return fail(GS_EINVAL);
+      }
       if (!share) share = c;
     }
     if ((rc = set_dev(m.device)) != GS_OK) return fail(rc);

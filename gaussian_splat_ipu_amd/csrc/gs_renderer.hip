@@ -422,6 +422,10 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     set_error("gs_create: invalid configuration");
     return GS_EINVAL;
   }
+  if ((cfg->flags & GS_FLAG_BIN_GLOBAL) && (cfg->band_count > 1 || cfg->band_row_end > cfg->band_row_begin)) {
+    set_error("gs_create: the global-atomic binning (GS_FLAG_BIN_GLOBAL) is not supported inside a row band");
+    return GS_EINVAL;
+  }
   const bool lattice = (cfg->flags & GS_FLAG_LATTICE) != 0;
   if (lattice && (cfg->width % cfg->tile_width || cfg->height % cfg->tile_height || cfg->band_count != 1 ||
                   cfg->band_row_end > cfg->band_row_begin || (cfg->flags & GS_FLAG_BAND_INTERLEAVED) || n == 0 ||
@@ -610,6 +614,16 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     }
   }
   r->stats.bin_global = (uint32_t)r->bin_global;
+  // The global-atomic binning is verified on whole frames only: inside row
+  // bands it produced wrong frames (and a faulting sort) in a process where a
+  // chunked renderer had run before; until that is understood a band
+  // renderer refuses it (a band's tile grid always fits the chunked path up
+  // to ~16.7 M Gaussians).
+  if (r->bin_global && r->band_nrows < r->tiles_y) {
+    set_error("gs_create: the global-atomic binning (GS_FLAG_BIN_GLOBAL, or more than ~16.7 M Gaussians) is "
+              "not supported inside a row band");
+    return fail(GS_EINVAL);
+  }
 
   // lazy big lists (gs_kernels.hip, kLazyPrefix): with the chunked binning
   // and 16x16 tiles (four 8x8 blend waves per tile); per tile 9 u32 + the

@@ -547,33 +547,3 @@ def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
         s.execute()  # big lists through the big-list sample sort
         _assert_parity(s, f, a)
     assert ref["stats"]["n_pairs"] > 0
-
-
-@pytest.mark.skip(reason="faults the GPU with band rows + global binning: under investigation")
-@pytest.mark.parametrize("band_cull", [False, True])
-def test_global_binning_in_explicit_bands(built, band_cull):
-    """The global-atomic binning path (GS_FLAG_BIN_GLOBAL) inside explicit
-    row bands, with and without the band cull: every band equals the oracle's
-    band (RGBA bits, BGR8, histogram)."""
-    from gaussian_splat_ipu_amd import camera, scene
-    from gaussian_splat_ipu_amd.splatter import GpuSplatter
-    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
-    from oracle import oracle as O
-
-    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=200_000, seed=1, sh_degree=0)))
-    W, H = 1920, 1080
-    view, proj = camera.headless(bb, W, H)
-    fb = TiledFramebuffer(W, H, 16, 16)
-    for ty0, ty1 in [(0, 18), (30, 36), (60, 68)]:
-        s = GpuSplatter(g, fb, device=0, band_rows=(ty0, ty1), band_pad_rows=ty1 - ty0, band_cull=band_cull,
-                        bin_global=True)
-        s.set_view_wire(view)
-        s.set_projection_wire(proj)
-        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
-        s.execute()
-        s.execute()
-        ref = O.render(g, O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1)))
-        assert_same_bits(s.get_rgba(), ref["rgba"], f"band {ty0}-{ty1}")
-        np.testing.assert_array_equal(s.get_frame_buffer(), ref["bgr"])
-        np.testing.assert_array_equal(s.get_histogram(), ref["hist"])
-        s.close()

@@ -29,7 +29,6 @@ def main():
     ap.add_argument("--contiguous", action="store_true")
     ap.add_argument("--balanced", action="store_true", help="work-balanced contiguous bands (bench.py's N > 1 default)")
     ap.add_argument("--no-cull", action="store_true")
-    ap.add_argument("--bin-global", action="store_true", help="bands bin with the global-atomic path")
     ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
     ap.add_argument("--config5", action="store_true", help="bench.py --config5's scene, 4K, orbit views")
     a = ap.parse_args()
@@ -76,7 +75,7 @@ def main():
             for f in range(a.inflight):
                 if bands is not None:
                     s = GpuSplatter(g, fb, device=0, band_rows=bands[r], band_pad_rows=pad, profile=(f == 0),
-                                    band_cull=not a.no_cull, write_rgba=False, bin_global=a.bin_global)
+                                    band_cull=not a.no_cull, write_rgba=False)
                 else:
                     s = GpuSplatter(g, fb, device=0, band_index=r, band_count=N, profile=(f == 0),
                                     band_interleaved=(N > 1 and not a.contiguous),
