@@ -190,7 +190,7 @@ def main():
     # ------------------------------------------------------------ renderers
     split = a.split if a.split > 1 else world
     if group:
-        if world > 1 or a.gather:
+        if world > 1 or (a.gather and a.split <= 1):  # RCCL (--split S emulates S bands with copies)
             if world > 1:
                 from gaussian_splat_ipu_amd import dist as gdist
 
