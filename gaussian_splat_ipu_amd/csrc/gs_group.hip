@@ -523,11 +523,6 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
       gs_renderer* c = nullptr;
       if ((rc = gsr::create(gs, n, &c2, share, &c)) != GS_OK) return fail(rc);
       m.slot.push_back(c);
-      if (c->bin_global) {  // see gsr::create: not inside row bands
-        set_error("gs_create: the row-band group needs the chunked binning (at most 81 920 tiles in the "
-                  "frame and ~16.7 M Gaussians)");
-        return fail(GS_EINVAL);
-      }
       if (!share) share = c;
     }
     if ((rc = set_dev(m.device)) != GS_OK) return fail(rc);
@@ -536,6 +531,7 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
       return fail(gsr::hip_fail(e, "hipStreamCreate(comm)"));
     if ((e = hipMalloc(&m.d_send, (size_t)g->F * g->slot_cap)) != hipSuccess)
       return fail(gsr::hip_fail(e, "hipMalloc(all-gather send)"));
+    gsr::poison(m.d_send, (size_t)g->F * g->slot_cap, "send");
     if ((e = hipMalloc(&m.d_recv, (size_t)g->F * g->world * g->slot_cap)) != hipSuccess)
       return fail(gsr::hip_fail(e, "hipMalloc(all-gather recv)"));
     if ((e = hipMemset(m.d_recv, 0, (size_t)g->F * g->world * g->slot_cap)) != hipSuccess)

@@ -109,6 +109,7 @@ struct gs_renderer {
 namespace gsr {
 
 int hip_fail(hipError_t e, const char* what);
+void poison(void* p, size_t bytes, const char* name);  // GSPLAT_DEBUG_POISON (gs_renderer.hip)
 
 #define GS_HIP(call)                                        \
   do {                                                      \

@@ -440,7 +440,10 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
       sum += c[j];
       mx = max(mx, c[j]);
       const int cl = sort_class(c[j]);
-      q += cl == 0 ? 1u : (cl == 1 ? (1u << 10) : (1u << 20));  // small queue: empty tiles too
+      // small queue: empty tiles too -- but not the round's slots past the
+      // last tile (counted, they made the small queue longer than the tiles
+      // written to it, and the sort read tile ids past its end)
+      if (i0 + j < T) q += cl == 0 ? 1u : (cl == 1 ? (1u << 10) : (1u << 20));
     }
     unsigned long long inc = sum;
     uint32_t qinc = q;

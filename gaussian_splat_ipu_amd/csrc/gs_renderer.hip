@@ -36,6 +36,21 @@ int select_device(gs_renderer* r) {
   return GS_OK;
 }
 
+// GSPLAT_DEBUG_POISON=1: every device buffer is filled with 0xA5 bytes when it
+// is allocated (before any initialisation the renderer does itself), so a
+// kernel that reads memory no earlier stage of the frame wrote gives a
+// different frame than in a fresh process (tests/test_gpu_poison.py).  A
+// comma-separated list of buffer names poisons just those.
+void poison(void* p, size_t bytes, const char* name) {
+  const char* ev = std::getenv("GSPLAT_DEBUG_POISON");
+  if (!p || !bytes || !ev || !*ev || std::strcmp(ev, "0") == 0) return;
+  if (std::strcmp(ev, "1") != 0) {
+    const std::string list = std::string(",") + ev + ",";
+    if (list.find(std::string(",") + name + ",") == std::string::npos) return;
+  }
+  (void)hipMemset(p, 0xA5, bytes);
+}
+
 void free_pairs(gs_renderer* r) {
   if (r->d_pairs) (void)hipFree(r->d_pairs);
   r->d_pairs = nullptr;
@@ -95,6 +110,7 @@ int alloc_pairs(gs_renderer* r, uint64_t cap) {
   const size_t bytes = (size_t)cap * (8 + 8 + 4) + n_bk * 8 + n_items * 4 + n_bk * 12 +
                        ((size_t)r->n_tiles + 1) * 4;
   GS_HIP(hipMalloc(&r->d_pairs, bytes));
+  poison(r->d_pairs, bytes, "pairs");
   r->pair_cap = cap;
   char* p = (char*)r->d_pairs;
   r->buf.pairs = (unsigned long long*)p;
@@ -422,10 +438,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     set_error("gs_create: invalid configuration");
     return GS_EINVAL;
   }
-  if ((cfg->flags & GS_FLAG_BIN_GLOBAL) && (cfg->band_count > 1 || cfg->band_row_end > cfg->band_row_begin)) {
-    set_error("gs_create: the global-atomic binning (GS_FLAG_BIN_GLOBAL) is not supported inside a row band");
-    return GS_EINVAL;
-  }
   const bool lattice = (cfg->flags & GS_FLAG_LATTICE) != 0;
   if (lattice && (cfg->width % cfg->tile_width || cfg->height % cfg->tile_height || cfg->band_count != 1 ||
                   cfg->band_row_end > cfg->band_row_begin || (cfg->flags & GS_FLAG_BAND_INTERLEAVED) || n == 0 ||
@@ -566,6 +578,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   const size_t nblk = (nn + 255) / 256;
   if ((e = hipMalloc(&r->d_gauss, nn * (48 + 8 + 8 + 8 + 4) + nblk * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(per-Gaussian)"));
+  poison(r->d_gauss, nn * (48 + 8 + 8 + 8 + 4) + nblk * 4, "gauss");
   r->buf.rec = (float4*)r->d_gauss;
   r->buf.rec_tail = (float2*)((char*)r->d_gauss + nn * 48);
   r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 56);
@@ -576,11 +589,13 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   const size_t T = (size_t)std::max(r->n_tiles, 1);
   r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
   if ((e = hipMalloc(&r->d_zero, r->zero_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(zero)"));
+  poison(r->d_zero, r->zero_bytes, "zero");
   r->buf.counters = (uint32_t*)r->d_zero;
   r->buf.tile_count = (uint32_t*)r->d_zero + 16;
   const size_t n_agg = (T + 63) / 64;
   if ((e = hipMalloc(&r->d_tiles, (T + 1 + 4 * T) * 4 + n_agg * 32 + 16)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(tiles)"));
+  poison(r->d_tiles, (T + 1 + 4 * T) * 4 + n_agg * 32 + 16, "tiles");
   r->buf.tile_start = (uint32_t*)r->d_tiles;
   r->buf.tile_cursor = r->buf.tile_start + T + 1;
   r->buf.big_tiles = r->buf.tile_cursor + T;
@@ -610,20 +625,11 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       r->n_chunks = (int)((n + cs - 1) / cs);
       if ((e = hipMalloc(&r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
+      poison(r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4, "chunk");
       r->buf.chunk_off = (uint32_t*)r->d_chunk;
     }
   }
   r->stats.bin_global = (uint32_t)r->bin_global;
-  // The global-atomic binning is verified on whole frames only: inside row
-  // bands it produced wrong frames (and a faulting sort) in a process where a
-  // chunked renderer had run before; until that is understood a band
-  // renderer refuses it (a band's tile grid always fits the chunked path up
-  // to ~16.7 M Gaussians).
-  if (r->bin_global && r->band_nrows < r->tiles_y) {
-    set_error("gs_create: the global-atomic binning (GS_FLAG_BIN_GLOBAL, or more than ~16.7 M Gaussians) is "
-              "not supported inside a row band");
-    return fail(GS_EINVAL);
-  }
 
   // lazy big lists (gs_kernels.hip, kLazyPrefix): with the chunked binning
   // and 16x16 tiles (four 8x8 blend waves per tile); per tile 9 u32 + the
@@ -632,6 +638,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     const size_t TT = (size_t)r->t_cap;
     if ((e = hipMalloc(&r->d_lazy, TT * (9 * 4 + 4 * 6 * 64 * 4))) != hipSuccess)
       return fail(hip_fail(e, "hipMalloc(lazy big lists)"));
+    poison(r->d_lazy, TT * (9 * 4 + 4 * 6 * 64 * 4), "lazy");
     uint32_t* u = (uint32_t*)r->d_lazy;
     r->buf.tile_big = u;
     r->buf.big_len = u + TT;
@@ -653,6 +660,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->bgr_bytes = px * 3;
   if ((e = hipMalloc(&r->d_out, px * 16 + (r->bgr_bytes + 15) / 16 * 16)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(framebuffer)"));
+  poison(r->d_out, px * 16 + (r->bgr_bytes + 15) / 16 * 16, "out");
   r->buf.rgba = (float4*)r->d_out;
   r->buf.bgr = (uint8_t*)r->d_out + px * 16;
   r->own_bgr = r->last_bgr = r->buf.bgr;

@@ -82,14 +82,6 @@ def test_create_rejects_bad_config_without_touching_the_device(built):
         assert rc == _lib.GS_EINVAL, (w, h_, bc, ngpu)
         assert "lattice" in _lib.last_error().lower()
     assert L.gs_get_lattice_stats(None, None) == _lib.GS_EINVAL
-    # global-atomic binning is refused inside a row band
-    for bc, rows in [(2, (0, 0)), (1, (3, 9))]:
-        L.gs_config_init(ctypes.byref(cfg))
-        cfg.band_count = bc
-        cfg.band_row_begin, cfg.band_row_end = rows
-        cfg.flags = _lib.GS_FLAG_BIN_GLOBAL
-        assert L.gs_create(gp, 4, ctypes.byref(cfg), ctypes.byref(h)) == _lib.GS_EINVAL
-        assert "row band" in _lib.last_error()
 
 
 def test_cpp_wrapper_compiles_and_links(built, tmp_path):

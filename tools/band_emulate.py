@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--contiguous", action="store_true")
     ap.add_argument("--balanced", action="store_true", help="work-balanced contiguous bands (bench.py's N > 1 default)")
     ap.add_argument("--no-cull", action="store_true")
+    ap.add_argument("--bin-global", action="store_true", help="the bands bin with global atomics")
     ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
     ap.add_argument("--config5", action="store_true", help="bench.py --config5's scene, 4K, orbit views")
     a = ap.parse_args()
@@ -75,11 +76,13 @@ def main():
             for f in range(a.inflight):
                 if bands is not None:
                     s = GpuSplatter(g, fb, device=0, band_rows=bands[r], band_pad_rows=pad, profile=(f == 0),
-                                    band_cull=not a.no_cull, write_rgba=False)
+                                    band_cull=not a.no_cull, write_rgba=False,
+                                    bin_global=a.bin_global)
                 else:
                     s = GpuSplatter(g, fb, device=0, band_index=r, band_count=N, profile=(f == 0),
                                     band_interleaved=(N > 1 and not a.contiguous),
-                                    band_cull=(N > 1 and not a.no_cull), write_rgba=False)
+                                    band_cull=(N > 1 and not a.no_cull), write_rgba=False,
+                                    bin_global=a.bin_global)
                 s.set_view_wire(view)
                 s.set_projection_wire(proj)
                 s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
