@@ -631,7 +631,8 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
 }
 
 // 64 tiles per workgroup (one per lane), the chunk rows split over 16 waves
-// (n_chunks <= 256: at most 16 rows per wave, held in registers).
+// (n_chunks <= 256: at most 16 rows per wave, held in registers; a larger
+// scene's rows past a wave's 16th are read twice, summed then rewritten).
 __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffers b) {
   __shared__ uint32_t wsum[16][64], whsum[16][64];
   const int T = fp.n_tiles, NC = fp.n_chunks;
@@ -651,6 +652,11 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
     sum += v[k];
     hsum += fp.pair_cull ? e >> 16 : e;
   }
+  for (int cc = c0 + 16; cc < c1; ++cc) {  // (n_chunks > 256 only)
+    const uint32_t e = t < T ? b.chunk_off[(size_t)cc * T + t] : 0u;
+    sum += e & lo_mask;
+    hsum += fp.pair_cull ? e >> 16 : e;
+  }
   wsum[wave][lane] = sum;
   whsum[wave][lane] = hsum;
   __syncthreads();
@@ -661,6 +667,12 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
     for (int k = 0; k < 16; ++k) {
       if (c0 + k < c1) b.chunk_off[(size_t)(c0 + k) * T + t] = run;
       run += v[k];
+    }
+    for (int cc = c0 + 16; cc < c1; ++cc) {
+      uint32_t* const p = b.chunk_off + (size_t)cc * T + t;
+      const uint32_t e = *p & lo_mask;
+      *p = run;
+      run += e;
     }
     if (wave == 15) b.tile_count[t] = run;
   }

@@ -611,13 +611,15 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (!r->bin_global && n > 0 && r->n_tiles > 0) {
     size_t cs = std::max<size_t>(4096, (n + 255) / 256);
     cs = std::min<size_t>(cs, 65535);
-    // gs_colscan_kernel holds at most 16 chunk rows per wave (16 waves): 256
-    // chunks of <= 65535 Gaussians, i.e. scenes up to ~16.7 M.  Larger scenes
-    // bin with the global-atomic path instead of failing.  (GSPLAT_BIN_MAX_CHUNKS
-    // lowers the limit so the fallback can be tested at small N.)
-    int max_chunks = 256;
-    if (const char* ev = std::getenv("GSPLAT_BIN_MAX_CHUNKS")) max_chunks = std::max(1, std::min(256, std::atoi(ev)));
-    if ((n + cs - 1) / cs > (size_t)max_chunks) {
+    // chunks of <= 65535 Gaussians (16-bit LDS counters): scenes beyond
+    // ~16.7 M take more than 256 chunks, which gs_colscan_kernel handles with a
+    // second read of the extra rows.  Test hooks: GSPLAT_BIN_CHUNK_SIZE sets
+    // the chunk size (many chunks at a small N); GSPLAT_BIN_MAX_CHUNKS sends
+    // scenes of more chunks to the global-atomic path.
+    if (const char* ev = std::getenv("GSPLAT_BIN_CHUNK_SIZE")) cs = (size_t)std::max(64, std::min(65535, std::atoi(ev)));
+    size_t max_chunks = SIZE_MAX;
+    if (const char* ev = std::getenv("GSPLAT_BIN_MAX_CHUNKS")) max_chunks = (size_t)std::max(1, std::atoi(ev));
+    if ((n + cs - 1) / cs > max_chunks) {
       r->bin_global = 1;
     } else {
       if ((e = gsk::init_kernel_attributes()) != hipSuccess) return fail(hip_fail(e, "hipFuncSetAttribute"));

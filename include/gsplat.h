@@ -157,8 +157,7 @@ typedef struct gs_frame_stats {
                               the pairs culled by the alpha box (= P with
                               GS_FLAG_NO_PAIR_CULL)                   */
   uint32_t bin_global;    /* ABI 5: 1 = the global-atomic binning path (tile
-                             grids beyond one CU's LDS, scenes beyond 256
-                             binning chunks ~ 16.7 M, or GS_FLAG_BIN_GLOBAL) */
+                             grids beyond one CU's LDS, or GS_FLAG_BIN_GLOBAL) */
   uint32_t reserved0;
 } gs_frame_stats;
 

@@ -228,10 +228,33 @@ def test_overflow_is_sticky_across_async_frames(built):
     s.close()
 
 
-def test_binning_chunk_limit_falls_back_to_global_atomics(built, monkeypatch):
-    """Scenes beyond 256 binning chunks (~16.7 M Gaussians) bin with the
-    global-atomic path instead of failing.  GSPLAT_BIN_MAX_CHUNKS lowers the
-    limit so the fallback runs at small N; the frame stays bit-exact."""
+@pytest.mark.parametrize("chunk,pair_cull", [(256, True), (128, True), (256, False)])
+def test_binning_more_than_256_chunks(built, monkeypatch, chunk, pair_cull):
+    """Scenes beyond 256 binning chunks (~16.7 M Gaussians at 65535 per chunk)
+    stay on the chunked binning: gs_colscan_kernel reads a wave's rows past
+    its 16th twice.  GSPLAT_BIN_CHUNK_SIZE shrinks the chunks so 120 k
+    Gaussians make 469 / 938 of them; the frame and the lists stay bit-exact."""
+    from gaussian_splat_ipu_amd import camera, scene
+    from oracle import oracle as O
+
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=120_000, seed=2, sh_degree=0)))
+    view, proj = camera.headless(bb, 1920, 1080)
+    monkeypatch.setenv("GSPLAT_BIN_CHUNK_SIZE", str(chunk))
+    s = _splatter(g, view, proj, 1920, 1080, 16, pair_cull=pair_cull)
+    monkeypatch.delenv("GSPLAT_BIN_CHUNK_SIZE")
+    assert s.stats()["bin_global"] == 0
+    f = O.make_frame(view, proj, 1920, 1080, 16, 16, camera.FOV_DEFAULT, 1.0)
+    ref = O.render(g, f)
+    for _ in range(2):
+        s.execute()
+        _check_frame(s, g, f, ref)
+    s.close()
+
+
+def test_binning_forced_to_global_atomics(built, monkeypatch):
+    """GSPLAT_BIN_MAX_CHUNKS sends a scene of more chunks to the global-atomic
+    binning (the path for tile grids too large for one CU's LDS); the frame
+    stays bit-exact."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
 
