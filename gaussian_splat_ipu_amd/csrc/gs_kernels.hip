@@ -1972,18 +1972,26 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers
   dst[2] = to_u8(o0);
 }
 
-// The records of one 32-bit word of a lane's batch mask (bit k = staged record
-// off + k), two per iteration in list order: their exponentials are
-// independent, the compositing is sequential.  The lane stops as soon as its
-// pixel has saturated (the reference's `break`).
+// The records of a lane's batch mask (bit k = staged record k), two per
+// iteration in list order: their exponentials are independent, the
+// compositing is sequential.  The mask is walked as two 32-bit words (w, then
+// h): a lane moves on to its high word as soon as its low word is used up,
+// inside the same loop, so the wave's iteration count is the largest number of
+// records of any lane, not the largest low-word count plus the largest
+// high-word count (blend 79.0 -> 77.3 us, interleaved A/B, bit-exact).  The
+// lane stops as soon as its pixel has saturated (the reference's `break`).
 template <bool FAST>
-__device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t mw, int off) {
-  while (mw) {
-    const int ja = off + __builtin_ctz(mw);
-    mw &= mw - 1u;
-    const bool two = mw != 0u;
-    const int jb = two ? off + __builtin_ctz(mw) : ja;
-    mw &= mw - 1u;
+__device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t w, uint32_t h) {
+  int off = 0;
+  if (w == 0u) { w = h; h = 0u; off = 32; }  // refill: the high word follows
+  while (w) {
+    const int ja = off + __builtin_ctz(w);
+    w &= w - 1u;
+    if (w == 0u) { w = h; h = 0u; off = 32; }
+    const bool two = w != 0u;
+    const int jb = two ? off + __builtin_ctz(w) : ja;
+    w &= w - 1u;
+    if (w == 0u) { w = h; h = 0u; off = 32; }
     const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
     const float4 b0 = st[0][jb], b1 = st[1][jb], b2 = st[2][jb];
     float pa, pb;
@@ -1991,7 +1999,7 @@ __device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t 
     const float eb = blend_power_exp<FAST>(q, b0, b1, pb);
     blend_composite(q, pa, ea, a1, a2, true);
     blend_composite(q, pb, eb, b1, b2, two);
-    mw = q.done ? 0u : mw;
+    w = q.done ? 0u : w;
   }
 }
 
@@ -2212,11 +2220,9 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
     // Each lane leaves as soon as its own pixel has saturated.
     const uint32_t m_lo = q.done ? 0u : (uint32_t)m, m_hi = (uint32_t)(m >> 32);
     if (fast) {
-      blend_records<true>(q, st, m_lo, 0);
-      blend_records<true>(q, st, q.done ? 0u : m_hi, 32);
+      blend_records<true>(q, st, m_lo, q.done ? 0u : m_hi);
     } else {
-      blend_records<false>(q, st, m_lo, 0);
-      blend_records<false>(q, st, q.done ? 0u : m_hi, 32);
+      blend_records<false>(q, st, m_lo, q.done ? 0u : m_hi);
     }
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
