@@ -90,6 +90,9 @@ STAGE_KERNELS = {
     "sort": ["gs_sort_tiles", "gs_big_prefix", "gs_big_split", "gs_big_count", "gs_big_bscan",
              "gs_big_scatter", "gs_big_bsort"],
     "blend": ["gs_blend"],
+    # lazy big lists (config 5): the full sort of the flagged lists + the
+    # continued blend; its PMC counters are the continued blend's
+    "blend_cont": ["gs_blend_cont"],
 }
 
 
@@ -111,33 +114,43 @@ def measured_copy_peak(torch) -> float:
     return round(2 * n / best / 1e9, 1)
 
 
-def alg_bytes(kernel: str, T: int, P: int, n: int, px: int) -> float:
+def alg_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int) -> float:
     """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md §4).
-    P = the pairs actually binned, sorted and blended (the reference rectangle's
-    pairs minus those the alpha box culls); T = tiles; px = pixels written."""
+    P = the pairs actually binned and sorted (the reference rectangle's pairs
+    minus those the alpha box culls); T = tiles; px = pixels written; rec =
+    the tile-list records the blend staged (gs_frame_stats.blend_records: a
+    wave stops when its pixels have saturated, and lazy big lists stage only
+    their sorted prefixes), rec_cont = the records the continuation staged."""
     return {
         "project": n * (56 + 52),
         "scan": n * 16 + T * 12,  # count reads each Gaussian's two rectangles; tile starts
         "emit": n * 12 + P * 12,
         "sort": P * 24,
-        "blend": T * 8 + P * (4 + 36) + px * (16 + 3),
+        "blend": T * 8 + rec * (4 + 36) + px * (16 + 3),
+        # the continued records only (the flagged lists' full sort is not counted)
+        "blend_cont": rec_cont * (4 + 36),
     }[kernel]
+
+
+def core_map():
+    """CPU id -> (core, socket) from lscpu (empty if lscpu is unavailable)."""
+    core_of = {}
+    try:
+        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line and not line.startswith("#"):
+                c, core, sock = line.split(",")[:3]
+                core_of[int(c)] = (core, sock)
+    except Exception:
+        pass
+    return core_of
 
 
 def host_cpus():
     """(usable CPUs, physical cores among them) from the affinity mask and lscpu."""
     cpus = sorted(os.sched_getaffinity(0))
-    phys = None
-    try:
-        out = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
-        core_of = {}
-        for line in out.splitlines():
-            if line and not line.startswith("#"):
-                c, core, sock = line.split(",")[:3]
-                core_of[int(c)] = (core, sock)
-        phys = len({core_of[c] for c in cpus if c in core_of}) or None
-    except Exception:
-        phys = None
+    core_of = core_map()
+    phys = len({core_of[c] for c in cpus if c in core_of}) or None
     return len(cpus), phys
 
 
@@ -166,6 +179,7 @@ def main():
     group = world > 1 or a.gather or a.split > 1
 
     from gaussian_splat_ipu_amd import camera, scene
+    from gaussian_splat_ipu_amd._lib import GsError
     from gaussian_splat_ipu_amd.splatter import GpuSplatter, comm_id_create
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
 
@@ -231,10 +245,28 @@ def main():
             r.set_view_wire(v)
             r.execute()
         r.set_view_wire(views[0])
+    def sync_all():
+        """Every renderer's gs_sync, then the status agreed over ranks BEFORE any
+        barrier: a rank that raised alone would leave the others waiting in
+        the barrier (the group decides overflow from the gathered footers, the
+        same on every rank; this is the belt to those braces)."""
+        err = None
+        for r in R:
+            try:
+                r.sync()
+            except GsError as e:
+                err = err or e
+        if world > 1:
+            t = torch.tensor([0 if err is None else 1], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if t.item() and err is None:
+                err = RuntimeError("another rank's frames overflowed their pair capacity")
+        if err is not None:
+            raise err
+
     for _ in range(a.warmup):
         one_frame()
-    for r in R:
-        r.sync()
+    sync_all()
     nframe[0] = 0
     torch.cuda.synchronize()
     if world > 1:
@@ -244,8 +276,7 @@ def main():
     for _ in range(a.steps):
         one_frame()
     t_enq = time.perf_counter()  # host time to enqueue the K frames
-    for r in R:
-        r.sync()  # raises on pair overflow
+    sync_all()  # raises (on every rank) on pair overflow
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -297,6 +328,7 @@ def main():
         px = (min(H, b1 * TW) - b0 * TW) * W
     else:
         T_b, P_b, px = st_view["n_tiles"], st_view["n_pairs_binned"], st_view["band_rows"] * W
+    rec, rec_cont = st_view["blend_records"], st_view["blend_cont_records"]
     kern = {}
     for name, (avg_ms, cnt) in kt.items():
         if name == "gather":
@@ -305,13 +337,22 @@ def main():
                               "note": "ncclAllGather on the comm stream, local band done -> frame gathered "
                                       "(includes waiting for the slowest rank)"}
             continue
-        b = alg_bytes(name, T_b, P_b, a.n, px)
+        if name == "blend_cont" and not cnt:
+            continue
+        b = alg_bytes(name, T_b, P_b, a.n, px, rec, rec_cont)
         kern[name] = {
             "avg_ms": round(avg_ms, 5),
             "launches": int(cnt),
             "alg_bytes": int(b),
             "alg_GBps": round(b / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None,
         }
+    if "blend" in kern:
+        kern["blend"]["records_staged"] = int(rec)
+        kern["blend"]["pairs_binned"] = int(P_b)
+    if "blend_cont" in kern:
+        kern["blend_cont"]["records_staged"] = int(rec_cont)
+        kern["blend_cont"]["note"] = ("full sample sort of the big lists the blend flagged + the continued blend; "
+                                      "alg_bytes counts the continued records only")
     stage = {k: v for k, v in kern.items() if k != "gather"}
     dom = max(stage, key=lambda k: stage[k]["avg_ms"])
     # PMC counters are per launch (kernel properties): the key names the
@@ -444,6 +485,12 @@ def cpu_baseline(a, g, view, proj, W, H, TW, np):
     # the cores the OpenMP team actually gets, so it does not cap the count
     threads = int(omp_env) if omp_env and omp_env.isdigit() else (phys or n_cpus)
     threads = max(1, threads)
+    # where the OpenMP team really runs: each thread reads its CPU inside a
+    # parallel region (the affinity mask of this thread says nothing about it)
+    team = O.omp_team_cpus(threads, spin_ms=100.0)
+    core_of = core_map()
+    team_cpus = len(set(team))
+    team_cores = len({core_of[c] for c in team if c in core_of}) or None
     f = O.make_frame(view, proj, W, H, TW, TW, camera.FOV_DEFAULT, a.scale_div)
 
     def timed(fn, frames, warm):
@@ -465,11 +512,16 @@ def cpu_baseline(a, g, view, proj, W, H, TW, np):
                     a.cpu_warmup)
     host = (f"{os.cpu_count()} CPUs on the host, {n_cpus} in this thread's affinity mask, {phys} physical "
             f"cores among those (lscpu); "
-            f"OMP_NUM_THREADS={omp_env} (the GPU box's CPU share), OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}")
+            f"OMP_NUM_THREADS={omp_env} (the GPU box's CPU share), OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}; "
+            f"the {threads}-thread OpenMP team ran on {team_cpus} distinct CPUs = {team_cores} physical cores "
+            f"(sched_getcpu inside a parallel region)")
     return {
         "value": round(1.0 / tc, 4),
         "unit": "frames/s",
-        "cores": threads,
+        "cores": team_cores or team_cpus,
+        "threads": threads,
+        "team_cpus": team_cpus,
+        "team_physical_cores": team_cores,
         "kind": "port",
         "sample": f"median of {nf} full frames (after {a.cpu_warmup} warm-up) of the same {a.n}-Gaussian {W}x{H} "
                   f"workload through the CPU oracle Gaussian rasteriser (OpenMP, {threads} threads)",

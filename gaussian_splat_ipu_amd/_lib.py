@@ -28,8 +28,8 @@ GS_FLAG_LATTICE = 512
 GS_MAX_GPUS = 16
 GS_LAYOUT_ROW_MAJOR = 0
 GS_LAYOUT_REF_TILE_MAJOR = 1
-GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_GATHER, GS_K_COUNT = range(7)
-KERNEL_NAMES = ("project", "scan", "emit", "sort", "blend", "gather")
+GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_GATHER, GS_K_BLEND_CONT, GS_K_COUNT = range(8)
+KERNEL_NAMES = ("project", "scan", "emit", "sort", "blend", "gather", "blend_cont")
 
 _STATUS_NAMES = {
     GS_EINVAL: "GS_EINVAL",
@@ -112,6 +112,8 @@ class FrameStats(C.Structure):
         ("n_pairs_binned", C.c_uint64),
         ("bin_global", C.c_uint32),
         ("reserved0", C.c_uint32),
+        ("blend_records", C.c_uint64),
+        ("blend_cont_records", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -166,6 +168,9 @@ _SIGS = {
                                  C.c_int, C.c_int, C.POINTER(_P)]),
     "gs_group_bands": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_size_t]),
     "gs_balanced_bands": (C.c_int, [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "gs_group_decide": (C.c_int, [C.POINTER(C.c_uint32), C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_uint32),
+                                  C.POINTER(C.c_uint64)]),
     "gs_get_lattice_stats": (C.c_int, [_P, C.POINTER(LatticeStats)]),
     "gs_read_lattice_slots": (C.c_int, [_P, _FP, C.c_size_t]),
     "gs_set_view": (C.c_int, [_P, _FP]),

@@ -15,16 +15,23 @@
 // by a footer: the band's frame counters and reference tile-list lengths.
 // After the gather every rank holds every band's footer, so every rank derives
 // the same next split from the same numbers (no extra collective) and reports
-// the whole frame's histogram.  Overflow is decided from the footers too, so a
-// blocking gs_render re-renders on every rank or on none.
+// the whole frame's histogram.  Overflow is decided from the footers too (the
+// frame's own bit, and a per-GPU sticky bit copied into the footer before the
+// gather that covers every frame since the last gs_sync), so gs_sync returns
+// the same status on every rank and a blocking gs_render re-renders on every
+// rank or on none (decide(), exported as gs_group_decide).
+//
+// Contract (gsplat.h): gs_render, gs_render_async and gs_sync are collective
+// -- every rank calls them for the same frames, in the same order.  The
+// readbacks are local: they wait for this rank's frames but change neither the
+// split nor the overflow state.
 //
 // Frames in flight: F band renderers per device take frames round-robin, each
 // on its own stream; the all-gathers run in frame order on one communication
 // stream per device.  gs_render_async never waits: the split is re-balanced
 // every kRebalanceEvery frames from the footers of the frame half that many
 // frames back (copied to the host when it was enqueued), the same frame on
-// every rank; gs_sync (and so a blocking gs_render) re-balances from the last
-// frame.
+// every rank; a blocking gs_render re-balances from its own frame.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -123,6 +130,9 @@ struct Member {
   uint8_t* d_recv = nullptr;          // F x world x slot_cap: the gathered frames
   std::vector<hipEvent_t> ev_render;    // per slot: the band is rendered
   std::vector<hipEvent_t> ev_gathered;  // per slot: the all-gather read the send slot
+  // set by the scan of any of this GPU's band frames that overflowed since
+  // the last sync; copied into footer word kFootSticky before every gather
+  uint32_t* d_sticky = nullptr;
 };
 
 struct SlotInfo {
@@ -158,6 +168,9 @@ struct Group {
   uint64_t frame = 0;
   int last_slot = -1;
   bool last_read = false;
+  int last_status = GS_OK;   // the decision of the last frame's footers (repeated syncs return it)
+  uint64_t need_pairs = 0;   // the largest band list of the last frame's footers
+  uint64_t pair_cap = 0;     // the group's pair capacity per band renderer (the same on every rank)
   float view[16], proj[16];
   float fov = 0.6981317f, sd = 0.1f;
   // the last frame whose footers were read
@@ -213,52 +226,98 @@ int nccl_fail(ncclResult_t r, const char* what) {
     if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
   } while (0)
 
-// The footers of one gathered frame (world x foot_words at h, the frame's
-// split `bounds`): the whole frame's histogram and, with `stats`, its stats
-// (kept for gs_get_stats / gs_read_tile_histogram); with `split`, the next
-// split.  Returns whether a band overflowed.
-bool parse_footers(Group* g, const uint32_t* h, const std::vector<uint32_t>& bounds, bool stats, bool split) {
-  const bool chunked = !g->mem[0].slot[0]->bin_global && g->mem[0].slot[0]->n_chunks > 0;
+}  // namespace
+
+// Every decision the group takes is a function of ONE gathered frame's
+// footers (world x foot_words at h; `frame_bounds` = that frame's split), the
+// same bytes on every rank, so every rank takes the same decision without a
+// collective of its own:
+//   * the status: GS_EOVERFLOW iff some band's frame overflowed (word 3) or
+//     some band's GPU had an overflowing frame since its last sync (word
+//     kFootSticky, the group's sticky bit copied in before the gather);
+//   * need_pairs: the longest band pair list of the frame (capacity growth);
+//   * next_bounds: the split of later frames (cur_bounds unless re-balancing
+//     lowers the slowest band's work by more than 3 %; never after overflow);
+//   * with `hist` / `st`: the whole frame's histogram and stats.
+// The blocking contract it serves: IpuSplatter::execute, ipu_rasteriser.cpp:408-420.
+int decide(const uint32_t* h, size_t foot_words, int world, int tiles_x, int tiles_y,
+           const uint32_t* frame_bounds, const uint32_t* cur_bounds, bool rebalance, bool chunked,
+           uint32_t* next_bounds, uint64_t* need_pairs, std::vector<uint32_t>* hist_out, gs_frame_stats* st) {
+  const size_t T = (size_t)tiles_x * tiles_y;
   bool ovf = false;
-  uint64_t P = 0, Pb = 0, V = 0, nbig = 0;
-  std::vector<uint32_t> hist((size_t)g->T, 0u);
-  for (int r = 0; r < g->world; ++r) {
-    const uint32_t* f = h + (size_t)r * g->foot_words;
-    ovf = ovf || f[3] != 0;
+  uint64_t P = 0, Pb = 0, V = 0, nbig = 0, need = 0;
+  std::vector<uint32_t> hist(T, 0u);
+  for (int r = 0; r < world; ++r) {
+    const uint32_t* f = h + (size_t)r * foot_words;
+    ovf = ovf || f[3] != 0 || f[gsk::kFootSticky] != 0;
     const uint64_t pb = (uint64_t)f[5] | ((uint64_t)f[6] << 32);
     Pb += pb;
+    need = std::max(need, pb);
     P += chunked ? ((uint64_t)f[10] | ((uint64_t)f[11] << 32)) : pb;
     V = std::max<uint64_t>(V, f[2]);
     nbig += f[0];
-    const size_t t0 = (size_t)bounds[r] * g->tiles_x, t1 = (size_t)bounds[r + 1] * g->tiles_x;
-    std::memcpy(hist.data() + t0, f + 16, (t1 - t0) * 4);
+    const size_t t0 = (size_t)frame_bounds[r] * tiles_x, t1 = (size_t)frame_bounds[r + 1] * tiles_x;
+    if (t1 > t0 && t1 <= T && 16 + (t1 - t0) <= foot_words) std::memcpy(hist.data() + t0, f + 16, (t1 - t0) * 4);
   }
-  if (split && g->rebalance && g->world > 1 && !ovf) {
-    std::vector<double> w((size_t)g->tiles_y, 0.0);
-    for (int y = 0; y < g->tiles_y; ++y) {
-      double sum = 0.0;
-      for (int x = 0; x < g->tiles_x; ++x) sum += hist[(size_t)y * g->tiles_x + x];
-      w[y] = sum + kTileCost * g->tiles_x;
-    }
-    std::vector<uint32_t> nb((size_t)g->world + 1);
-    balanced_bands(w.data(), g->tiles_y, g->world, nb.data());
-    if (nb != g->bounds && max_band_work(w, nb) < kRebalanceGain * max_band_work(w, g->bounds)) {
-      g->bounds = nb;
-      g->rebalances += 1;
+  if (need_pairs) *need_pairs = need;
+  if (next_bounds) {
+    std::copy(cur_bounds, cur_bounds + world + 1, next_bounds);
+    if (rebalance && world > 1 && !ovf) {
+      std::vector<double> w((size_t)tiles_y, 0.0);
+      for (int y = 0; y < tiles_y; ++y) {
+        double sum = 0.0;
+        for (int x = 0; x < tiles_x; ++x) sum += hist[(size_t)y * tiles_x + x];
+        w[y] = sum + kTileCost * tiles_x;
+      }
+      std::vector<uint32_t> nb((size_t)world + 1), cb(cur_bounds, cur_bounds + world + 1);
+      balanced_bands(w.data(), tiles_y, world, nb.data());
+      if (nb != cb && max_band_work(w, nb) < kRebalanceGain * max_band_work(w, cb))
+        std::copy(nb.begin(), nb.end(), next_bounds);
     }
   }
-  if (stats) {
+  if (st) {
     uint32_t mx = 0;
     for (uint32_t v : hist) mx = std::max(mx, v);
+    st->n_rendered = V;
+    st->n_pairs = P;
+    st->n_pairs_binned = Pb;
+    st->max_list = mx;
+    st->n_big_tiles = (uint32_t)nbig;
+  }
+  if (hist_out) hist_out->swap(hist);
+  return ovf ? GS_EOVERFLOW : GS_OK;
+}
+
+namespace {
+
+// The footers of one gathered frame: its status, and with `stats` the whole
+// frame's histogram and stats (gs_get_stats / gs_read_tile_histogram); with
+// `split`, the split of later frames.  Only called where every rank calls it
+// for the same frame: at the frame indices of the re-balancing snapshot
+// (enqueue), in a blocking gs_render, and in gs_sync (status and stats only).
+int parse_footers(Group* g, const uint32_t* h, const std::vector<uint32_t>& bounds, bool stats, bool split) {
+  const bool chunked = !g->mem[0].slot[0]->bin_global && g->mem[0].slot[0]->n_chunks > 0;
+  std::vector<uint32_t> nb((size_t)g->world + 1), hist;
+  gs_frame_stats st{};
+  uint64_t need = 0;
+  const int rc = decide(h, g->foot_words, g->world, g->tiles_x, g->tiles_y, bounds.data(), g->bounds.data(),
+                        split && g->rebalance, chunked, nb.data(), &need, stats ? &hist : nullptr,
+                        stats ? &st : nullptr);
+  if (split && nb != g->bounds) {
+    g->bounds = nb;
+    g->rebalances += 1;
+  }
+  if (stats) {
+    g->need_pairs = need;
     std::lock_guard<std::mutex> lk(g->hist_mu);
     g->hist.swap(hist);
-    g->stats.n_rendered = V;
-    g->stats.n_pairs = P;
-    g->stats.n_pairs_binned = Pb;
-    g->stats.max_list = mx;
-    g->stats.n_big_tiles = (uint32_t)nbig;
+    g->stats.n_rendered = st.n_rendered;
+    g->stats.n_pairs = st.n_pairs;
+    g->stats.n_pairs_binned = st.n_pairs_binned;
+    g->stats.max_list = st.max_list;
+    g->stats.n_big_tiles = st.n_big_tiles;
   }
-  return ovf;
+  return rc;
 }
 
 // every band's footer of the frame in slot i -> h (one strided copy on s)
@@ -318,6 +377,10 @@ int enqueue(Group* g) {
     if ((rc = set_dev(m.device)) != GS_OK) return rc;
     if (g->rccl) {
       GS_HIP(hipStreamWaitEvent(m.comm_stream, m.ev_render[i], 0));
+      // the GPU's sticky overflow bit into the footer: every frame up to this
+      // one has finished its render here (the gathers run in frame order)
+      gsk::launch_copy_word(m.comm_stream, (uint32_t*)(m.d_send + (size_t)i * g->slot_cap + bgr_part) +
+                                               gsk::kFootSticky, m.d_sticky);
     } else {  // copies read every member's band
       for (Member& o : g->mem) GS_HIP(hipStreamWaitEvent(m.comm_stream, o.ev_render[i], 0));
     }
@@ -340,9 +403,14 @@ int enqueue(Group* g) {
     for (Member& m : g->mem) {
       if ((rc = set_dev(m.device)) != GS_OK) return rc;
       uint8_t* recv = m.d_recv + (size_t)i * g->world * g->slot_cap;
-      for (const Member& o : g->mem)
+      for (const Member& o : g->mem) {
         GS_HIP(hipMemcpyAsync(recv + (size_t)o.rank * bytes, o.d_send + (size_t)i * g->slot_cap, bytes,
                               hipMemcpyDeviceToDevice, m.comm_stream));
+        // o's sticky bit into its gathered footer (this stream has waited for
+        // every frame of o up to this one)
+        GS_HIP(hipMemcpyAsync((uint32_t*)(recv + (size_t)o.rank * bytes + bgr_part) + gsk::kFootSticky, o.d_sticky,
+                              4, hipMemcpyDeviceToDevice, m.comm_stream));
+      }
     }
   }
   for (Member& m : g->mem) {
@@ -373,21 +441,23 @@ int enqueue(Group* g) {
 }
 
 int ensure_capacity(Group* g) {
-  // after an overflow: every local band renderer gets room for the largest
-  // band list any of them binned (the next frames may move the bands)
-  uint64_t need = 0;
-  for (Member& m : g->mem)
-    for (gs_renderer* c : m.slot) need = std::max(need, c->stats.n_pairs_binned);
-  need = std::min<uint64_t>(need + need / 4 + 1024, 0xFFFFFFF0ull);
+  // after an overflow: every band renderer of every rank gets the same new
+  // capacity, from the gathered footers (the longest band list of the last
+  // frame; the next frames may move the bands) and at least twice the old
+  // one (the overflow may have come from an earlier in-flight frame)
+  const uint64_t need = g->need_pairs + g->need_pairs / 4 + 1024;
+  if (g->need_pairs > 0xFFFFFFF0ull || g->pair_cap >= 0xFFFFFFF0ull) {
+    set_error("gs_render: a band's pair count exceeds 2^32");
+    return GS_EOVERFLOW;
+  }
+  g->pair_cap = std::min<uint64_t>(std::max<uint64_t>(need, 2 * g->pair_cap), 0xFFFFFFF0ull);
   for (Member& m : g->mem) {
     int rc = set_dev(m.device);
     if (rc != GS_OK) return rc;
     for (gs_renderer* c : m.slot) {
-      if (c->pair_cap >= need) continue;
+      if (c->pair_cap >= g->pair_cap) continue;
       GS_HIP(hipStreamSynchronize(c->stream));
-      if ((rc = gsr::alloc_pairs(c, std::min<uint64_t>(std::max<uint64_t>(need, 2 * c->pair_cap), 0xFFFFFFF0ull))) !=
-          GS_OK)
-        return rc;
+      if ((rc = gsr::alloc_pairs(c, g->pair_cap)) != GS_OK) return rc;
     }
   }
   return GS_OK;
@@ -402,6 +472,7 @@ void release(Group* g) {
     if (m.comm) (void)rccl().CommDestroy(m.comm);
     if (m.d_send) (void)hipFree(m.d_send);
     if (m.d_recv) (void)hipFree(m.d_recv);
+    if (m.d_sticky) (void)hipFree(m.d_sticky);
     for (hipEvent_t e : m.ev_render)
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : m.ev_gathered)
@@ -536,6 +607,9 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
       return fail(gsr::hip_fail(e, "hipMalloc(all-gather recv)"));
     if ((e = hipMemset(m.d_recv, 0, (size_t)g->F * g->world * g->slot_cap)) != hipSuccess)
       return fail(gsr::hip_fail(e, "hipMemset(all-gather recv)"));
+    if ((e = hipMalloc(&m.d_sticky, 256)) != hipSuccess) return fail(gsr::hip_fail(e, "hipMalloc(sticky)"));
+    if ((e = hipMemset(m.d_sticky, 0, 256)) != hipSuccess) return fail(gsr::hip_fail(e, "hipMemset(sticky)"));
+    for (gs_renderer* c : m.slot) c->buf.group_sticky = m.d_sticky;
     m.ev_render.assign((size_t)g->F, nullptr);
     m.ev_gathered.assign((size_t)g->F, nullptr);
     for (int s = 0; s < g->F; ++s) {
@@ -583,6 +657,7 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
 
   {
     gs_renderer* c0 = g->mem[0].slot[0];
+    g->pair_cap = c0->pair_cap;  // the same on every rank (same configuration and scene size)
     g->stats.n_gaussians = n;
     g->stats.n_tiles = (uint32_t)g->T;
     g->stats.tiles_x = (uint32_t)g->tiles_x;
@@ -626,28 +701,27 @@ int set_focal(Group* g, float fov, float sd) {
 
 int render_async(Group* g) { return enqueue(g); }
 
-// Waits for every frame, then reads the last frame's footers (its stats and
-// histogram).  Overflow: the last frame's footers (the same on every rank) or
-// an earlier frame of this process's bands since the last sync.
-int sync(Group* g) {
+// Waits for every frame of this rank, then reads the last frame's footers
+// (its stats and histogram) once.  The status is decided from those gathered
+// bytes only -- the same on every rank -- never from a rank-local flag: a
+// band's overflow in an earlier in-flight frame reaches the last frame's
+// footer through its GPU's sticky word.  Readbacks call this too; it changes
+// neither the split nor the sticky words, so a readback on some ranks only
+// cannot make the ranks diverge.
+int wait_frames(Group* g) {
   int rc = GS_OK;
-  bool local_ovf = false;
   for (Member& m : g->mem) {
     if ((rc = set_dev(m.device)) != GS_OK) return rc;
     GS_HIP(hipStreamSynchronize(m.comm_stream));
     for (gs_renderer* c : m.slot) {
-      rc = gsr::finish_frame(c);
-      if (rc == GS_EOVERFLOW) local_ovf = true;
-      else if (rc != GS_OK) return rc;
+      rc = gsr::finish_frame(c);  // (a local overflow is in the footers already)
+      if (rc != GS_OK && rc != GS_EOVERFLOW) return rc;
     }
   }
-  bool ovf = false;
   if (g->last_slot >= 0 && !g->last_read) {
     if ((rc = set_dev(g->mem[0].device)) != GS_OK) return rc;
     if ((rc = copy_footers(g, g->last_slot, g->h_last, nullptr, false)) != GS_OK) return rc;
-    // (a blocking frame also re-balances the split from itself: every rank
-    // calls gs_sync after the same frames)
-    ovf = parse_footers(g, g->h_last, g->sinfo[g->last_slot].bounds, true, true);
+    g->last_status = parse_footers(g, g->h_last, g->sinfo[g->last_slot].bounds, true, false);
     g->last_read = true;
     SlotInfo& si = g->sinfo[g->last_slot];
     if (si.gather_timed) {
@@ -658,20 +732,44 @@ int sync(Group* g) {
       si.gather_timed = false;
     }
   }
-  if (ovf || local_ovf) {
-    set_error("pair list overflow: a band of a frame since the last sync binned more pairs than its capacity");
+  if (g->last_status == GS_EOVERFLOW) {
+    set_error("pair list overflow: a band of a frame since the last gs_sync binned more pairs than its capacity");
     return GS_EOVERFLOW;
   }
   return GS_OK;
 }
 
+// gs_sync: collective (every rank calls it after the same frames).  The
+// status of the frames since the last gs_sync, then the sticky words start
+// over (on every rank at the same frame).
+int sync(Group* g) {
+  const int st = wait_frames(g);
+  if (st != GS_OK && st != GS_EOVERFLOW) return st;
+  for (Member& m : g->mem) {
+    int rc = set_dev(m.device);
+    if (rc != GS_OK) return rc;
+    GS_HIP(hipMemsetAsync(m.d_sticky, 0, 4, m.comm_stream));
+    GS_HIP(hipStreamSynchronize(m.comm_stream));
+  }
+  if (st == GS_EOVERFLOW)
+    set_error("pair list overflow: a band of a frame since the last gs_sync binned more pairs than its capacity");
+  return st;
+}
+
+// gs_render: collective.  Every rank decides from the same footers whether
+// to grow and render again, and re-balances the split from its frame.
 int render(Group* g) {
   for (int attempt = 0; attempt < 8; ++attempt) {
     int rc = enqueue(g);
     if (rc != GS_OK) return rc;
     rc = sync(g);
+    if (rc == GS_OK) {
+      if (g->rebalance && g->world > 1)
+        parse_footers(g, g->h_last, g->sinfo[g->last_slot].bounds, false, true);
+      return GS_OK;
+    }
     if (rc != GS_EOVERFLOW) return rc;
-    // every rank saw the same footers: all of them render the frame again
+    // every rank saw the same footers: all of them grow and render the frame again
     if ((rc = ensure_capacity(g)) != GS_OK) return rc;
   }
   set_error("gs_render: capacity growth did not converge");
@@ -689,7 +787,7 @@ int read_bgr8(Group* g, uint8_t* dst, size_t bytes) {
     set_error("gs_read_bgr8: destination too small");
     return GS_EINVAL;
   }
-  int rc = sync(g);
+  int rc = wait_frames(g);
   if (rc != GS_OK) return rc;
   if (g->last_slot < 0) {
     set_error("gs_read_bgr8: no frame rendered yet");
@@ -721,7 +819,7 @@ int read_rgba32f(Group* g, float* dst, size_t n_floats, int layout) {
     set_error("gs_read_rgba32f: destination too small");
     return GS_EINVAL;
   }
-  int rc = sync(g);
+  int rc = wait_frames(g);
   if (rc != GS_OK) return rc;
   if (g->last_slot < 0) {
     set_error("gs_read_rgba32f: no frame rendered yet");
@@ -756,6 +854,9 @@ int read_tile_histogram(Group* g, uint32_t* dst, size_t n) {
 int get_stats(Group* g, gs_frame_stats* st) {
   std::lock_guard<std::mutex> lk(g->hist_mu);
   *st = g->stats;
+  // the profiled band renderer's own counts (this rank's band)
+  st->blend_records = g->mem[0].slot[0]->stats.blend_records;
+  st->blend_cont_records = g->mem[0].slot[0]->stats.blend_cont_records;
   uint64_t cap = ~0ull;
   for (Member& m : g->mem)
     for (gs_renderer* c : m.slot) cap = std::min<uint64_t>(cap, c->pair_cap);
@@ -768,7 +869,7 @@ int read_bins(Group* g, uint64_t* tile_start, size_t n_start, uint32_t* list, si
     set_error("gs_read_bins: a rank of a multi-process group holds only its band's lists");
     return GS_EINVAL;
   }
-  int rc = sync(g);
+  int rc = wait_frames(g);
   if (rc != GS_OK) return rc;
   if (g->last_slot < 0) {
     set_error("gs_read_bins: no frame rendered yet");
@@ -798,7 +899,7 @@ int read_bins(Group* g, uint64_t* tile_start, size_t n_start, uint32_t* list, si
 }
 
 int read_projected(Group* g, float* dst, size_t n_floats) {
-  int rc = sync(g);
+  int rc = wait_frames(g);
   if (rc != GS_OK) return rc;
   if (g->last_slot < 0) {
     set_error("gs_read_projected: no frame rendered yet");
@@ -831,7 +932,7 @@ int kernel_times(Group* g, double* avg_ms, uint64_t* launches, int n) {
 }
 
 int reset_kernel_times(Group* g) {
-  int rc = sync(g);
+  int rc = wait_frames(g);
   if (rc != GS_OK && rc != GS_EOVERFLOW) return rc;
   gs_renderer* c = g->mem[0].slot[0];
   if (c->profile) {
@@ -869,6 +970,27 @@ int bands(Group* g, uint32_t* bounds, size_t n) {
 }
 
 }  // namespace gsg
+
+extern "C" int gs_group_decide(const uint32_t* footers, size_t foot_words, uint32_t world, uint32_t tiles_x,
+                               uint32_t tiles_y, const uint32_t* frame_bounds, const uint32_t* cur_bounds,
+                               int rebalance, uint32_t* next_bounds, uint64_t* need_pairs) {
+  if (!footers || !frame_bounds || !cur_bounds || world == 0 || tiles_y < world || foot_words < 16) {
+    set_error("gs_group_decide: invalid arguments");
+    return GS_EINVAL;
+  }
+  for (uint32_t r = 0; r < world; ++r)
+    if (frame_bounds[r] >= frame_bounds[r + 1] || cur_bounds[r] >= cur_bounds[r + 1] ||
+        16 + (size_t)(frame_bounds[r + 1] - frame_bounds[r]) * tiles_x > foot_words) {
+      set_error("gs_group_decide: bounds are not a split of the tile rows that fits the footers");
+      return GS_EINVAL;
+    }
+  if (frame_bounds[0] != 0 || cur_bounds[0] != 0 || frame_bounds[world] != tiles_y || cur_bounds[world] != tiles_y) {
+    set_error("gs_group_decide: bounds must cover tile rows [0, tiles_y)");
+    return GS_EINVAL;
+  }
+  return gsg::decide(footers, foot_words, (int)world, (int)tiles_x, (int)tiles_y, frame_bounds, cur_bounds,
+                     rebalance != 0, true, next_bounds, need_pairs, nullptr, nullptr);
+}
 
 extern "C" int gs_comm_id_create(gs_comm_id* out) {
   if (!out) return GS_EINVAL;

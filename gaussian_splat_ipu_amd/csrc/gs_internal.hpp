@@ -21,7 +21,9 @@ struct Group;
 namespace gsr {
 
 constexpr int kProfileRing = 64;
-constexpr int kStages = gsk::GS_STAGE_EVENTS - 1;  // project .. blend (GS_K_PROJECT .. GS_K_BLEND)
+constexpr int kStages = gsk::GS_STAGE_EVENTS - 1;  // project .. blend, blend continuation
+// the kernel id (GS_K_*) of profile stage k
+constexpr int kStageKernel[kStages] = {GS_K_PROJECT, GS_K_SCAN, GS_K_EMIT, GS_K_SORT, GS_K_BLEND, GS_K_BLEND_CONT};
 
 struct ProfileSlot {
   hipEvent_t ev[gsk::GS_STAGE_EVENTS];
@@ -99,6 +101,9 @@ struct gs_renderer {
   // profiling
   bool profile = false;
   uint32_t profile_every = 1;  // stage events on every n-th frame
+  void* d_bcount = nullptr;    // blend_count (profile renderers)
+  size_t bcount_words = 0;
+  bool last_counted = false;   // the last enqueued frame counted its blend records
   uint64_t frame_seq = 0;
   gsr::ProfileSlot ring[gsr::kProfileRing];
   int ring_head = 0;

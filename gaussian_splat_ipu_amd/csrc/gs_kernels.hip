@@ -523,7 +523,10 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
     const unsigned long long total = carry;
     b.tile_start[T] = (uint32_t)(total < 0xFFFFFFFFull ? total : 0xFFFFFFFFull);
     b.counters[3] = total > fp.pair_cap ? 1u : 0u;
-    if (total > fp.pair_cap) *b.host_sticky = 1u;  // sticky until the host's sync
+    if (total > fp.pair_cap) {  // sticky until the host's sync
+      *b.host_sticky = 1u;
+      if (b.group_sticky) *b.group_sticky = 1u;
+    }
     b.counters[4] = m;
     b.counters[5] = (uint32_t)total;
     b.counters[6] = (uint32_t)(total >> 32);
@@ -808,7 +811,10 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
       b.counters[1] = 0;
       b.counters[2] = s_mx[0] + s_mx[1] + s_mx[2] + s_mx[3];
       b.counters[3] = ts > fp.pair_cap ? 1u : 0u;
-      if (ts > fp.pair_cap) *b.host_sticky = 1u;  // sticky until the host's sync
+      if (ts > fp.pair_cap) {  // sticky until the host's sync
+        *b.host_sticky = 1u;
+        if (b.group_sticky) *b.group_sticky = 1u;
+      }
       b.counters[4] = mx;
       b.counters[5] = (uint32_t)ts;
       b.counters[6] = (uint32_t)(ts >> 32);
@@ -2016,8 +2022,16 @@ __device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t 
 // quads have.  The per-pixel arithmetic and record order are those of
 // renderTile (codelets.cpp:385-411): a record is skipped for a quad only when
 // no pixel of the quad can take it ("blend culling").
+// profiled frames (FrameParams::count_records): the records a blend wave
+// staged, for the bench's algorithmic bytes (lane 0 of the wave)
+__device__ __forceinline__ void blend_count_store(const FrameParams& fp, const Buffers& b, int wid,
+                                                  uint32_t staged) {
+  if (fp.count_records && (threadIdx.x & 63) == 0)
+    (fp.blend_cont ? b.blend_count_cont : b.blend_count)[wid] = staged;
+}
+
 template <int BQW>
-__global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
+__device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers& b) {
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wid = blockIdx.x * GS_BLEND_WPG + wave;
   const int slot = wid / fp.chunks_per_tile;
@@ -2027,7 +2041,10 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   // are (slot, chunk) of the flagged lists whose state was saved.
   uint32_t jb = 0xFFFFFFFFu;
   if (fp.blend_cont) {
-    if ((uint32_t)slot >= b.counters[0] || b.cont_flag[4 * slot + chunk] == 0u) return;
+    if ((uint32_t)slot >= b.counters[0] || b.cont_flag[4 * slot + chunk] == 0u) {
+      blend_count_store(fp, b, wid, 0u);
+      return;
+    }
     jb = (uint32_t)slot;
   }
   // row bands: longest lists first (the sort queues: big, medium, then small
@@ -2127,8 +2144,10 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   }
   uint32_t g_next = load_idx(64 + lane);
 
+  uint32_t staged = 0;  // records staged (profiled frames)
   for (uint32_t base = 0; base < L; base += 64) {
     if (ballot64(!q.done) == 0ull) break;
+    staged += min(64u, L - base);
     // stage this batch
     const bool have = g_cur != 0xFFFFFFFFu;
     st[0][lane] = a0;
@@ -2240,13 +2259,35 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
       b.cont_flag[4 * jb + chunk] = 1u;
       b.big_flag[jb] = 1u;
     }
+    blend_count_store(fp, b, wid, staged);
     return;  // the continuation stores these pixels
   }
+  blend_count_store(fp, b, wid, staged);
   if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
 
+template <int BQW>
+__global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
+  blend_body<BQW>(fp, b);
+}
+
+// the lazy big lists' continuation (its own symbol, so profiles tell it from
+// the prefix blend)
+__global__ __launch_bounds__(256) void gs_blend_cont_kernel(FrameParams fp, Buffers b) {
+  blend_body<4>(fp, b);
+}
+
+
+__global__ __launch_bounds__(64) void gs_copy_word_kernel(uint32_t* dst, const uint32_t* src) {
+  // a device-scope load: the word was written by other kernels on other streams
+  if (threadIdx.x == 0) *dst = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 }  // namespace
+
+void launch_copy_word(hipStream_t s, uint32_t* dst, const uint32_t* src) {
+  gs_copy_word_kernel<<<1, 64, 0, s>>>(dst, src);
+}
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
@@ -2307,7 +2348,7 @@ void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     // list's last one skip it)
     gs_big_prefix_kernel<<<1, 1024, 0, s>>>(fp, b);
     gs_big_split_kernel<<<1024, 256, 0, s>>>(fp, b);
-    if (fp.lazy) {  // only the prefixes now; the rest after the blend (launch_blend)
+    if (fp.lazy) {  // only the prefixes now; the rest after the blend (launch_blend_cont)
       gs_big_select_kernel<<<4096, 256, 0, s>>>(fp, b);
       gs_big_psort_kernel<<<2048, 256, 0, s>>>(fp, b);
     } else {
@@ -2329,17 +2370,22 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     gs_blend_kernel<8><<<grid, block, 0, s>>>(fp, b);
   else
     gs_blend_kernel<0><<<grid, block, 0, s>>>(fp, b);
-  if (fp.lazy) {
-    // the big lists whose blend outlived the prefix: sorted in full, then
-    // their saved waves continue (nothing to do when none was flagged)
-    FrameParams f1 = fp;
-    f1.big_pass = 1;
-    gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f1, b);
-    gs_big_split_kernel<<<1024, 256, 0, s>>>(f1, b);
-    launch_big_buckets(f1, b, s);
-    f1.blend_cont = 1;
-    gs_blend_kernel<4><<<grid, block, 0, s>>>(f1, b);
-  }
+}
+
+void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
+  if (waves == 0 || !fp.lazy) return;
+  const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
+  const unsigned block = 64 * GS_BLEND_WPG;
+  // the big lists whose blend outlived the prefix: sorted in full, then
+  // their saved waves continue (nothing to do when none was flagged)
+  FrameParams f1 = fp;
+  f1.big_pass = 1;
+  gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f1, b);
+  gs_big_split_kernel<<<1024, 256, 0, s>>>(f1, b);
+  launch_big_buckets(f1, b, s);
+  f1.blend_cont = 1;
+  gs_blend_cont_kernel<<<grid, block, 0, s>>>(f1, b);
 }
 
 }  // namespace gsk

@@ -47,6 +47,7 @@ struct FrameParams {
                       //   blocks whose pixels outlive that prefix continue after a full sort
   int big_pass;       // big-list kernels: 0 = every big list, 1 = the lists flagged by the blend
   int blend_cont;     // blend: 1 = the continuation of the flagged big-list blocks
+  int count_records;  // blend: each wave writes the records it composited to blend_count
   int pow2;           // tile size, band stride and fxy[1] are powers of two: the
                       // projection divides by them with exact multiplies / shifts
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)
@@ -115,9 +116,17 @@ struct Buffers {
   uint32_t* footer;         // row-band group: counters[16] + reference list lengths[n_tiles]
                             //   of this frame, next to its BGR8 band in the all-gather slot
                             //   (written by the chunked scan; nullptr = none)
+  uint32_t* blend_count;    // [n_tiles * chunks_per_tile] records each blend wave staged
+  uint32_t* blend_count_cont;  //   ... and each continuation wave (GS_FLAG_PROFILE frames only)
+  uint32_t* group_sticky;   // row-band group: one device word per GPU, set by the scan of any
+                            //   frame of any of its band renderers that overflowed; copied into
+                            //   footer word kFootSticky before each all-gather (nullptr = none)
 };
 
-constexpr int GS_STAGE_EVENTS = 6;  // profile events: before project .. after blend
+// footer word that carries the group's sticky overflow bit (counters[15] is unused)
+constexpr int kFootSticky = 15;
+
+constexpr int GS_STAGE_EVENTS = 7;  // profile events: before project .. after blend, after the continuation
 constexpr int kSortLdsCap = 2048;  // largest tile list sorted by one workgroup (registers + LDS)
 constexpr uint32_t kSortRegCap = 256;  // largest tile list sorted in the registers of one wave
 constexpr size_t kBinLdsMax = 160 * 1024;  // LDS of one CU: chunk histograms up to 81920 tiles
@@ -131,6 +140,10 @@ void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s);
+// lazy big lists: the full sort of the lists the blend flagged + the continued blend (no-op otherwise)
+void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s);
+// *dst = *src, one word, ordered on stream s (the group's sticky bit into a footer)
+void launch_copy_word(hipStream_t s, uint32_t* dst, const uint32_t* src);
 
 // ---- the lattice-migration emulator (gs_lattice.hip, GS_FLAG_LATTICE)
 constexpr int kLatChan = 75;        // records per channel (edge_builder.cpp:18, ipu_rasteriser.cpp:307-308)

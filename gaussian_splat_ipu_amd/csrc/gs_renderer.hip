@@ -134,7 +134,7 @@ void release(gs_renderer* r) {
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
-  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat})
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount})
     if (p) (void)hipFree(p);
   free_pairs(r);
   if (r->h_counters) (void)hipHostFree(r->h_counters);
@@ -240,8 +240,8 @@ int profile_harvest(gs_renderer* r, ProfileSlot& s) {
   for (int k = 0; k < kStages; ++k) {
     float ms = 0.0f;
     GS_HIP(hipEventElapsedTime(&ms, s.ev[k], s.ev[k + 1]));
-    r->k_ms[k] += ms;
-    r->k_launches[k] += 1;
+    r->k_ms[kStageKernel[k]] += ms;
+    r->k_launches[kStageKernel[k]] += 1;
   }
   s.pending = false;
   return GS_OK;
@@ -279,9 +279,10 @@ int enqueue_lattice(gs_renderer* r, const gsk::FrameParams& fp, ProfileSlot* slo
   lb.bgr = r->buf.bgr;
   lb.host_counters = r->buf.host_counters;
   if (slot)
-    for (int k = 0; k < gsk::GS_STAGE_EVENTS - 1; ++k) GS_HIP(hipEventRecord(slot->ev[k], s));
+    for (int k = 0; k < gsk::GS_STAGE_EVENTS - 2; ++k) GS_HIP(hipEventRecord(slot->ev[k], s));
   gsk::launch_lattice(lp, lb, s);
   if (slot) {
+    GS_HIP(hipEventRecord(slot->ev[gsk::GS_STAGE_EVENTS - 2], s));
     GS_HIP(hipEventRecord(slot->ev[gsk::GS_STAGE_EVENTS - 1], s));
     slot->pending = true;
   }
@@ -322,9 +323,14 @@ int enqueue_frame(gs_renderer* r) {
   if (slot) GS_HIP(hipEventRecord(slot->ev[3], s));
   gsk::launch_sort(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[4], s));
-  gsk::launch_blend(fp, r->buf, s);
+  gsk::FrameParams fb = fp;
+  fb.count_records = (slot && r->buf.blend_count) ? 1 : 0;  // profiled frames count the blend's records
+  r->last_counted = fb.count_records != 0;
+  gsk::launch_blend(fb, r->buf, s);
+  if (slot) GS_HIP(hipEventRecord(slot->ev[5], s));
+  gsk::launch_blend_cont(fb, r->buf, s);
   if (slot) {
-    GS_HIP(hipEventRecord(slot->ev[5], s));
+    GS_HIP(hipEventRecord(slot->ev[6], s));
     slot->pending = true;
   }
   GS_HIP(hipGetLastError());
@@ -361,6 +367,17 @@ int finish_frame(gs_renderer* r) {
   r->stats.max_list = mx;
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
+  r->stats.blend_records = r->stats.blend_cont_records = 0;
+  if (r->last_counted && r->bcount_words) {  // profiled frame: what the blend staged
+    const size_t nw = std::min(r->bcount_words / 2, (size_t)r->n_tiles * (size_t)r->last_fp.chunks_per_tile);
+    std::vector<uint32_t> bc(2 * nw);
+    GS_HIP(hipMemcpy(bc.data(), r->buf.blend_count, nw * 4, hipMemcpyDeviceToHost));
+    GS_HIP(hipMemcpy(bc.data() + nw, r->buf.blend_count + r->bcount_words / 2, nw * 4, hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < nw; ++k) {
+      r->stats.blend_records += bc[k];
+      if (r->last_fp.lazy) r->stats.blend_cont_records += bc[nw + k];  // (the continuation ran)
+    }
+  }
   // the scan of EVERY frame ORs its overflow into the sticky word (several
   // frames may have run since the last sync; counters[3] is only the last one's)
   volatile uint32_t* sticky = r->h_counters + 16 + r->t_cap;
@@ -682,6 +699,21 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     const int rc2 = lattice_init(r, g, n);
     if (rc2 != GS_OK) return fail(rc2);
   }
+  if (r->profile && !lattice) {
+    // the blend's staged-record counts of profiled frames: one word per blend
+    // wave of the prefix pass, one per wave of the continuation
+    const uint32_t tw = cfg->tile_width, th = cfg->tile_height;
+    const size_t cpt = (tw % 8 == 0 && th % 8 == 0)    ? (size_t)(tw / 8) * (th / 8)
+                       : (tw % 16 == 0 && th % 4 == 0) ? (size_t)(tw / 16) * (th / 4)
+                                                       : (size_t)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
+    r->bcount_words = 2 * (size_t)r->t_cap * cpt;
+    if ((e = hipMalloc(&r->d_bcount, r->bcount_words * 4)) != hipSuccess)
+      return fail(hip_fail(e, "hipMalloc(blend counts)"));
+    if ((e = hipMemset(r->d_bcount, 0, r->bcount_words * 4)) != hipSuccess)
+      return fail(hip_fail(e, "hipMemset(blend counts)"));
+    r->buf.blend_count = (uint32_t*)r->d_bcount;
+    r->buf.blend_count_cont = r->buf.blend_count + r->bcount_words / 2;
+  }
   if (r->profile) {
     for (auto& s : r->ring)
       for (auto& ev : s.ev)
@@ -807,7 +839,8 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
     gsk::FrameParams fp = r->last_fp;
     fp.pair_cull = 0;
     gsk::Buffers bb = r->buf;
-    bb.footer = nullptr;  // (a group's all-gather slot belongs to the frame)
+    bb.footer = nullptr;        // (a group's all-gather slot belongs to the frame)
+    bb.group_sticky = nullptr;  // (this re-binning's overflow is handled here, not by the group)
     for (int attempt = 0; attempt < 8; ++attempt) {
       fp.pair_cap = r->pair_cap;
       bb.pairs = r->buf.pairs;

@@ -94,7 +94,10 @@ class InterfaceServer {
     bool detach = false;
   };
 
-  explicit InterfaceServer(int port) : port_(port) {}
+  // bind_host: the address to listen on (an IPv4 literal); the default is
+  // loopback -- a render server is reachable from other hosts only when the
+  // caller names an address (bin/splat --ui-host)
+  explicit InterfaceServer(int port, const char* bind_host = "127.0.0.1") : port_(port), host_(bind_host) {}
   ~InterfaceServer() { stop(); }
 
   // Launch the server thread and block until a client is connected and the
@@ -111,7 +114,7 @@ class InterfaceServer {
     ::setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
     sockaddr_in addr{};
     addr.sin_family = AF_INET;
-    addr.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (::inet_pton(AF_INET, host_.c_str(), &addr.sin_addr) != 1) return false;
     addr.sin_port = htons((uint16_t)port_);
     if (::bind(listen_fd_, (sockaddr*)&addr, sizeof(addr)) != 0 || ::listen(listen_fd_, 1) != 0) return false;
     std::printf("[info] User interface server listening on port %d\n", port_);
@@ -227,9 +230,13 @@ class InterfaceServer {
     } else if (name == "detach") {
       state_.detach = !p.empty() && p[0] != 0;
     } else if (name == "device") {
+      // u64 length + bytes; a length the payload does not hold (or an
+      // implausible one) is ignored, never trusted
+      if (p.size() < 8) return;
       uint64_t n = 0;
-      if (p.size() >= 8) std::memcpy(&n, p.data(), 8);
-      if (8 + n <= p.size()) state_.device.assign((const char*)p.data() + 8, (size_t)n);
+      std::memcpy(&n, p.data(), 8);
+      if (n > p.size() - 8 || n > kMaxDeviceName) return;
+      state_.device.assign((const char*)p.data() + 8, (size_t)n);
     } else {
       return;  // not a client -> server packet
     }
@@ -274,7 +281,9 @@ class InterfaceServer {
     return hdr[1] == 0 || recv_all(payload.data(), hdr[1]);
   }
 
+  static constexpr uint64_t kMaxDeviceName = 64;
   int port_;
+  std::string host_;
   int listen_fd_ = -1, conn_ = -1;
   std::thread thread_;
   std::atomic<bool> stop_server_{false};

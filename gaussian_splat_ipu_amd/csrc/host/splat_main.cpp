@@ -44,7 +44,7 @@
 namespace {
 
 struct Args {
-  std::string input, device = "cpu", log_level = "info", out = "test.png";
+  std::string input, device = "cpu", log_level = "info", out = "test.png", ui_host = "127.0.0.1";
   int ui_port = 0, frames = 1, gpus = 0;
   bool lattice = false;
   uint32_t width = 1280, height = 720, tw = 32, th = 20;
@@ -54,6 +54,7 @@ struct Args {
 void usage() {
   std::printf(
       "splat --input <file.ply|file.xyz> [--device cpu|gpu] [--log-level info] [--ui-port 0]\n"
+      "      [--ui-host 127.0.0.1 (the address the UI server listens on; 0.0.0.0 = every interface)]\n"
       "      [--gpus N] [--width 1280] [--height 720] [--tile-width 32] [--tile-height 20]\n"
       "      [--frames 1] [--scale-div 0.1] [--out test.png] [--lattice]\n");
 }
@@ -79,6 +80,8 @@ bool parse(int argc, char** argv, Args& a) {
       a.log_level = val();
     } else if (k == "--ui-port") {
       a.ui_port = std::atoi(val());
+    } else if (k == "--ui-host") {
+      a.ui_host = val();
     } else if (k == "--gpus") {
       a.gpus = std::atoi(val());
     } else if (k == "--width") {
@@ -283,7 +286,7 @@ int main(int argc, char** argv) {
 #if GSPLAT_REMOTE_UI
     std::unique_ptr<gsui::InterfaceServer> ui;
     if (a.ui_port) {
-      ui.reset(new gsui::InterfaceServer(a.ui_port));
+      ui.reset(new gsui::InterfaceServer(a.ui_port, a.ui_host.c_str()));
       if (!ui->start(state)) throw std::runtime_error("remote UI server could not start");
       ui->updateFov(state.fov);
     }

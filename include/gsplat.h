@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 7
+#define GSPLAT_ABI_VERSION 8
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -159,6 +159,12 @@ typedef struct gs_frame_stats {
   uint32_t bin_global;    /* ABI 5: 1 = the global-atomic binning path (tile
                              grids beyond one CU's LDS, or GS_FLAG_BIN_GLOBAL) */
   uint32_t reserved0;
+  uint64_t blend_records;      /* ABI 8, GS_FLAG_PROFILE renderers (frames with
+                                  stage events; else 0): tile-list records the
+                                  blend staged in the last frame (every wave
+                                  stops when its pixels have saturated; lazy
+                                  big lists: the sorted prefixes only)       */
+  uint64_t blend_cont_records; /* ... and the records the continuation staged */
 } gs_frame_stats;
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */
@@ -171,7 +177,10 @@ enum {
   GS_K_GATHER = 5,  /* group: the frame's all-gather on the communication
                        stream, from the local band's completion to the
                        gathered frame (includes waiting for the slowest rank) */
-  GS_K_COUNT = 6
+  GS_K_BLEND_CONT = 6, /* ABI 8: lazy big lists (16x16 tiles, lists > 2048): the
+                          full sort of the lists whose blend outlived the sorted
+                          prefix + the continued blend (gs_blend_cont) */
+  GS_K_COUNT = 7
 };
 
 typedef struct gs_renderer gs_renderer;
@@ -197,10 +206,18 @@ void gs_destroy(gs_renderer* r);
  * cfg->device and every frame ends with one ncclAllGather over a communicator
  * built from `id` (ncclCommInitRank).  Rank 0 creates the id
  * (gs_comm_id_create) and the caller hands its bytes to the other ranks (e.g.
- * a torch.distributed broadcast).  Every rank must call gs_render /
- * gs_render_async for every frame (the all-gather is collective); camera
- * inputs must be the same on every rank.  gs_read_bgr8 and
- * gs_read_tile_histogram return the whole frame on every rank. */
+ * a torch.distributed broadcast).
+ * Collective calls: gs_render, gs_render_async and gs_sync -- every rank calls
+ * them for the same frames, in the same order (each frame ends with an
+ * all-gather); camera inputs must be the same on every rank.  Their status and
+ * the split of later frames are decided from the gathered footers only, the
+ * same bytes on every rank (gs_group_decide), so every rank returns the same
+ * status and a blocking gs_render re-renders on all ranks or on none.
+ * Local calls: the readbacks (gs_read_*, gs_get_stats, gs_kernel_times, ...)
+ * wait for this rank's frames and return the last frame's status, but change
+ * neither the split nor the overflow state, so any subset of ranks may call
+ * them.  gs_read_bgr8 and gs_read_tile_histogram return the whole frame on
+ * every rank. */
 typedef struct gs_comm_id {
   unsigned char bytes[128]; /* ncclUniqueId */
 } gs_comm_id;
@@ -215,6 +232,20 @@ int gs_group_bands(gs_renderer* r, uint32_t* bounds, size_t n);
  * bounds = world + 1 entries.  Deterministic, so every rank derives the same
  * split from the same gathered histograms. */
 int gs_balanced_bands(const double* row_work, uint32_t rows, uint32_t world, uint32_t* bounds);
+/* ABI 8: the group's decision rule over one gathered frame (host only, no
+ * device), the function every rank applies to the same bytes.  footers: world
+ * x foot_words u32, band r's footer at r * foot_words: words 0..15 the band's
+ * frame counters (3 = this frame overflowed, 5/6 = binned pairs low/high, 15 =
+ * its GPU's sticky overflow bit since the last gs_sync), then the band's tile
+ * list lengths (rows frame_bounds[r] .. frame_bounds[r + 1] of tiles_x tiles).
+ * Returns GS_EOVERFLOW iff some band overflowed, else GS_OK.  next_bounds
+ * (world + 1, may be NULL) = the split of later frames: cur_bounds unless
+ * `rebalance` and the balanced split of this frame's histogram lowers the
+ * slowest band's work by more than 3 % (never after an overflow).  need_pairs
+ * (may be NULL) = the longest band pair list (capacity growth). */
+int gs_group_decide(const uint32_t* footers, size_t foot_words, uint32_t world, uint32_t tiles_x,
+                    uint32_t tiles_y, const uint32_t* frame_bounds, const uint32_t* cur_bounds, int rebalance,
+                    uint32_t* next_bounds, uint64_t* need_pairs);
 
 /* GS_FLAG_LATTICE renderers: the emulated lattice after the last frame. */
 typedef struct gs_lattice_stats {
@@ -259,7 +290,9 @@ int gs_get_stream(gs_renderer* r, void** hip_stream);
  * 408-420): synchronous.  Grows the pair capacity and re-renders on overflow. */
 int gs_render(gs_renderer* r);
 /* Enqueue one frame on the stream and return; gs_sync waits and reports
- * GS_EOVERFLOW if the capacity was exceeded (then call gs_render). */
+ * GS_EOVERFLOW if the capacity was exceeded by any frame since the last
+ * gs_sync (then call gs_render).  Row-band groups: collective, see
+ * gs_create_rank. */
 int gs_render_async(gs_renderer* r);
 int gs_sync(gs_renderer* r);
 

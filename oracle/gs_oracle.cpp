@@ -14,6 +14,7 @@
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
+#include <sched.h>
 #endif
 
 namespace {
@@ -979,3 +980,21 @@ void or_lattice_read(const or_lattice* L, float* rgba, uint32_t* hist, float* sl
 void or_lattice_destroy(or_lattice* L) { delete L; }
 
 }  // extern "C"
+
+// OpenMP team placement probe (bench.py's CPU baseline records the cores its
+// threads really ran on, not the calling thread's affinity mask)
+int or_omp_team_cpus(int nthreads, int* cpus, int cap, double spin_ms) {
+  const int nt = nthreads_or_default(nthreads);
+  int team = 0;
+#pragma omp parallel num_threads(nt)
+  {
+    const double t0 = omp_get_wtime();
+    volatile double x = 0.0;
+    while ((omp_get_wtime() - t0) * 1e3 < spin_ms) x = x + 1.0;
+    const int id = omp_get_thread_num();
+    if (id < cap) cpus[id] = sched_getcpu();
+#pragma omp single
+    team = omp_get_num_threads();
+  }
+  return team;
+}

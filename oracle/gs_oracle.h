@@ -104,6 +104,12 @@ int or_render(const float* g64, int64_t n, const or_frame* f, float* rgba, uint8
 
 /* Restated CPU point-splat path (cpu_rasteriser.cpp:9-92): image is H x W x 3
  * u8 (zeroed by caller); returns splatted count.  hist may be NULL. */
+/* The CPU the OpenMP team's threads run on: a parallel region of nthreads
+ * threads (0 = the runtime's default), each spinning ~spin_ms so the team is
+ * live at once, records sched_getcpu() into cpus[thread] (cap entries).
+ * Returns the team size.  bench.py's CPU baseline reports the distinct CPUs
+ * (and physical cores) of the team that actually ran. */
+int or_omp_team_cpus(int nthreads, int* cpus, int cap, double spin_ms);
 uint32_t or_point_splat(const float* xyz, int64_t n, const float* view_rm, const float* proj_rm,
                         int32_t width, int32_t height, int32_t tile_w, int32_t tile_h,
                         uint8_t* image, uint32_t* hist, int nthreads);

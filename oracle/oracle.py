@@ -108,6 +108,8 @@ def lib():
         L.or_lattice_total_slots.argtypes = [C.c_void_p]
         L.or_lattice_read.argtypes = [C.c_void_p, _FP, C.POINTER(C.c_uint32), _FP, C.POINTER(C.c_uint64)]
         L.or_lattice_destroy.argtypes = [C.c_void_p]
+        L.or_omp_team_cpus.restype = C.c_int
+        L.or_omp_team_cpus.argtypes = [C.c_int, C.POINTER(C.c_int), C.c_int, C.c_double]
         _lib = L
     return _lib
 
@@ -245,3 +247,10 @@ class Lattice:
             self.close()
         except Exception:
             pass
+
+
+def omp_team_cpus(nthreads: int = 0, spin_ms: float = 50.0):
+    """The CPU ids the OpenMP team's threads ran on (one per thread)."""
+    cpus = (C.c_int * 1024)()
+    n = lib().or_omp_team_cpus(int(nthreads), cpus, 1024, float(spin_ms))
+    return [int(cpus[i]) for i in range(min(n, 1024))]

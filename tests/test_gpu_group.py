@@ -207,3 +207,133 @@ def test_group_projected_and_tile_major(synth):
             blk[: src.shape[0], : src.shape[1]] = src
             want[t * T * T * 4:(t + 1) * T * T * 4] = blk.reshape(-1)
         assert_same_bits(tm, want, "tile-major RGBA")
+
+
+def _band_pairs(g, views, proj, W, H, T, bounds):
+    """Reference pairs of every band (tile rows bounds[r]..bounds[r + 1]) for
+    each view, from the oracle's lists (pair cull off: binned = reference)."""
+    from gaussian_splat_ipu_amd import camera
+    from oracle import oracle as O
+
+    tx = (W + T - 1) // T
+    out = []
+    for v in views:
+        f = O.make_frame(v, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0)
+        ts, _ = O.bin_lists(O.project(g, f), f)
+        lens = np.diff(ts.astype(np.int64))
+        out.append([int(lens[b0 * tx:b1 * tx].sum()) for b0, b1 in zip(bounds[:-1], bounds[1:])])
+    return np.array(out)  # [view][band]
+
+
+def _overflow_views(P, band):
+    """(light view, heavy view, cap): at the heavy view only `band` exceeds
+    cap; at the light view every band fits."""
+    others = np.delete(P, band, axis=1).max(axis=1) if P.shape[1] > 1 else np.zeros(P.shape[0], np.int64)
+    heavy = int(np.argmax(P[:, band] - others))
+    light = int(np.argmin(P.max(axis=1)))
+    cap = max(int(P[light].max()), int(others[heavy])) + 1
+    assert cap < P[heavy, band], "no view sequence overflows just one band"
+    return light, heavy, cap
+
+
+def test_async_overflow_in_one_band_is_every_members(clustered):
+    """only band 1 of 3 overflows, in frame 1 of 3 in-flight
+    frames (the last frame fits everywhere).  The status comes from the
+    gathered footers (band 1's sticky word rides in the last frame's footer),
+    so gs_sync reports GS_EOVERFLOW for the group; a repeated gs_sync without a
+    new frame reports the same; then one blocking gs_render of the heavy view
+    regrows every band renderer and matches the oracle."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd._lib import GS_EOVERFLOW, GsError
+
+    g, bb = clustered
+    W, H, T, G = 960, 540, 16, 3
+    _, proj = camera.headless(bb, W, H)
+    views = [camera.orbit_view(k) for k in range(0, 120, 8)]
+    with _group(g, W, H, T, num_gpus=G, device_ids=[0] * G, frames_in_flight=3, rebalance=False,
+                pair_cull=False, pair_capacity=1 << 26) as probe:
+        bounds = [b0 for b0, _ in probe.bands()] + [probe.bands()[-1][1]]
+    P = _band_pairs(g, views, proj, W, H, T, bounds)
+    light, heavy, cap = _overflow_views(P, 1)
+    with _group(g, W, H, T, num_gpus=G, device_ids=[0] * G, frames_in_flight=3, rebalance=False,
+                pair_cull=False, pair_capacity=cap) as s:
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        for v in (light, heavy, light):
+            s.set_view_wire(views[v])
+            s.execute_async()
+        with pytest.raises(GsError) as ei:
+            s.sync()
+        assert ei.value.status == GS_EOVERFLOW
+        with pytest.raises(GsError) as ei:  # the same frame's decision again
+            s.sync()
+        assert ei.value.status == GS_EOVERFLOW
+        assert s.stats()["n_pairs"] == int(P[light].sum())  # the last frame is the light view's
+        s.set_view_wire(views[heavy])
+        s.execute()  # grows and renders again on every band
+        assert s.stats()["pair_capacity"] >= P[heavy].max()
+        f, ref = _oracle(g, views[heavy], proj, W, H, T)
+        _check(s, g, f, ref, lists=False)
+        # and the pipeline is clean afterwards
+        for v in (light, heavy, light):
+            s.set_view_wire(views[v])
+            s.execute_async()
+        s.sync()
+
+
+def test_rank_world_one_async_overflow_sticky(clustered):
+    """The one-process-per-GPU path (RCCL world 1): the sticky word reaches the
+    footer by the copy on the communication stream before the ncclAllGather."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd._lib import GS_EOVERFLOW, GsError
+    from gaussian_splat_ipu_amd.splatter import comm_id_create
+
+    g, bb = clustered
+    W, H, T = 960, 540, 16
+    _, proj = camera.headless(bb, W, H)
+    views = [camera.orbit_view(k) for k in range(0, 120, 8)]
+    P = _band_pairs(g, views, proj, W, H, T, [0, (H + T - 1) // T])
+    light, heavy, cap = _overflow_views(P, 0)
+    with _group(g, W, H, T, comm_id=comm_id_create(), rank=0, world=1, device=0, frames_in_flight=3,
+                pair_cull=False, pair_capacity=cap) as s:
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        for v in (light, heavy, light):
+            s.set_view_wire(views[v])
+            s.execute_async()
+        with pytest.raises(GsError) as ei:
+            s.sync()
+        assert ei.value.status == GS_EOVERFLOW
+        s.set_view_wire(views[light])
+        s.execute()  # the sticky word was cleared by the sync: this frame fits
+        f, ref = _oracle(g, views[light], proj, W, H, T)
+        np.testing.assert_array_equal(s.get_frame_buffer(), ref["bgr"])
+        s.set_view_wire(views[heavy])
+        s.execute()
+        f, ref = _oracle(g, views[heavy], proj, W, H, T)
+        np.testing.assert_array_equal(s.get_frame_buffer(), ref["bgr"])
+        assert s.stats()["n_pairs"] == ref["stats"]["n_pairs"]
+
+
+def test_readback_on_one_member_keeps_the_split(synth):
+    """A readback (local call) between frames neither re-balances nor clears
+    the overflow state: the split only moves inside collective calls."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = synth
+    W, H, T = 640, 360, 16
+    view, proj = camera.headless(bb, W, H)
+    with _group(g, W, H, T, num_gpus=4, device_ids=[0] * 4, frames_in_flight=2) as s:
+        s.set_view_wire(view)
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        s.execute_async()
+        b0 = s.bands()
+        s.get_frame_buffer()  # local: waits, reads, changes nothing
+        s.get_histogram()
+        s.execute_async()
+        assert s.bands() == b0  # (the first re-balancing point is frame 8)
+        s.sync()
+        s.execute()  # collective: re-balances from its own frame
+        f, ref = _oracle(g, view, proj, W, H, T)
+        _check(s, g, f, ref, lists=False)

@@ -102,6 +102,40 @@ def test_remote_ui_cpu_device(built, pc12_scene, tmp_path):
             p.kill()
 
 
+
+def test_remote_ui_survives_malformed_device_packets(built, pc12_scene, tmp_path):
+    """the "device" packet's u64 length is the client's; lengths the
+    payload does not hold (2^64 - 1 wraps 8 + n), or implausibly long names,
+    are ignored -- the server keeps serving and the next valid packets apply."""
+    import struct
+
+    from oracle import oracle as O
+
+    g, bb = pc12_scene
+    xyz = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16)[:, 0:3]
+    p, c, out = _start(tmp_path, "cpu")
+    try:
+        c.recv()
+        c.frame()
+        c.send_raw("device", struct.pack("<Q", (1 << 64) - 1))           # wraps 8 + n
+        c.send_raw("device", struct.pack("<Q", (1 << 64) - 4) + b"gpu")   # wraps to a small sum
+        c.send_raw("device", struct.pack("<Q", 100) + b"x" * 100)        # longer than any device name
+        c.send_raw("device", b"\x01\x02")                                 # no length at all
+        c.send("X", 100.0)
+        view, proj, _ = _camera(bb, X=100.0)
+        rimg, rhist, _ = O.point_splat(xyz, view, proj, W, H, T, T)
+        for _ in range(400):
+            hist, img = c.frame()
+            if np.array_equal(hist, rhist):
+                break
+        else:
+            raise AssertionError("the server stopped applying state after malformed packets")
+        np.testing.assert_array_equal(img, rimg)  # still the CPU device
+        _stop(p, c, out)
+    finally:
+        if p.poll() is None:
+            p.kill()
+
 @pytest.mark.gpu
 def test_remote_ui_switches_to_the_gpu_device(built, pc12_scene, tmp_path):
     """The "device" packet moves the loop to the Gaussian frame path (the UI's
