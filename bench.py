@@ -74,6 +74,9 @@ def parse():
                     help="N = 1 through the group path (gs_create_rank, world 1: one ncclAllGather per "
                     "frame), to exercise the multi-GPU frame path on one GPU")
     ap.add_argument("--no-rebalance", action="store_true", help="group: keep the first (equal-rows) split")
+    ap.add_argument("--fast-exp", action="store_true",
+                    help="GS_FLAG_FAST_EXP (opt-in): the blend's exp from the hardware exp2, per-pixel RGBA within "
+                    "the tolerance of tests/test_gpu_fast_exp.py instead of bit-exact (not the headline mode)")
     ap.add_argument("--cpu-frames", type=int, default=20, help="timed CPU baseline frames (median)")
     ap.add_argument("--cpu-warmup", type=int, default=3)
     ap.add_argument("--cpu-budget-s", type=float, default=30.0,
@@ -215,12 +218,12 @@ def main():
             else:
                 cid = comm_id_create()
             R = [GpuSplatter(g, fb, device=local, comm_id=cid, rank=rank, world=world, frames_in_flight=F,
-                             profile=True, rebalance=not a.no_rebalance)]
+                             profile=True, rebalance=not a.no_rebalance, fast_exp=a.fast_exp)]
         else:  # --split S: S bands emulated on this GPU
             R = [GpuSplatter(g, fb, num_gpus=split, device_ids=[local] * split, frames_in_flight=F,
-                             profile=True, rebalance=not a.no_rebalance)]
+                             profile=True, rebalance=not a.no_rebalance, fast_exp=a.fast_exp)]
     else:
-        R = [GpuSplatter(g, fb, device=local, profile=(f == 0)) for f in range(F)]
+        R = [GpuSplatter(g, fb, device=local, profile=(f == 0), fast_exp=a.fast_exp) for f in range(F)]
     for r in R:
         setup(r)
     s = R[0]
@@ -337,8 +340,8 @@ def main():
                               "note": "ncclAllGather on the comm stream, local band done -> frame gathered "
                                       "(includes waiting for the slowest rank)"}
             continue
-        if name == "blend_cont" and not cnt:
-            continue
+        if name == "blend_cont" and (not cnt or not rec_cont):
+            continue  # (no lazy continuation ran: its stage is two back-to-back events)
         b = alg_bytes(name, T_b, P_b, a.n, px, rec, rec_cont)
         kern[name] = {
             "avg_ms": round(avg_ms, 5),
@@ -416,6 +419,8 @@ def main():
             workload = f"synthetic {a.n} Gaussians, {W}x{H}, {TW}x{TW} tiles, headless camera, fxy[1]={a.scale_div}"
         if a.split > 1:
             metric = f"frames/sec, {a.split} row bands emulated on one MI355X (group path, device-copy gather)"
+        if a.fast_exp:
+            metric += " [GS_FLAG_FAST_EXP: RGBA within tolerance, not bit-exact]"
         if world > 1:
             par = f"row-band x{world}: one process per GPU, work-balanced contiguous bands, one ncclAllGather/frame"
         elif a.split > 1:
@@ -510,6 +515,19 @@ def cpu_baseline(a, g, view, proj, W, H, TW, np):
     xyz = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16)[:, 0:3]
     tp, npf = timed(lambda: O.point_splat(xyz, view, proj, W, H, TW, TW, nthreads=threads), a.cpu_frames,
                     a.cpu_warmup)
+    # BASELINE configs[0] (bonsai-7k-mini.ply at 720p on the CPU rasteriser; the
+    # file is absent): its SURVEY §8 d substitute, the seeded synthetic 7k scene
+    # and point_cloud_12 at 1280x720 / 32x20 through the same CPU point splatter
+    from gaussian_splat_ipu_amd import scene as gscene
+
+    c1 = {}
+    for name, ply in (("synthetic_7k_seed7", gscene.synthetic(gscene.SynthSpec(n=7000, seed=7, sh_degree=3))),
+                      ("point_cloud_12", gscene.load_ply(os.path.join(ROOT, "tests", "golden", "point_cloud_12.ply")))):
+        g1, bb1 = gscene.prepare_scene(ply)
+        v1, p1 = camera.headless(bb1, 1280, 720)
+        x1 = np.ascontiguousarray(g1).view(np.float32).reshape(-1, 16)[:, 0:3].copy()
+        t1, n1 = timed(lambda: O.point_splat(x1, v1, p1, 1280, 720, 32, 20, nthreads=threads), 50, 3)
+        c1[name] = {"points": int(len(x1)), "frames_per_s": round(1.0 / t1, 1), "median_of": n1}
     host = (f"{os.cpu_count()} CPUs on the host, {n_cpus} in this thread's affinity mask, {phys} physical "
             f"cores among those (lscpu); "
             f"OMP_NUM_THREADS={omp_env} (the GPU box's CPU share), OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}; "
@@ -527,6 +545,10 @@ def cpu_baseline(a, g, view, proj, W, H, TW, np):
                   f"workload through the CPU oracle Gaussian rasteriser (OpenMP, {threads} threads)",
         "host": host,
         "gaussians_per_sec": round(a.n / tc, 1),
+        "config1_substitute": {
+            "workload": "BASELINE configs[0] substitute (bonsai-7k-mini.ply is absent): 1280x720, 32x20 tiles, "
+                        "the reference's CPU point splatter (cpu_rasteriser.cpp:9-92) restated",
+            "threads": threads, **c1},
         "reference_cpu_path": {
             "value": round(1.0 / tp, 2),
             "unit": "frames/s",

@@ -25,6 +25,7 @@ GS_FLAG_NO_PAIR_CULL = 64
 GS_FLAG_NO_REBALANCE = 128
 GS_FLAG_GATHER_COPY = 256
 GS_FLAG_LATTICE = 512
+GS_FLAG_FAST_EXP = 1024
 GS_MAX_GPUS = 16
 GS_LAYOUT_ROW_MAJOR = 0
 GS_LAYOUT_REF_TILE_MAJOR = 1

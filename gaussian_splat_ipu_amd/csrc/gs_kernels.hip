@@ -1,20 +1,27 @@
 // gs_kernels.hip -- the frame path as hand-written HIP for gfx950 (MI355X).
 //
 //   project  one thread per Gaussian: MVP transform, clip-space EWA covariance,
-//            eigenvalue radius, guard band + z cull, conic, tile rectangle,
-//            per-tile list lengths (global atomics)
+//            eigenvalue radius, guard band + z cull, conic, alpha footprint
+//            (pcut + integer pixel box), tile rectangle and its alpha-box cut;
+//            V per 256-Gaussian block (no single-address atomics)
 //            reference: codelets.cpp:437-499, ipu_geometry.hpp:247-383
-//   scan     one workgroup: exclusive scan of the per-tile lengths
-//   emit     one thread per Gaussian: scatter (depth key << 32 | index) into
-//            its tiles' segments (the converged lattice of codelets.cpp:194-293,
-//            507-602 in one frame)
-//   sort     one workgroup per tile: bitonic sort of the tile's keys in LDS;
-//            lists longer than kSortLdsCap go to a block-wide LSD radix sort
-//            with wave64 ballot multisplit ranking
+//   bin      chunked LDS binning: count (one 1024-thread workgroup per chunk of
+//            Gaussians keeps the chunk's per-tile histogram in LDS; runs of
+//            equal rectangles add once), colscan (per tile, exclusive scan over
+//            the chunks), scan_multi (tile starts, sort queues, frame counters
+//            straight into mapped host memory), emit (LDS cursors per tile;
+//            runs of equal rectangles reserve their slots with one atomic)
+//            -- the converged lattice of codelets.cpp:194-293, 507-602 in one
+//            frame; global-atomic fallback kernels for huge tile grids
+//   sort     one launch for all lists, longest first: register bitonic
+//            networks (DPP / permlane) for <= 256 keys, register runs + LDS
+//            merge path for <= 2048, and a sample sort over many workgroups
+//            (lazy: only each big list's nearest keys before the blend)
 //            reference: codelets.cpp:295-356 (per-tile quicksort by clip z)
-//   blend    one wave per 64-pixel chunk of a tile: front-to-back alpha
-//            compositing with the Gaussian records read by wave-uniform
-//            (scalar) loads; RGBA f32 + BGR8 stores fused
+//   blend    one wave per 8x8 pixel block of a tile: batches of 64 records
+//            staged in LDS, one 64-bit record mask per pixel from column / row
+//            ballots, a per-lane walk of the mask (one record per step) with
+//            the reference's early exit; RGBA f32 + BGR8 stores fused
 //            reference: codelets.cpp:358-421, ipu_rasteriser.cpp:131-144
 //
 // Arithmetic: fp32 everywhere, compiled with -ffp-contract=off and the default
@@ -873,14 +880,30 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
         r[k] = live[k] ? rects[i] : kEmptyRect;
         dk[k] = live[k] ? b.depth_key[i] : 0u;
       }
+      // Consecutive Gaussians (Morton order) often share their rectangle: the
+      // first lane of each run of equal rectangles reserves the run's slots
+      // with one LDS atomic per tile and the run's lanes take consecutive
+      // slots from it (the pairs of a tile are sorted afterwards, so their
+      // order within the chunk's segment is free).
+      const int lane = threadIdx.x & 63;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
+        const uint32_t px = (uint32_t)__shfl_up((int)r[k].x, 1, 64), py = (uint32_t)__shfl_up((int)r[k].y, 1, 64);
+        const bool start = lane == 0 || r[k].x != px || r[k].y != py;
+        const unsigned long long st = ballot64(start);
+        const unsigned long long upto = st & ((2ull << lane) - 1ull);  // (lane 63: 2 << 63 wraps to 0 - 1 = all)
+        const int head = 63 - __builtin_clzll(upto);
+        const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
+        const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
         const uint32_t x0 = r[k].x & 0xFFFFu, x1 = r[k].x >> 16, y0 = r[k].y & 0xFFFFu, y1 = r[k].y >> 16;
-        if (x0 > x1) continue;
+        if (x0 > x1) continue;  // (the whole run)
         const unsigned long long key = ((unsigned long long)dk[k] << 32) | (uint32_t)(i0 + k * 1024 + (int)threadIdx.x);
+        const uint32_t rank = (uint32_t)(lane - head);
         for (uint32_t y = y0; y <= y1; ++y)
           for (uint32_t x = x0; x <= x1; ++x) {
-            const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
+            uint32_t base = 0;
+            if (start) base = atomicAdd(&cnt[y * fp.tiles_x + x], len);
+            const uint32_t pos = (uint32_t)__shfl((int)base, head, 64) + rank;
             if (pos < fp.pair_cap) b.pairs[pos] = key;
           }
       }
@@ -1927,23 +1950,36 @@ __device__ __forceinline__ float gs_expf_inrange(float x) {
   return __builtin_amdgcn_ldexpf(p, (int)k);  // == p * 2^k: k in [-115, 0], p in [0.7, 1.5]
 }
 
+// GS_FLAG_FAST_EXP: e^x = 2^t with t = x log2(e) split into t + lo by an fma
+// (lo carries the product's rounding error), then 2^(t + lo) = 2^t (1 + lo ln 2)
+// with the hardware exp2.  A few ulp, for every x (NaN in, NaN out; large
+// negative x -> 0); not the oracle's bits, so opt-in only.
+__device__ __forceinline__ float gs_expf_hw(float x) {
+  const float t = x * 1.44269502162933349609f;
+  const float lo = __builtin_fmaf(x, 1.925963033500011079e-08f, __builtin_fmaf(x, 1.44269502162933349609f, -t));
+  const float p = __builtin_amdgcn_exp2f(t);
+  return __builtin_fmaf(p * lo, 0.693147182464599609375f, p);
+}
+
+// exponential variants of the blend loop
+enum BlendExp { kExpExact = 0, kExpInRange = 1, kExpHw = 2 };
+
 // One staged record (48 B, see the project kernel):
 //   r0 = (mx, my, k0, k2)   r1 = (k1, pcut, r, g)   r2 = (b, opacity, box_x, box_y)
 // One pixel's front-to-back step for one record (renderTile inner loop,
 // codelets.cpp:385-411), split in two: blend_power_exp (independent of the
-// pixel's state, so two records' exponentials overlap) and blend_composite
-// (branch-free: every quantity is computed and the state update selected).
-// The pairs (dx, dy), (k0 dx, k2 dy), (r, g) and (b, opacity) are computed as
-// packed fp32 (each half is the same IEEE operation as the scalar
-// expression).  FAST: the record's pcut >= -80, so any power the update
-// accepts lies in [-80, 0], where gs_expf_inrange == gs_expf bit for bit.
-template <bool FAST>
+// pixel's state) and blend_composite (the decisions, then the state update).
+// All scalar fp32 (the build disables SLP packing: packed fp32 chains were
+// 15 % slower).  kExpInRange: the batch's records all have pcut >= -80, so
+// any power the update accepts lies in [-80, 0], where gs_expf_inrange ==
+// gs_expf bit for bit; kExpHw: GS_FLAG_FAST_EXP.
+template <int EXP>
 __device__ __forceinline__ float blend_power_exp(const Px& q, const float4& r0, const float4& r1,
                                                  float& power) {
   const float dx = r0.x - q.p.x, dy = r0.y - q.p.y;
   const float k0 = r0.z, k2 = r0.w, k1 = r1.x;
   power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
-  return FAST ? gs_expf_inrange(power) : gs_expf(power);
+  return EXP == kExpHw ? gs_expf_hw(power) : (EXP == kExpInRange ? gs_expf_inrange(power) : gs_expf(power));
 }
 
 __device__ __forceinline__ void blend_composite(Px& q, float power, float e, const float4& r1,
@@ -1978,34 +2014,24 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers
   dst[2] = to_u8(o0);
 }
 
-// The records of a lane's batch mask (bit k = staged record k), two per
-// iteration in list order: their exponentials are independent, the
-// compositing is sequential.  The mask is walked as two 32-bit words (w, then
-// h): a lane moves on to its high word as soon as its low word is used up,
-// inside the same loop, so the wave's iteration count is the largest number of
-// records of any lane, not the largest low-word count plus the largest
-// high-word count (blend 79.0 -> 77.3 us, interleaved A/B, bit-exact).  The
-// lane stops as soon as its pixel has saturated (the reference's `break`).
-template <bool FAST>
+// The records of a lane's batch mask (bit k = staged record k), one per
+// iteration in list order, so the wave's iteration count is the largest
+// number of records of any lane.  (Round 3: one record per step instead of
+// two with independent exponentials -- a lane with an odd count no longer
+// evaluates a dead second record and the walk is simpler: blend 78.2 -> 75.6
+// us, 7 527 -> 7 728 frames/s, three interleaved A/B repeats, bit-exact.)
+// The lane stops as soon as its pixel has saturated (the reference's `break`).
+template <int EXP>
 __device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t w, uint32_t h) {
-  int off = 0;
-  if (w == 0u) { w = h; h = 0u; off = 32; }  // refill: the high word follows
-  while (w) {
-    const int ja = off + __builtin_ctz(w);
-    w &= w - 1u;
-    if (w == 0u) { w = h; h = 0u; off = 32; }
-    const bool two = w != 0u;
-    const int jb = two ? off + __builtin_ctz(w) : ja;
-    w &= w - 1u;
-    if (w == 0u) { w = h; h = 0u; off = 32; }
+  unsigned long long m = ((unsigned long long)h << 32) | w;
+  while (m) {
+    const int ja = __builtin_ctzll(m);
+    m &= m - 1ull;
     const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
-    const float4 b0 = st[0][jb], b1 = st[1][jb], b2 = st[2][jb];
-    float pa, pb;
-    const float ea = blend_power_exp<FAST>(q, a0, a1, pa);
-    const float eb = blend_power_exp<FAST>(q, b0, b1, pb);
+    float pa;
+    const float ea = blend_power_exp<EXP>(q, a0, a1, pa);
     blend_composite(q, pa, ea, a1, a2, true);
-    blend_composite(q, pb, eb, b1, b2, two);
-    w = q.done ? 0u : w;
+    m = q.done ? 0ull : m;
   }
 }
 
@@ -2030,7 +2056,7 @@ __device__ __forceinline__ void blend_count_store(const FrameParams& fp, const B
     (fp.blend_cont ? b.blend_count_cont : b.blend_count)[wid] = staged;
 }
 
-template <int BQW>
+template <int BQW, bool HWEXP>
 __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers& b) {
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wid = blockIdx.x * GS_BLEND_WPG + wave;
@@ -2238,10 +2264,12 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
     // list order = ascending bits: the low word's records, then the high word's.
     // Each lane leaves as soon as its own pixel has saturated.
     const uint32_t m_lo = q.done ? 0u : (uint32_t)m, m_hi = (uint32_t)(m >> 32);
-    if (fast) {
-      blend_records<true>(q, st, m_lo, q.done ? 0u : m_hi);
+    if (HWEXP) {
+      blend_records<kExpHw>(q, st, m_lo, q.done ? 0u : m_hi);
+    } else if (fast) {
+      blend_records<kExpInRange>(q, st, m_lo, q.done ? 0u : m_hi);
     } else {
-      blend_records<false>(q, st, m_lo, q.done ? 0u : m_hi);
+      blend_records<kExpExact>(q, st, m_lo, q.done ? 0u : m_hi);
     }
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
@@ -2266,15 +2294,17 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
   if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
 
-template <int BQW>
+// HWEXP: GS_FLAG_FAST_EXP (its own kernel: the default path's code is unchanged)
+template <int BQW, bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
-  blend_body<BQW>(fp, b);
+  blend_body<BQW, HWEXP>(fp, b);
 }
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
 // the prefix blend)
+template <bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_cont_kernel(FrameParams fp, Buffers b) {
-  blend_body<4>(fp, b);
+  blend_body<4, HWEXP>(fp, b);
 }
 
 
@@ -2364,12 +2394,21 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (waves == 0) return;
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
-  if (fp.blend_bqw == 4)
-    gs_blend_kernel<4><<<grid, block, 0, s>>>(fp, b);
-  else if (fp.blend_bqw == 8)
-    gs_blend_kernel<8><<<grid, block, 0, s>>>(fp, b);
-  else
-    gs_blend_kernel<0><<<grid, block, 0, s>>>(fp, b);
+  if (fp.fast_exp) {
+    if (fp.blend_bqw == 4)
+      gs_blend_kernel<4, true><<<grid, block, 0, s>>>(fp, b);
+    else if (fp.blend_bqw == 8)
+      gs_blend_kernel<8, true><<<grid, block, 0, s>>>(fp, b);
+    else
+      gs_blend_kernel<0, true><<<grid, block, 0, s>>>(fp, b);
+  } else {
+    if (fp.blend_bqw == 4)
+      gs_blend_kernel<4, false><<<grid, block, 0, s>>>(fp, b);
+    else if (fp.blend_bqw == 8)
+      gs_blend_kernel<8, false><<<grid, block, 0, s>>>(fp, b);
+    else
+      gs_blend_kernel<0, false><<<grid, block, 0, s>>>(fp, b);
+  }
 }
 
 void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
@@ -2385,7 +2424,10 @@ void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   gs_big_split_kernel<<<1024, 256, 0, s>>>(f1, b);
   launch_big_buckets(f1, b, s);
   f1.blend_cont = 1;
-  gs_blend_cont_kernel<<<grid, block, 0, s>>>(f1, b);
+  if (fp.fast_exp)
+    gs_blend_cont_kernel<true><<<grid, block, 0, s>>>(f1, b);
+  else
+    gs_blend_cont_kernel<false><<<grid, block, 0, s>>>(f1, b);
 }
 
 }  // namespace gsk

@@ -48,6 +48,7 @@ struct FrameParams {
   int big_pass;       // big-list kernels: 0 = every big list, 1 = the lists flagged by the blend
   int blend_cont;     // blend: 1 = the continuation of the flagged big-list blocks
   int count_records;  // blend: each wave writes the records it composited to blend_count
+  int fast_exp;       // blend: hardware exp2 (GS_FLAG_FAST_EXP, within a stated tolerance)
   int pow2;           // tile size, band stride and fxy[1] are powers of two: the
                       // projection divides by them with exact multiplies / shifts
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)

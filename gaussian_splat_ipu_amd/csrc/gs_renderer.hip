@@ -214,6 +214,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   }
   fp.big_pass = 0;
   fp.blend_cont = 0;
+  fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   {
     auto log2_exact = [](double v, int& sh) -> bool {  // v == 2^sh, sh in [-126, 126]
       int e = 0;
@@ -368,14 +369,23 @@ int finish_frame(gs_renderer* r) {
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
   r->stats.blend_records = r->stats.blend_cont_records = 0;
-  if (r->last_counted && r->bcount_words) {  // profiled frame: what the blend staged
-    const size_t nw = std::min(r->bcount_words / 2, (size_t)r->n_tiles * (size_t)r->last_fp.chunks_per_tile);
+  if (r->last_counted && r->bcount_words) {
+    // profiled frame: the list records the blend read.  The waves of a tile
+    // each stage a prefix of the same list (the tile's records come from HBM
+    // once, the other waves' reads hit L2), so a tile counts its longest prefix.
+    const size_t cpt = (size_t)r->last_fp.chunks_per_tile;
+    const size_t nw = std::min(r->bcount_words / 2, (size_t)r->n_tiles * cpt);
     std::vector<uint32_t> bc(2 * nw);
     GS_HIP(hipMemcpy(bc.data(), r->buf.blend_count, nw * 4, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(bc.data() + nw, r->buf.blend_count + r->bcount_words / 2, nw * 4, hipMemcpyDeviceToHost));
-    for (size_t k = 0; k < nw; ++k) {
-      r->stats.blend_records += bc[k];
-      if (r->last_fp.lazy) r->stats.blend_cont_records += bc[nw + k];  // (the continuation ran)
+    for (size_t t = 0; t + cpt <= nw; t += cpt) {
+      uint32_t m0 = 0, m1 = 0;
+      for (size_t k = t; k < t + cpt; ++k) {
+        m0 = std::max(m0, bc[k]);
+        m1 = std::max(m1, bc[nw + k]);
+      }
+      r->stats.blend_records += m0;
+      if (r->last_fp.lazy) r->stats.blend_cont_records += m1;  // (the continuation ran)
     }
   }
   // the scan of EVERY frame ORs its overflow into the sticky word (several

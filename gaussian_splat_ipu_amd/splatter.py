@@ -24,6 +24,7 @@ from ._lib import (
     GS_FLAG_BAND_CULL,
     GS_FLAG_GATHER_COPY,
     GS_FLAG_LATTICE,
+    GS_FLAG_FAST_EXP,
     GS_FLAG_NO_PAIR_CULL,
     GS_FLAG_NO_REBALANCE,
     GS_FLAG_BAND_INTERLEAVED,
@@ -96,6 +97,7 @@ class GpuSplatter:
         rank: int = 0,
         world: int = 1,
         lattice: bool = False,
+        fast_exp: bool = False,
     ):
         g = gaussians
         if isinstance(g, np.ndarray) and g.dtype != GAUSSIAN_DTYPE:
@@ -127,6 +129,7 @@ class GpuSplatter:
             | (0 if rebalance else GS_FLAG_NO_REBALANCE)
             | (GS_FLAG_GATHER_COPY if gather_copy else 0)
             | (GS_FLAG_LATTICE if lattice else 0)
+            | (GS_FLAG_FAST_EXP if fast_exp else 0)
         )
         cfg.num_gpus = int(num_gpus)
         if device_ids is not None:

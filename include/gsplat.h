@@ -130,6 +130,16 @@ typedef struct gs_config {
                                   tile_height == 0, one band, one device; the
                                   guard band uses the tile's own diagonal;
                                   gs_read_bins is unavailable. */
+#define GS_FLAG_FAST_EXP 1024u   /* ABI 8, opt-in: the blend takes exp() from the
+                                  hardware exp2 on an fma-split argument
+                                  (a few ulp; the oracle's portable expf is
+                                  not reproduced).  Tile lists, histograms and
+                                  stats stay bit-exact; per-pixel RGBA is within
+                                  the tolerance DESIGN.md states and
+                                  tests/test_gpu_fast_exp.py checks (SURVEY §8:
+                                  "per-pixel RGB within a stated float
+                                  tolerance").  Not the default: without it
+                                  every frame is bit-exact. */
 
 typedef enum gs_layout {
   GS_LAYOUT_ROW_MAJOR = 0,      /* H x W x 4, row-major                     */
@@ -161,9 +171,11 @@ typedef struct gs_frame_stats {
   uint32_t reserved0;
   uint64_t blend_records;      /* ABI 8, GS_FLAG_PROFILE renderers (frames with
                                   stage events; else 0): tile-list records the
-                                  blend staged in the last frame (every wave
-                                  stops when its pixels have saturated; lazy
-                                  big lists: the sorted prefixes only)       */
+                                  blend read in the last frame, per tile the
+                                  longest prefix any of its waves staged
+                                  (a wave stops when its pixels have
+                                  saturated; lazy big lists: the sorted
+                                  prefixes only)                             */
   uint64_t blend_cont_records; /* ... and the records the continuation staged */
 } gs_frame_stats;
 

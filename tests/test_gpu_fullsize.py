@@ -143,6 +143,37 @@ def test_config5_8m_4k_orbit_full_size(built, config5_scene, k):
     _check_frame(s, g, f, ref)
 
 
+
+def test_config5_8m_4k_8_band_group(built, config5_scene):
+    """configs[4] as the 8-GPU job renders it: the row-band group over 8 bands
+    (emulated on this GPU: repeated device ids, device-copy gather -- every
+    other part is the 8-GPU code), two orbit frames (the split re-balances
+    between them), every frame bit for bit the oracle's whole frame."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+    from oracle import oracle as O
+
+    g, proj, _ = config5_scene
+    W, H, T = 3840, 2160, 16
+    with GpuSplatter(g, TiledFramebuffer(W, H, T, T), num_gpus=8, device_ids=[0] * 8, frames_in_flight=2) as s:
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        for k in (0, 30):
+            view = camera.orbit_view(k)
+            s.set_view_wire(view)
+            s.execute()
+            s.execute()  # (the second frame: the big-list launch and a re-balanced split)
+            ref = O.render(g, O.make_frame(view, proj, W, H, T, T, camera.FOV_DEFAULT, 1.0))
+            st = s.stats()
+            assert st["n_pairs"] == ref["stats"]["n_pairs"]
+            assert st["max_list"] == ref["stats"]["max_list"]
+            np.testing.assert_array_equal(s.get_histogram(), ref["hist"])
+            np.testing.assert_array_equal(s.get_frame_buffer(), ref["bgr"])
+            _same_bits(s.get_rgba(), ref["rgba"], f"RGBA f32, orbit frame {k}")
+            b = s.bands()
+            assert len(b) == 8 and b[0][0] == 0 and b[-1][1] == (H + T - 1) // T
+
 @pytest.fixture(scope="module")
 def config5_scene(built):
     from gaussian_splat_ipu_amd import camera, scene

@@ -59,7 +59,7 @@ def main():
         from gaussian_splat_ipu_amd import dist as gdist
 
         cal = GpuSplatter(g, fb, device=0, write_rgba=False)
-        cal.set_view_wire(view)
+        cal.set_view_wire(views[0] if views else view)  # (config 5: the orbit's first view)
         cal.set_projection_wire(proj)
         cal.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
         cal.execute()
@@ -128,8 +128,13 @@ def main():
         if base is None:
             base = worst
         i = per_band.index(worst)
-        print(json.dumps({"bands": N, "inflight": a.inflight, "us_per_frame_by_band": [round(v, 1) for v in per_band],
-                          "slowest_us": round(worst, 1), "speedup": round(base / worst, 2),
+        mean = sum(per_band) / len(per_band)
+        print(json.dumps({"workload": "config5 8M/4K orbit" if a.config5 else f"config4 {a.n}/1080p",
+                          "bands": N, "inflight": a.inflight, "split": bands,
+                          "us_per_frame_by_band": [round(v, 1) for v in per_band],
+                          "slowest_us": round(worst, 1), "fastest_us": round(min(per_band), 1),
+                          "skew_slowest_over_mean": round(worst / mean, 3),
+                          "speedup": round(base / worst, 2),
                           "slowest_band_stage_us": stages[i]}), flush=True)
 
 
