@@ -74,6 +74,9 @@ def parse():
                     help="N = 1 through the group path (gs_create_rank, world 1: one ncclAllGather per "
                     "frame), to exercise the multi-GPU frame path on one GPU")
     ap.add_argument("--no-rebalance", action="store_true", help="group: keep the first (equal-rows) split")
+    ap.add_argument("--sh", action="store_true",
+                    help="opt-in view-dependent colour (gs_set_sh, SH degree 3 of the synthetic scene's f_dc / "
+                    "f_rest) -- not the reference's DC-only colour, so not the headline mode")
     ap.add_argument("--fast-exp", action="store_true",
                     help="GS_FLAG_FAST_EXP (opt-in): the blend's exp from the hardware exp2, per-pixel RGBA within "
                     "the tolerance of tests/test_gpu_fast_exp.py instead of bit-exact (not the headline mode)")
@@ -196,6 +199,9 @@ def main():
     else:
         ply = scene.synthetic(scene.SynthSpec(n=a.n, seed=a.seed, sh_degree=a.sh_degree))
     g, bb = scene.prepare_scene(ply)
+    sh = scene.sh_arrays(ply) if a.sh else None
+    if a.sh and sh[1] is None:
+        raise SystemExit("--sh needs a scene with f_rest (SH degree 3)")
     del ply
     view, proj = camera.headless(bb, W, H)
     fb = TiledFramebuffer(W, H, TW, TW)
@@ -206,6 +212,8 @@ def main():
         r.set_view_wire(view)
         r.set_projection_wire(proj)
         r.update_focal_lengths(camera.FOV_DEFAULT, a.scale_div)
+        if sh is not None:
+            r.set_sh(sh[0], sh[1], 3)
 
     # ------------------------------------------------------------ renderers
     split = a.split if a.split > 1 else world
@@ -421,6 +429,8 @@ def main():
             metric = f"frames/sec, {a.split} row bands emulated on one MI355X (group path, device-copy gather)"
         if a.fast_exp:
             metric += " [GS_FLAG_FAST_EXP: RGBA within tolerance, not bit-exact]"
+        if a.sh:
+            metric += " [gs_set_sh: view-dependent SH-3 colour]"
         if world > 1:
             par = f"row-band x{world}: one process per GPU, work-balanced contiguous bands, one ncclAllGather/frame"
         elif a.split > 1:

@@ -959,6 +959,15 @@ int set_profile_interval(Group* g, uint32_t every) {
   return GS_OK;
 }
 
+int set_sh(Group* g, const float* f_dc, const float* f_rest, size_t n, int degree) {
+  int rc = wait_frames(g);
+  if (rc != GS_OK && rc != GS_EOVERFLOW) return rc;
+  for (Member& m : g->mem)
+    for (gs_renderer* c : m.slot)
+      if ((rc = gsr::set_sh(c, f_dc, f_rest, n, degree)) != GS_OK) return rc;
+  return GS_OK;
+}
+
 int bands(Group* g, uint32_t* bounds, size_t n) {
   const std::vector<uint32_t>& b = g->last_slot >= 0 ? g->sinfo[g->last_slot].bounds : g->bounds;
   if (n < b.size()) {

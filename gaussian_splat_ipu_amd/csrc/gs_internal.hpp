@@ -48,6 +48,10 @@ struct gs_renderer {
   float proj_rm[16];
   float fov = 0.6981317f;  // glm::radians(40.f) (splat.cpp:170)
   float scale_div = 0.1f;  // lambda1 / 10 with lambda1 = 1 (InterfaceServer.hpp:238)
+  // gs_set_sh: the SH coefficients on the device ([16 x 3][n], device order)
+  void* d_sh = nullptr;
+  bool owns_sh = false;
+  int sh_degree = -1;  // < 0: off
 
   std::vector<uint32_t> perm;  // device index -> input index
 
@@ -141,6 +145,9 @@ int profile_harvest(gs_renderer* r, ProfileSlot& s);
 int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list, size_t n_list);
 int read_projected(gs_renderer* r, float* dst, size_t n_floats);
 int read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout);
+int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree);
+// the camera position (scene frame) of a row-major view matrix: -A^-1 t, double, rounded once
+void camera_position(const float* view_rm, float* campos);
 // the IPU tile-major layout (codelets.cpp:174-176) of a row-major RGBA f32 band
 void retile(const float* rm, size_t rows, size_t W, size_t tw, size_t th, int tiles_x, int n_tiles,
             float* dst);
@@ -170,6 +177,7 @@ int kernel_times(Group* grp, double* avg_ms, uint64_t* launches, int n);
 int reset_kernel_times(Group* grp);
 int set_profile_interval(Group* grp, uint32_t every);
 int bands(Group* grp, uint32_t* bounds, size_t n);
+int set_sh(Group* grp, const float* f_dc, const float* f_rest, size_t n, int degree);
 // the split rule (also exported as gs_balanced_bands)
 void balanced_bands(const double* work, int rows, int world, uint32_t* bounds);
 

@@ -215,6 +215,56 @@ __device__ __forceinline__ bool band_culled_fast(const FrameParams& fp, float4 m
   return band_culled<P2>(fp, vy, m3_mul(W, J), sg, 1e-5f * __builtin_fabsf(vy) + 0.05f);
 }
 
+// gs_set_sh (opt-in, not in the reference: its loader reads
+// f_dc only, file_io.cpp:66-68): the view-dependent colour of the 3DGS
+// convention (degree <= 3) for the direction from the camera to the mean.
+// The scene's frame has z negated against the PLY's (splat.cpp:93-100), so
+// the direction's z is negated back before the basis is evaluated.  Every
+// operation is written out in the order oracle/gs_oracle.cpp
+// (or_sh_colours) restates; degree 0 is the scene preparation's own colour,
+// max(0.28209479 f_dc + 0.5, 0) (splat.cpp:136-147, gs_scene.cpp), bit for bit.
+__device__ __forceinline__ float sh_coef(const Buffers& b, int n, int k, int c, int i) {
+  return b.sh[((size_t)(k * 3 + c)) * (size_t)n + (size_t)i];
+}
+
+__device__ __forceinline__ void sh_colour(const FrameParams& fp, const Buffers& b, int i, float4 mean, float4& col) {
+  const float ddx = mean.x - fp.campos[0], ddy = mean.y - fp.campos[1], ddz = mean.z - fp.campos[2];
+  const float len = __builtin_sqrtf((ddx * ddx + ddy * ddy) + ddz * ddz);
+  const float x = ddx / len, y = ddy / len, z = -ddz / len;
+  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+  float out[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float r = 0.28209479177387814f * sh_coef(b, fp.n, 0, c, i);
+    if (fp.sh_degree > 0) {
+      r = r - (0.4886025119029199f * y) * sh_coef(b, fp.n, 1, c, i);
+      r = r + (0.4886025119029199f * z) * sh_coef(b, fp.n, 2, c, i);
+      r = r - (0.4886025119029199f * x) * sh_coef(b, fp.n, 3, c, i);
+      if (fp.sh_degree > 1) {
+        r = r + (1.0925484305920792f * xy) * sh_coef(b, fp.n, 4, c, i);
+        r = r + (-1.0925484305920792f * yz) * sh_coef(b, fp.n, 5, c, i);
+        r = r + (0.31539156525252005f * ((2.0f * zz - xx) - yy)) * sh_coef(b, fp.n, 6, c, i);
+        r = r + (-1.0925484305920792f * xz) * sh_coef(b, fp.n, 7, c, i);
+        r = r + (0.5462742152960396f * (xx - yy)) * sh_coef(b, fp.n, 8, c, i);
+        if (fp.sh_degree > 2) {
+          r = r + ((-0.5900435899266435f * y) * (3.0f * xx - yy)) * sh_coef(b, fp.n, 9, c, i);
+          r = r + ((2.890611442640554f * xy) * z) * sh_coef(b, fp.n, 10, c, i);
+          r = r + ((-0.4570457994644658f * y) * ((4.0f * zz - xx) - yy)) * sh_coef(b, fp.n, 11, c, i);
+          r = r + ((0.3731763325901154f * z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy)) * sh_coef(b, fp.n, 12, c, i);
+          r = r + ((-0.4570457994644658f * x) * ((4.0f * zz - xx) - yy)) * sh_coef(b, fp.n, 13, c, i);
+          r = r + ((1.445305721320277f * z) * (xx - yy)) * sh_coef(b, fp.n, 14, c, i);
+          r = r + ((-0.5900435899266435f * x) * (xx - 3.0f * yy)) * sh_coef(b, fp.n, 15, c, i);
+        }
+      }
+    }
+    r = r + 0.5f;
+    out[c] = (r < 0.0f) ? 0.0f : r;  // glm::max(colour, vec3(0)) as the scene preparation
+  }
+  col.x = out[0];
+  col.y = out[1];
+  col.z = out[2];
+}
+
 template <bool P2>
 __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i) {
   bool rendered = false;
@@ -283,6 +333,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       col = b.colour[i];
       rot = b.rot[i];
     }
+    if (fp.sh_degree >= 0 && b.sh) sh_colour(fp, b, i, mean, col);
     const M3 C3 = cov3d(rot, div_p2<P2>(sg.x, fp.scale_div, fp.inv_sd), div_p2<P2>(sg.y, fp.scale_div, fp.inv_sd),
                         div_p2<P2>(sg.z, fp.scale_div, fp.inv_sd));
     M3 cov = m3_mul(m3_mul(m3_t(T), m3_t(C3)), T);

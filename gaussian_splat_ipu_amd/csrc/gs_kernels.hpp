@@ -49,6 +49,8 @@ struct FrameParams {
   int blend_cont;     // blend: 1 = the continuation of the flagged big-list blocks
   int count_records;  // blend: each wave writes the records it composited to blend_count
   int fast_exp;       // blend: hardware exp2 (GS_FLAG_FAST_EXP, within a stated tolerance)
+  int sh_degree;      // > 0: view-dependent colour from spherical harmonics (gs_set_sh)
+  float campos[3];    // camera position in the scene's (prepared) frame, for the SH direction
   int pow2;           // tile size, band stride and fxy[1] are powers of two: the
                       // projection divides by them with exact multiplies / shifts
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)
@@ -119,6 +121,8 @@ struct Buffers {
                             //   (written by the chunked scan; nullptr = none)
   uint32_t* blend_count;    // [n_tiles * chunks_per_tile] records each blend wave staged
   uint32_t* blend_count_cont;  //   ... and each continuation wave (GS_FLAG_PROFILE frames only)
+  const float* sh;          // gs_set_sh: [16 coefficients x 3 channels][n] (coefficient-major, device
+                            //   order): DC then f_rest 1..15 per channel (nullptr = off)
   uint32_t* group_sticky;   // row-band group: one device word per GPU, set by the scan of any
                             //   frame of any of its band renderers that overflowed; copied into
                             //   footer word kFootSticky before each all-gather (nullptr = none)

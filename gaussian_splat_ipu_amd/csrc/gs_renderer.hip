@@ -136,6 +136,7 @@ void release(gs_renderer* r) {
   if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
   for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount})
     if (p) (void)hipFree(p);
+  if (r->d_sh && r->owns_sh) (void)hipFree(r->d_sh);
   free_pairs(r);
   if (r->h_counters) (void)hipHostFree(r->h_counters);
   for (auto& s : r->ring)
@@ -215,6 +216,8 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.big_pass = 0;
   fp.blend_cont = 0;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
+  fp.sh_degree = r->d_sh ? r->sh_degree : -1;
+  camera_position(r->view_rm, fp.campos);
   {
     auto log2_exact = [](double v, int& sh) -> bool {  // v == 2^sh, sh in [-126, 126]
       int e = 0;
@@ -233,6 +236,68 @@ gsk::FrameParams make_params(const gs_renderer* r) {
     fp.inv_sd = std::ldexp(1.0f, -ssd);
   }
   return fp;
+}
+
+void camera_position(const float* v, float* campos) {
+  // view (row-major wire) = [A t; 0 1]: the camera sits at -A^-1 t
+  double a[3][3], t[3];
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) a[i][j] = v[i * 4 + j];
+    t[i] = v[i * 4 + 3];
+  }
+  const double c00 = a[1][1] * a[2][2] - a[1][2] * a[2][1];
+  const double c01 = a[1][2] * a[2][0] - a[1][0] * a[2][2];
+  const double c02 = a[1][0] * a[2][1] - a[1][1] * a[2][0];
+  const double det = (a[0][0] * c00 + a[0][1] * c01) + a[0][2] * c02;
+  double inv[3][3];
+  inv[0][0] = c00;
+  inv[1][0] = c01;
+  inv[2][0] = c02;
+  inv[0][1] = a[0][2] * a[2][1] - a[0][1] * a[2][2];
+  inv[1][1] = a[0][0] * a[2][2] - a[0][2] * a[2][0];
+  inv[2][1] = a[0][1] * a[2][0] - a[0][0] * a[2][1];
+  inv[0][2] = a[0][1] * a[1][2] - a[0][2] * a[1][1];
+  inv[1][2] = a[0][2] * a[1][0] - a[0][0] * a[1][2];
+  inv[2][2] = a[0][0] * a[1][1] - a[0][1] * a[1][0];
+  for (int i = 0; i < 3; ++i)
+    campos[i] = (float)(-((inv[i][0] * t[0] + inv[i][1] * t[1]) + inv[i][2] * t[2]) / det);
+}
+
+int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree) {
+  if (degree < 0) {
+    if (r->d_sh && r->owns_sh) (void)hipFree(r->d_sh);
+    r->d_sh = nullptr;
+    r->buf.sh = nullptr;
+    r->sh_degree = -1;
+    return GS_OK;
+  }
+  if (degree > 3 || n != r->n || !f_dc || (degree > 0 && !f_rest)) {
+    set_error("gs_set_sh: need degree 0..3, n equal to the scene's Gaussians, f_dc and (degree > 0) f_rest");
+    return GS_EINVAL;
+  }
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  if (r->frame_pending) GS_HIP(hipStreamSynchronize(r->stream));
+  const size_t nn = std::max<size_t>(n, 1);
+  const int K = (degree + 1) * (degree + 1);
+  // [16 x 3][n], device order; unused coefficients zero
+  std::vector<float> h((size_t)48 * nn, 0.0f);
+  for (size_t i = 0; i < n; ++i) {
+    const size_t o = r->perm[i];  // device index i holds input Gaussian o
+    for (int c = 0; c < 3; ++c) {
+      h[(size_t)(0 * 3 + c) * nn + i] = f_dc[o * 3 + c];
+      for (int k = 1; k < K; ++k) h[(size_t)(k * 3 + c) * nn + i] = f_rest[o * 45 + (size_t)c * 15 + (k - 1)];
+    }
+  }
+  if (!r->d_sh || !r->owns_sh) {
+    r->d_sh = nullptr;
+    GS_HIP(hipMalloc(&r->d_sh, h.size() * 4));
+    r->owns_sh = true;
+  }
+  GS_HIP(hipMemcpy(r->d_sh, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  r->buf.sh = (const float*)r->d_sh;
+  r->sh_degree = degree;
+  return GS_OK;
 }
 
 int profile_harvest(gs_renderer* r, ProfileSlot& s) {
@@ -1030,6 +1095,16 @@ int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor) {
   r->fov = fov_rad;
   r->scale_div = scale_divisor;
   return GS_OK;
+}
+
+int gs_set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree) {
+  if (!r) return GS_EINVAL;
+  if (r->grp) return gsg::set_sh(r->grp, f_dc, f_rest, n, degree);
+  if (r->lattice) {
+    set_error("gs_set_sh: the lattice emulator keeps the reference's DC colours");
+    return GS_EINVAL;
+  }
+  return gsr::set_sh(r, f_dc, f_rest, n, degree);
 }
 
 int gs_set_stream(gs_renderer* r, void* hip_stream) {

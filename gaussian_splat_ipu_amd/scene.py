@@ -126,3 +126,13 @@ def as_float16(g: np.ndarray) -> np.ndarray:
 def from_float16(a: np.ndarray) -> np.ndarray:
     a = np.ascontiguousarray(a, dtype=np.float32).reshape(-1, 16)
     return a.view(GAUSSIAN_DTYPE).reshape(-1)
+
+
+def sh_arrays(ply: Ply):
+    """(f_dc n x 3, f_rest n x 45 or None) of a 3DGS PLY in input order: the
+    view-dependent colour's coefficients (GpuSplatter.set_sh)."""
+    dc = np.stack([ply[f"f_dc_{c}"] for c in range(3)], 1).astype(np.float32)
+    rest = None
+    if ply.has("f_rest_0"):
+        rest = np.stack([ply[f"f_rest_{k}"] for k in range(45)], 1).astype(np.float32)
+    return dc, rest

@@ -200,6 +200,17 @@ class GpuSplatter:
         check(lib().gs_set_focal(self._h, fov, scale_divisor))
         self.fov, self.scale_divisor = fov, scale_divisor
 
+    def set_sh(self, f_dc, f_rest=None, degree: int = 3) -> None:
+        """Opt-in view-dependent colour (gs_set_sh): f_dc (n x 3) and f_rest
+        (n x 45, the PLY's f_rest_0..44) in input order; degree < 0 = off."""
+        if degree < 0:
+            check(lib().gs_set_sh(self._h, None, None, 0, -1), "gs_set_sh")
+            return
+        dc = np.ascontiguousarray(f_dc, np.float32).reshape(self.n, 3)
+        rest = None if f_rest is None else np.ascontiguousarray(f_rest, np.float32).reshape(self.n, 45)
+        check(lib().gs_set_sh(self._h, fptr(dc), None if rest is None else fptr(rest), self.n, int(degree)),
+              "gs_set_sh")
+
     def set_stream(self, stream_ptr: int | None) -> None:
         check(lib().gs_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
 

@@ -289,6 +289,17 @@ int gs_set_projection(gs_renderer* r, const float rowmajor[16]);
 /* Replaces IpuSplatter::updateFocalLengths(fx, fy) (ipu_rasteriser.cpp:108-110):
  * fxy = (fov radians, scale divisor lambda1/10). */
 int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor);
+/* ABI 8, opt-in view-dependent colour (the reference reads f_dc
+ * only, file_io.cpp:66-68): spherical-harmonic coefficients of the n
+ * Gaussians in INPUT order -- f_dc (n x 3) and f_rest (n x 3 x 15, the 3DGS
+ * PLY's f_rest_0..44: channel-major, 15 coefficients per channel; may be NULL
+ * when degree == 0) -- evaluated per frame for the direction from the camera
+ * (the inverse of the view matrix) to the mean, 3DGS convention, degree 0..3.
+ * degree < 0 switches it off (the gs_gaussian3d colours again).  Degree 0
+ * gives the scene preparation's own colour bit for bit.  Not parity-pinned by
+ * the reference (it never evaluates SH); the oracle restates the same fp32
+ * operations (or_sh_colours). */
+int gs_set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree);
 /* HIP stream (hipStream_t as void*) the frame is enqueued on; NULL = the
  * renderer's own stream. */
 int gs_set_stream(gs_renderer* r, void* hip_stream);

@@ -998,3 +998,60 @@ int or_omp_team_cpus(int nthreads, int* cpus, int cap, double spin_ms) {
   }
   return team;
 }
+
+// Opt-in SH colour (3DGS convention, computeColorFromSH of the INRIA
+// rasteriser restated; constants are its SH_C0..SH_C3).  Every operation in
+// the order written; -ffp-contract=off.
+void or_sh_colours(const float* g64, int64_t n, const float* f_dc, const float* f_rest, int degree,
+                   const float campos[3], float* out_g64) {
+  const float C0 = 0.28209479177387814f, C1 = 0.4886025119029199f;
+  const float C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f, -1.0925484305920792f,
+                       0.5462742152960396f};
+  const float C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f, 0.3731763325901154f,
+                       -0.4570457994644658f, 1.445305721320277f, -0.5900435899266435f};
+  for (int64_t i = 0; i < n; ++i) {
+    const float* g = g64 + i * 16;
+    float* o = out_g64 + i * 16;
+    for (int k = 0; k < 16; ++k) o[k] = g[k];
+    const float dx = g[0] - campos[0], dy = g[1] - campos[1], dz = g[2] - campos[2];
+    const float len = std::sqrt((dx * dx + dy * dy) + dz * dz);
+    const float x = dx / len, y = dy / len, z = -dz / len;  // the PLY frame's z
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    for (int c = 0; c < 3; ++c) {
+      const float* sh = f_rest ? f_rest + i * 45 + c * 15 - 1 : nullptr;  // sh[k], k = 1..15
+      float r = C0 * f_dc[i * 3 + c];
+      if (degree > 0) {
+        r = r - C1 * y * sh[1] + C1 * z * sh[2] - C1 * x * sh[3];
+        if (degree > 1) {
+          r = r + C2[0] * xy * sh[4] + C2[1] * yz * sh[5] + C2[2] * (2.0f * zz - xx - yy) * sh[6] +
+              C2[3] * xz * sh[7] + C2[4] * (xx - yy) * sh[8];
+          if (degree > 2)
+            r = r + C3[0] * y * (3.0f * xx - yy) * sh[9] + C3[1] * xy * z * sh[10] +
+                C3[2] * y * (4.0f * zz - xx - yy) * sh[11] + C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * sh[12] +
+                C3[4] * x * (4.0f * zz - xx - yy) * sh[13] + C3[5] * z * (xx - yy) * sh[14] +
+                C3[6] * x * (xx - 3.0f * yy) * sh[15];
+        }
+      }
+      r = r + 0.5f;
+      o[4 + c] = (r < 0.0f) ? 0.0f : r;  // glm::max(colour, vec3(0)) (splat.cpp:136-147)
+    }
+  }
+}
+
+void or_camera_position(const float* v, float* campos) {
+  double a[3][3], t[3];
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) a[i][j] = v[i * 4 + j];
+    t[i] = v[i * 4 + 3];
+  }
+  // adjugate rows / determinant
+  const double c00 = a[1][1] * a[2][2] - a[1][2] * a[2][1];
+  const double c01 = a[1][2] * a[2][0] - a[1][0] * a[2][2];
+  const double c02 = a[1][0] * a[2][1] - a[1][1] * a[2][0];
+  const double det = (a[0][0] * c00 + a[0][1] * c01) + a[0][2] * c02;
+  const double inv[3][3] = {
+      {c00, a[0][2] * a[2][1] - a[0][1] * a[2][2], a[0][1] * a[1][2] - a[0][2] * a[1][1]},
+      {c01, a[0][0] * a[2][2] - a[0][2] * a[2][0], a[0][2] * a[1][0] - a[0][0] * a[1][2]},
+      {c02, a[0][1] * a[2][0] - a[0][0] * a[2][1], a[0][0] * a[1][1] - a[0][1] * a[1][0]}};
+  for (int i = 0; i < 3; ++i) campos[i] = (float)(-((inv[i][0] * t[0] + inv[i][1] * t[1]) + inv[i][2] * t[2]) / det);
+}

@@ -104,6 +104,18 @@ int or_render(const float* g64, int64_t n, const or_frame* f, float* rgba, uint8
 
 /* Restated CPU point-splat path (cpu_rasteriser.cpp:9-92): image is H x W x 3
  * u8 (zeroed by caller); returns splatted count.  hist may be NULL. */
+/* Opt-in view-dependent colour (the product's gs_set_sh; the reference
+ * itself reads f_dc only, file_io.cpp:66-68): out_g64 = g64 with every
+ * Gaussian's colour.rgb replaced by the 3DGS spherical-harmonic colour of
+ * degree 0..3 for the direction from campos to its mean (scene frame, z
+ * negated back to the PLY frame), max(.., 0).  f_dc: n x 3, f_rest: n x 45
+ * (channel-major), both in input order.  Not parity-pinned by the reference. */
+void or_sh_colours(const float* g64, int64_t n, const float* f_dc, const float* f_rest, int degree,
+                   const float campos[3], float* out_g64);
+/* The camera position (scene frame) of a row-major view matrix [A t; 0 1]:
+ * -A^-1 t in double, rounded once. */
+void or_camera_position(const float* view_rm, float* campos);
+
 /* The CPU the OpenMP team's threads run on: a parallel region of nthreads
  * threads (0 = the runtime's default), each spinning ~spin_ms so the team is
  * live at once, records sched_getcpu() into cpus[thread] (cap entries).

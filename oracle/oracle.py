@@ -108,6 +108,8 @@ def lib():
         L.or_lattice_total_slots.argtypes = [C.c_void_p]
         L.or_lattice_read.argtypes = [C.c_void_p, _FP, C.POINTER(C.c_uint32), _FP, C.POINTER(C.c_uint64)]
         L.or_lattice_destroy.argtypes = [C.c_void_p]
+        L.or_sh_colours.argtypes = [_FP, C.c_int64, _FP, _FP, C.c_int, _FP, _FP]
+        L.or_camera_position.argtypes = [_FP, _FP]
         L.or_omp_team_cpus.restype = C.c_int
         L.or_omp_team_cpus.argtypes = [C.c_int, C.POINTER(C.c_int), C.c_int, C.c_double]
         _lib = L
@@ -254,3 +256,25 @@ def omp_team_cpus(nthreads: int = 0, spin_ms: float = 50.0):
     cpus = (C.c_int * 1024)()
     n = lib().or_omp_team_cpus(int(nthreads), cpus, 1024, float(spin_ms))
     return [int(cpus[i]) for i in range(min(n, 1024))]
+
+
+def camera_position(view_rm):
+    v = np.ascontiguousarray(view_rm, np.float32).reshape(16)
+    out = np.zeros(3, np.float32)
+    lib().or_camera_position(v.ctypes.data_as(_FP), out.ctypes.data_as(_FP))
+    return out
+
+
+def sh_colours(g64, f_dc, f_rest, degree: int, view_rm):
+    """The scene with every colour replaced by its SH colour for the camera of
+    view_rm (the product's gs_set_sh, restated)."""
+    g = _g(g64)
+    n = g.shape[0]
+    dc = np.ascontiguousarray(f_dc, np.float32).reshape(n, 3)
+    rest = None if f_rest is None else np.ascontiguousarray(f_rest, np.float32).reshape(n, 45)
+    out = np.empty_like(g)
+    cp = camera_position(view_rm)
+    lib().or_sh_colours(g.ctypes.data_as(_FP), n, dc.ctypes.data_as(_FP),
+                        None if rest is None else rest.ctypes.data_as(_FP), int(degree), cp.ctypes.data_as(_FP),
+                        out.ctypes.data_as(_FP))
+    return out.view(np.ascontiguousarray(g64).dtype).reshape(np.shape(g64))
