@@ -238,7 +238,12 @@ def lib():
                 "or `make -C gaussian_splat_ipu_amd/csrc` (there is no CPU fallback)"
             )
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        # a GSPLAT_LIB override may be an older A/B build: entry points it
+        # lacks are left unbound there (the default library must have all)
+        lenient = "GSPLAT_LIB" in os.environ
         for name, (res, args) in _SIGS.items():
+            if lenient and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
