@@ -9,8 +9,7 @@
 //            Gaussians keeps the chunk's per-tile histogram in LDS; runs of
 //            equal rectangles add once), colscan (per tile, exclusive scan over
 //            the chunks), scan_multi (tile starts, sort queues, frame counters
-//            straight into mapped host memory), emit (LDS cursors per tile;
-//            runs of equal rectangles reserve their slots with one atomic)
+//            straight into mapped host memory), emit (LDS cursors per tile)
 //            -- the converged lattice of codelets.cpp:194-293, 507-602 in one
 //            frame; global-atomic fallback kernels for huge tile grids
 //   sort     one launch for all lists, longest first: register bitonic
@@ -931,30 +930,14 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
         r[k] = live[k] ? rects[i] : kEmptyRect;
         dk[k] = live[k] ? b.depth_key[i] : 0u;
       }
-      // Consecutive Gaussians (Morton order) often share their rectangle: the
-      // first lane of each run of equal rectangles reserves the run's slots
-      // with one LDS atomic per tile and the run's lanes take consecutive
-      // slots from it (the pairs of a tile are sorted afterwards, so their
-      // order within the chunk's segment is free).
-      const int lane = threadIdx.x & 63;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint32_t px = (uint32_t)__shfl_up((int)r[k].x, 1, 64), py = (uint32_t)__shfl_up((int)r[k].y, 1, 64);
-        const bool start = lane == 0 || r[k].x != px || r[k].y != py;
-        const unsigned long long st = ballot64(start);
-        const unsigned long long upto = st & ((2ull << lane) - 1ull);  // (lane 63: 2 << 63 wraps to 0 - 1 = all)
-        const int head = 63 - __builtin_clzll(upto);
-        const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
-        const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
         const uint32_t x0 = r[k].x & 0xFFFFu, x1 = r[k].x >> 16, y0 = r[k].y & 0xFFFFu, y1 = r[k].y >> 16;
-        if (x0 > x1) continue;  // (the whole run)
+        if (x0 > x1) continue;
         const unsigned long long key = ((unsigned long long)dk[k] << 32) | (uint32_t)(i0 + k * 1024 + (int)threadIdx.x);
-        const uint32_t rank = (uint32_t)(lane - head);
         for (uint32_t y = y0; y <= y1; ++y)
           for (uint32_t x = x0; x <= x1; ++x) {
-            uint32_t base = 0;
-            if (start) base = atomicAdd(&cnt[y * fp.tiles_x + x], len);
-            const uint32_t pos = (uint32_t)__shfl((int)base, head, 64) + rank;
+            const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
             if (pos < fp.pair_cap) b.pairs[pos] = key;
           }
       }
@@ -2024,12 +2007,19 @@ enum BlendExp { kExpExact = 0, kExpInRange = 1, kExpHw = 2 };
 // 15 % slower).  kExpInRange: the batch's records all have pcut >= -80, so
 // any power the update accepts lies in [-80, 0], where gs_expf_inrange ==
 // gs_expf bit for bit; kExpHw: GS_FLAG_FAST_EXP.
+// The staging stores h0 = -0.5 k0 and h2 = -0.5 k2, so power = (h0 dx dx +
+// h2 dy dy) - k1 dx dy saves the reference's multiply by -0.5 per step.
+// Scaling by a power of two commutes with rounding, so every product and the
+// sum are the reference's values times -0.5 exactly -- except below the
+// normal range, where only powers of magnitude < 1e-37 can differ: those give
+// expf = 1 and the same sign tests either way.  (A/B: blend 75.1 -> 74.0 us
+// with the loads issued up front; parity tests bit-exact.)
 template <int EXP>
 __device__ __forceinline__ float blend_power_exp(const Px& q, const float4& r0, const float4& r1,
                                                  float& power) {
   const float dx = r0.x - q.p.x, dy = r0.y - q.p.y;
-  const float k0 = r0.z, k2 = r0.w, k1 = r1.x;
-  power = -0.5f * (k0 * dx * dx + k2 * dy * dy) - k1 * dx * dy;
+  const float h0 = r0.z, h2 = r0.w, k1 = r1.x;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
+  power = (h0 * dx * dx + h2 * dy * dy) - k1 * dx * dy;
   return EXP == kExpHw ? gs_expf_hw(power) : (EXP == kExpInRange ? gs_expf_inrange(power) : gs_expf(power));
 }
 
@@ -2079,6 +2069,7 @@ __device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t 
     const int ja = __builtin_ctzll(m);
     m &= m - 1ull;
     const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
+    asm volatile("" ::"v"(a1.z), "v"(a1.w), "v"(a2.x), "v"(a2.y));  // all loads issued up front
     float pa;
     const float ea = blend_power_exp<EXP>(q, a0, a1, pa);
     blend_composite(q, pa, ea, a1, a2, true);
@@ -2227,7 +2218,7 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
     staged += min(64u, L - base);
     // stage this batch
     const bool have = g_cur != 0xFFFFFFFFu;
-    st[0][lane] = a0;
+    st[0][lane] = make_float4(a0.x, a0.y, -0.5f * a0.z, -0.5f * a0.w);
     st[1][lane] = a1;
     st[2][lane] = a2;
     const uint32_t boxx = __float_as_uint(a2.z), boxy = __float_as_uint(a2.w);
