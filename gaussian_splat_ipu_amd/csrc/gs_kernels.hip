@@ -362,9 +362,9 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     float pcut;
     uint32_t b01, b23;
     alpha_footprint(vx, vy, k0, k1, k2, k3, fp, pcut, b01, b23);
-    rec[0] = make_float4(vx, vy, k0, k2);
-    rec[1] = make_float4(k1, pcut, col.x, col.y);
-    rec[2] = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
+    const float4 rec0 = make_float4(vx, vy, k0, k2);
+    const float4 rec1 = make_float4(k1, pcut, col.x, col.y);
+    const float4 rec2 = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
     if (fp.full_record) b.rec_tail[i] = make_float2(radius, cz);  // readback only
     if (within && cz < 0.0f) {  // codelets.cpp:493
       rendered = true;
@@ -405,6 +405,15 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
           for (uint32_t y = y0; y <= y1; ++y)
             for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&b.tile_count[y * fp.tiles_x + x], 1u);
       }
+    }
+    // the blend reads the records of binned Gaussians only: the others'
+    // 48 B stay unwritten (off-screen, culled, outside the band, or no tile
+    // met by the alpha box); the readback pass writes every record
+    const uint2 binned = fp.pair_cull ? crect : rect;
+    if (fp.full_record || (binned.x & 0xFFFFu) <= (binned.x >> 16)) {
+      rec[0] = rec0;
+      rec[1] = rec1;
+      rec[2] = rec2;
     }
   } else {  // empty slot: never binned; a neutral record for the readback
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1589,6 +1598,7 @@ __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buf
   __shared__ uint32_t s_maxl;
   const uint32_t n_big = b.counters[0];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool keep_buckets = fp.lazy && fp.big_pass == 1;
   if (tid == 0) s_maxl = 0;
   uint32_t carry = 0, carry_b = 0, maxl = 0;
   for (uint32_t j0 = 0; j0 < n_big; j0 += 1024) {
@@ -1600,7 +1610,7 @@ __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buf
       // pass 1 (lazy frames): only the lists whose blend outlived the prefix
       const bool use = fp.big_pass == 0 || b.big_flag[j] != 0u;
       c = use ? (L + kBigSeg - 1) / kBigSeg : 0u;
-      nb = use ? big_buckets(L) : 0u;
+      nb = (use || keep_buckets) ? big_buckets(L) : 0u;
       maxl = use ? max(maxl, L) : maxl;
       if (fp.lazy && fp.big_pass == 0) {
         b.big_flag[j] = 0u;
@@ -1633,7 +1643,9 @@ __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buf
       const uint32_t off = carry + before + inc - c;
       b.tile_cursor[j] = off;
       for (uint32_t q = 0; q < c; ++q) b.big_item[off + q] = j;  // segment -> list slot
-      b.bk_off[j] = carry_b + before_b + inc_b - nb;              // the list's first bucket
+      // the list's first bucket (the continuation of lazy frames keeps the
+      // numbering -- and the splitters -- of the frame's first pass)
+      if (!keep_buckets) b.bk_off[j] = carry_b + before_b + inc_b - nb;
     }
     carry += tot;
     carry_b += tot_b;
@@ -1695,6 +1707,14 @@ __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffe
       if (tid == 0u) {
         const uint32_t q = (uint32_t)(((unsigned long long)kLazyPrefix * S) / L);
         b.big_thr[j] = (uint32_t)(keys[min(q, S - 1u)] >> 32);
+      }
+      // and the buckets of the full sort the continuation may need, from this
+      // (larger) sample: the continuation's sample sort then needs no split
+      // pass of its own (splitters only size the buckets, never the order)
+      for (uint32_t t = tid; t < B; t += 256u) {
+        if (t + 1u < B) b.bk_spl[bo + t] = keys[((unsigned long long)(t + 1u) * S) / B - 1u];
+        b.bk_cnt[bo + t] = 0u;
+        b.bk_list[bo + t] = j;
       }
       __syncthreads();
       continue;
@@ -1912,6 +1932,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   const uint32_t n_bk = b.counters[0] ? b.counters[14] : 0u;
   for (uint32_t k = blockIdx.x; k < n_bk; k += gridDim.x) {
     const uint32_t j = b.bk_list[k];
+    if (fp.big_pass == 1 && b.big_flag[j] == 0u) continue;  // (uniform) lazy continuation: flagged lists only
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t bo = b.bk_off[j], B = big_buckets(L);
@@ -2463,7 +2484,7 @@ void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   FrameParams f1 = fp;
   f1.big_pass = 1;
   gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f1, b);
-  gs_big_split_kernel<<<1024, 256, 0, s>>>(f1, b);
+  // (the splitters of every big list were chosen by the frame's first split pass)
   launch_big_buckets(f1, b, s);
   f1.blend_cont = 1;
   if (fp.fast_exp)
