@@ -615,6 +615,44 @@ __device__ __forceinline__ bool block_live(const FrameParams& fp, const Buffers&
   return !fp.band_cull || b.block_rendered[i >> 8] != 0u;
 }
 
+// Wave-level aggregation of the binning atomics: when the union of the
+// wave's (64 consecutive, Morton-ordered) Gaussians' rectangles spans at most
+// GS_BIN_UNION tiles, the wave walks that union once, tile by tile, and each
+// tile gets ONE LDS atomic for all its lanes (a ballot's popcount) instead of
+// one per lane -- clustered scenes (config 5) put many lanes on the same
+// counters, whose atomics the LDS serialises.  0 disables it.
+#ifndef GS_BIN_UNION
+#define GS_BIN_UNION 8
+#endif
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// the wave's union of its lanes' non-empty rectangles (tx0 | tx1 << 16, ty0 |
+// ty1 << 16); its tile count (0: no lane has one)
+__device__ __forceinline__ uint32_t wave_union(uint2 r, uint32_t& ux0, uint32_t& ux1, uint32_t& uy0,
+                                               uint32_t& uy1) {
+  const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+  const bool ne = x0 <= x1 && y0 <= y1;
+  uint32_t lo = ne ? (x0 | (y0 << 16)) : 0xFFFFFFFFu;  // (x0, y0) minima, packed u16
+  uint32_t hi = ne ? (x1 | (y1 << 16)) : 0u;           // (x1, y1) maxima
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t ol = (uint32_t)__shfl_xor((int)lo, d, 64), oh = (uint32_t)__shfl_xor((int)hi, d, 64);
+    lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, lo), __builtin_bit_cast(u16x2, ol)));
+    hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hi), __builtin_bit_cast(u16x2, oh)));
+  }
+  ux0 = lo & 0xFFFFu;
+  uy0 = lo >> 16;
+  ux1 = hi & 0xFFFFu;
+  uy1 = hi >> 16;
+  if (ux0 > ux1 || uy0 > uy1) return 0u;
+  return (ux1 - ux0 + 1u) * (uy1 - uy0 + 1u);
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ void lds_zero(uint32_t* cnt, int words) {
   for (int i = threadIdx.x; i < words; i += blockDim.x) cnt[i] = 0;
 }
@@ -653,6 +691,23 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint2 r = rr[k], q = qq[k];
+        if (GS_BIN_UNION > 0) {
+          uint32_t ux0, ux1, uy0, uy1;
+          const uint32_t area = wave_union(r, ux0, ux1, uy0, uy1);
+          if (area == 0u) continue;  // (uniform)
+          if (area <= (uint32_t)GS_BIN_UNION) {
+            const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+            const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
+            for (uint32_t y = uy0; y <= uy1; ++y)
+              for (uint32_t x = ux0; x <= ux1; ++x) {
+                const bool in_r = x0 <= x && x <= x1 && y0 <= y && y <= y1;
+                const bool in_q = in_r && u0 <= x && x <= u1 && v0 <= y && y <= v1;
+                const uint32_t nr = (uint32_t)__popcll(ballot64(in_r)), nq = (uint32_t)__popcll(ballot64(in_q));
+                if (lane == 0 && nr) atomicAdd(&cnt[y * fp.tiles_x + x], (nr << 16) | nq);
+              }
+            continue;
+          }
+        }
         const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
         const uint32_t qx = (uint32_t)__shfl_up((int)q.x, 1, 64), qy = (uint32_t)__shfl_up((int)q.y, 1, 64);
         const bool start = lane == 0 || r.x != px || r.y != py || q.x != qx || q.y != qy;
@@ -942,8 +997,30 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t x0 = r[k].x & 0xFFFFu, x1 = r[k].x >> 16, y0 = r[k].y & 0xFFFFu, y1 = r[k].y >> 16;
-        if (x0 > x1) continue;
         const unsigned long long key = ((unsigned long long)dk[k] << 32) | (uint32_t)(i0 + k * 1024 + (int)threadIdx.x);
+        if (GS_BIN_UNION > 0) {
+          uint32_t ux0, ux1, uy0, uy1;
+          const uint32_t area = wave_union(r[k], ux0, ux1, uy0, uy1);
+          if (area == 0u) continue;  // (uniform)
+          if (area <= (uint32_t)GS_BIN_UNION) {
+            // one atomic per union tile reserves its lanes' slots, in lane order
+            const int lane = threadIdx.x & 63;
+            for (uint32_t y = uy0; y <= uy1; ++y)
+              for (uint32_t x = ux0; x <= ux1; ++x) {
+                const bool in = x0 <= x && x <= x1 && y0 <= y && y <= y1;
+                const unsigned long long m = ballot64(in);
+                if (m == 0ull) continue;  // (uniform)
+                const int first = __builtin_ctzll(m);
+                uint32_t base = 0u;
+                if (lane == first) base = atomicAdd(&cnt[y * fp.tiles_x + x], (uint32_t)__popcll(m));
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, first);
+                const uint32_t pos = base + lanes_below(m);
+                if (in && pos < fp.pair_cap) b.pairs[pos] = key;
+              }
+            continue;
+          }
+        }
+        if (x0 > x1) continue;
         for (uint32_t y = y0; y <= y1; ++y)
           for (uint32_t x = x0; x <= x1; ++x) {
             const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
