@@ -615,42 +615,16 @@ __device__ __forceinline__ bool block_live(const FrameParams& fp, const Buffers&
   return !fp.band_cull || b.block_rendered[i >> 8] != 0u;
 }
 
-// Wave-level aggregation of the binning atomics: when the union of the
-// wave's (64 consecutive, Morton-ordered) Gaussians' rectangles spans at most
-// GS_BIN_UNION tiles, the wave walks that union once, tile by tile, and each
-// tile gets ONE LDS atomic for all its lanes (a ballot's popcount) instead of
-// one per lane -- clustered scenes (config 5) put many lanes on the same
-// counters, whose atomics the LDS serialises.  0 disables it.
-#ifndef GS_BIN_UNION
-#define GS_BIN_UNION 8
-#endif
-
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-// the wave's union of its lanes' non-empty rectangles (tx0 | tx1 << 16, ty0 |
-// ty1 << 16); its tile count (0: no lane has one)
-__device__ __forceinline__ uint32_t wave_union(uint2 r, uint32_t& ux0, uint32_t& ux1, uint32_t& uy0,
-                                               uint32_t& uy1) {
-  const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
-  const bool ne = x0 <= x1 && y0 <= y1;
-  uint32_t lo = ne ? (x0 | (y0 << 16)) : 0xFFFFFFFFu;  // (x0, y0) minima, packed u16
-  uint32_t hi = ne ? (x1 | (y1 << 16)) : 0u;           // (x1, y1) maxima
+// wave-wide min of lo and max of hi, each two packed u16 (v_pk_min / max_u16)
+__device__ __forceinline__ void wave_minmax_u16x2(uint32_t& lo, uint32_t& hi) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t ol = (uint32_t)__shfl_xor((int)lo, d, 64), oh = (uint32_t)__shfl_xor((int)hi, d, 64);
     lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, lo), __builtin_bit_cast(u16x2, ol)));
     hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hi), __builtin_bit_cast(u16x2, oh)));
   }
-  ux0 = lo & 0xFFFFu;
-  uy0 = lo >> 16;
-  ux1 = hi & 0xFFFFu;
-  uy1 = hi >> 16;
-  if (ux0 > ux1 || uy0 > uy1) return 0u;
-  return (ux1 - ux0 + 1u) * (uy1 - uy0 + 1u);
-}
-
-__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 __device__ __forceinline__ void lds_zero(uint32_t* cnt, int words) {
@@ -691,23 +665,6 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint2 r = rr[k], q = qq[k];
-        if (GS_BIN_UNION > 0) {
-          uint32_t ux0, ux1, uy0, uy1;
-          const uint32_t area = wave_union(r, ux0, ux1, uy0, uy1);
-          if (area == 0u) continue;  // (uniform)
-          if (area <= (uint32_t)GS_BIN_UNION) {
-            const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
-            const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
-            for (uint32_t y = uy0; y <= uy1; ++y)
-              for (uint32_t x = ux0; x <= ux1; ++x) {
-                const bool in_r = x0 <= x && x <= x1 && y0 <= y && y <= y1;
-                const bool in_q = in_r && u0 <= x && x <= u1 && v0 <= y && y <= v1;
-                const uint32_t nr = (uint32_t)__popcll(ballot64(in_r)), nq = (uint32_t)__popcll(ballot64(in_q));
-                if (lane == 0 && nr) atomicAdd(&cnt[y * fp.tiles_x + x], (nr << 16) | nq);
-              }
-            continue;
-          }
-        }
         const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
         const uint32_t qx = (uint32_t)__shfl_up((int)q.x, 1, 64), qy = (uint32_t)__shfl_up((int)q.y, 1, 64);
         const bool start = lane == 0 || r.x != px || r.y != py || q.x != qx || q.y != qy;
@@ -998,28 +955,6 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
       for (int k = 0; k < 4; ++k) {
         const uint32_t x0 = r[k].x & 0xFFFFu, x1 = r[k].x >> 16, y0 = r[k].y & 0xFFFFu, y1 = r[k].y >> 16;
         const unsigned long long key = ((unsigned long long)dk[k] << 32) | (uint32_t)(i0 + k * 1024 + (int)threadIdx.x);
-        if (GS_BIN_UNION > 0) {
-          uint32_t ux0, ux1, uy0, uy1;
-          const uint32_t area = wave_union(r[k], ux0, ux1, uy0, uy1);
-          if (area == 0u) continue;  // (uniform)
-          if (area <= (uint32_t)GS_BIN_UNION) {
-            // one atomic per union tile reserves its lanes' slots, in lane order
-            const int lane = threadIdx.x & 63;
-            for (uint32_t y = uy0; y <= uy1; ++y)
-              for (uint32_t x = ux0; x <= ux1; ++x) {
-                const bool in = x0 <= x && x <= x1 && y0 <= y && y <= y1;
-                const unsigned long long m = ballot64(in);
-                if (m == 0ull) continue;  // (uniform)
-                const int first = __builtin_ctzll(m);
-                uint32_t base = 0u;
-                if (lane == first) base = atomicAdd(&cnt[y * fp.tiles_x + x], (uint32_t)__popcll(m));
-                base = (uint32_t)__builtin_amdgcn_readlane((int)base, first);
-                const uint32_t pos = base + lanes_below(m);
-                if (in && pos < fp.pair_cap) b.pairs[pos] = key;
-              }
-            continue;
-          }
-        }
         if (x0 > x1) continue;
         for (uint32_t y = y0; y <= y1; ++y)
           for (uint32_t x = x0; x <= x1; ++x) {
@@ -1905,10 +1840,13 @@ template <bool SCATTER>
 __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buffers& b) {
   __shared__ unsigned long long s_spl[kBktMax];
   __shared__ uint32_t s_h[kBktMax], s_base[SCATTER ? kBktMax : 1];
-  __shared__ uint32_t s_par[4];
+  __shared__ uint32_t s_par[9];
   const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
   const uint32_t tid = threadIdx.x;
   constexpr int Q = kBigSeg / 256;
+  // lazy continuation (pass 1): only the keys past the prefix whose alpha box
+  // meets the list's live pixels (the saved waves' boxes) are sorted
+  const bool filt = fp.lazy && fp.big_pass == 1;
   for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
     if (tid == 0) {
       uint32_t j, c;
@@ -1919,6 +1857,25 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
       s_par[1] = L;
       s_par[2] = c;
       s_par[3] = b.bk_off[j];
+      if (filt) {
+        int bx0 = 0x7FFFFFFF, bx1 = -1, by0 = 0x7FFFFFFF, by1 = -1;
+        for (int w = 0; w < 4; ++w)
+          if (b.cont_flag[4 * j + w]) {
+            const uint2 cb = b.cont_box[4 * j + w];
+            bx0 = min(bx0, (int)(cb.x & 0xFFFFu));
+            bx1 = max(bx1, (int)(cb.x >> 16));
+            by0 = min(by0, (int)(cb.y & 0xFFFFu));
+            by1 = max(by1, (int)(cb.y >> 16));
+          }
+        s_par[4] = (uint32_t)bx0;
+        s_par[5] = (uint32_t)bx1;
+        s_par[6] = (uint32_t)by0;
+        s_par[7] = (uint32_t)by1;
+        // keys below the bound were composited by the prefix blend -- unless
+        // the prefix was not sorted (big_len 0: more than kSortLdsCap keys
+        // below the bound), when the continuation walks the whole list
+        s_par[8] = b.big_len[j] ? b.big_thr[j] : 0u;
+      }
     }
     __syncthreads();
     const uint32_t s = s_par[0], L = s_par[1], c = s_par[2], bo = s_par[3];
@@ -1930,15 +1887,32 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
     __syncthreads();
     unsigned long long key[Q];
     uint32_t bk[Q], rk[Q];
+    bool use[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
       key[q] = i < L ? b.pairs[s + i] : 0ull;
+      use[q] = i < L;
+    }
+    if (filt) {
+      const int lx0 = (int)s_par[4], lx1 = (int)s_par[5], ly0 = (int)s_par[6], ly1 = (int)s_par[7];
+      const uint32_t thr = s_par[8];
+      uint2 bx[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)  // the record's alpha box (its 3rd float4's z, w)
+        bx[q] = (use[q] && (uint32_t)(key[q] >> 32) >= thr)
+                    ? reinterpret_cast<const uint2*>(b.rec)[(3ull * (uint32_t)key[q] + 2ull) * 2ull + 1ull]
+                    : make_uint2(kEmptyBox, kEmptyBox);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int rx0 = (int)(bx[q].x << 16) >> 16, rx1 = (int)bx[q].x >> 16;
+        const int ry0 = (int)(bx[q].y << 16) >> 16, ry1 = (int)bx[q].y >> 16;
+        use[q] = use[q] && (uint32_t)(key[q] >> 32) >= thr && rx0 <= lx1 && rx1 >= lx0 && ry0 <= ly1 && ry1 >= ly0;
+      }
     }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
-      if (i < L) {
+      if (use[q]) {
         bk[q] = big_bucket_of(s_spl, B - 1u, key[q]);
         rk[q] = atomicAdd(&s_h[bk[q]], 1u);
       }
@@ -1952,10 +1926,8 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
     __syncthreads();
     if constexpr (SCATTER) {
 #pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
-        if (i < L) b.pairs_alt[s + s_base[bk[q]] + rk[q]] = key[q];
-      }
+      for (int q = 0; q < Q; ++q)
+        if (use[q]) b.pairs_alt[s + s_base[bk[q]] + rk[q]] = key[q];
     }
   }
 }
@@ -1994,6 +1966,7 @@ __global__ __launch_bounds__(256) void gs_big_bscan_kernel(FrameParams fp, Buffe
       }
       carry += (uint32_t)__shfl(inc, 63, 64);
     }
+    if (fp.lazy && fp.big_pass == 1 && lane == 0) b.cont_len[j] = carry;  // the filtered keys
   }
 }
 
@@ -2013,7 +1986,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t bo = b.bk_off[j], B = big_buckets(L);
-    const uint32_t st = b.bk_start[k], en = k + 1u < bo + B ? b.bk_start[k + 1u] : L;
+    const uint32_t Lk = (fp.lazy && fp.big_pass == 1) ? b.cont_len[j] : L;  // (pass 1: the filtered keys)
+    const uint32_t st = b.bk_start[k], en = k + 1u < bo + B ? b.bk_start[k + 1u] : Lk;
     const uint32_t n = en - st;
     if (n == 0u) continue;  // (uniform)
     if (n > (uint32_t)kSortLdsCap) {
@@ -2277,7 +2251,10 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
   if (jb != 0xFFFFFFFFu) {
     const uint32_t np = min(b.big_len[jb], L);
     if (fp.blend_cont) {
-      k0 = np;
+      // the list now holds, from its start, the keys past the prefix whose
+      // alpha box meets the live pixels (big-list pass 1), in list order
+      L = min(b.cont_len[jb], L);
+      k0 = 0u;
       float* sv = b.cont_state + (size_t)(4 * jb + chunk) * 6 * 64 + lane;
       q.T = sv[0];
       q.c01 = f32x2{sv[64], sv[128]};
@@ -2423,7 +2400,13 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
     sv[192] = q.c23.x;
     sv[256] = q.c23.y;
     sv[320] = q.done ? 1.0f : 0.0f;
+    // the live pixels' box: the continuation's list keeps only the records
+    // whose alpha box meets it (the others cannot touch a live pixel)
+    uint32_t blo = q.done ? 0xFFFFFFFFu : ((uint32_t)px | ((uint32_t)py << 16));
+    uint32_t bhi = q.done ? 0u : ((uint32_t)px | ((uint32_t)py << 16));
+    wave_minmax_u16x2(blo, bhi);
     if (lane == 0) {
+      b.cont_box[4 * jb + chunk] = make_uint2((blo & 0xFFFFu) | (bhi << 16), (blo >> 16) | (bhi & 0xFFFF0000u));
       b.cont_flag[4 * jb + chunk] = 1u;
       b.big_flag[jb] = 1u;
     }
@@ -2517,7 +2500,7 @@ void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     // run covers the longest list the pair buffer can hold (passes after a
     // list's last one skip it)
     gs_big_prefix_kernel<<<1, 1024, 0, s>>>(fp, b);
-    gs_big_split_kernel<<<1024, 256, 0, s>>>(fp, b);
+    gs_big_split_kernel<<<2048, 256, 0, s>>>(fp, b);  // (one workgroup per list: 1024 -> 2048, sort stage -10 us at config 5)
     if (fp.lazy) {  // only the prefixes now; the rest after the blend (launch_blend_cont)
       gs_big_select_kernel<<<4096, 256, 0, s>>>(fp, b);
       gs_big_psort_kernel<<<2048, 256, 0, s>>>(fp, b);

@@ -116,6 +116,10 @@ struct Buffers {
   uint32_t* big_flag;       // [n_tiles] 1: a pixel outlived the prefix (continuation)
   uint32_t* cont_flag;      // [n_tiles * 4] per slot and blend wave: its state is saved
   float* cont_state;        // [n_tiles * 4 * 6 * 64] T, colour, done of the saved waves
+  uint2* cont_box;          // [n_tiles * 4] per slot and blend wave: the saved live pixels' box
+                            //   (x0 | x1 << 16, y0 | y1 << 16)
+  uint32_t* cont_len;       // [n_tiles] keys the continuation walks (the list's keys past the
+                            //   prefix whose alpha box meets its live pixels, sorted)
   uint32_t* footer;         // row-band group: counters[16] + reference list lengths[n_tiles]
                             //   of this frame, next to its BGR8 band in the all-gather slot
                             //   (written by the chunked scan; nullptr = none)

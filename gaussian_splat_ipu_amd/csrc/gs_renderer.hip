@@ -730,9 +730,10 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   // saved state of 4 waves (6 x 64 floats each)
   if (!r->bin_global && r->n_chunks > 0 && cfg->tile_width == 16 && cfg->tile_height == 16) {
     const size_t TT = (size_t)r->t_cap;
-    if ((e = hipMalloc(&r->d_lazy, TT * (9 * 4 + 4 * 6 * 64 * 4))) != hipSuccess)
+    const size_t lazy_bytes = TT * (9 * 4 + 4 * 6 * 64 * 4 + 4 * 8 + 4) + 8;
+    if ((e = hipMalloc(&r->d_lazy, lazy_bytes)) != hipSuccess)
       return fail(hip_fail(e, "hipMalloc(lazy big lists)"));
-    poison(r->d_lazy, TT * (9 * 4 + 4 * 6 * 64 * 4), "lazy");
+    poison(r->d_lazy, lazy_bytes, "lazy");
     uint32_t* u = (uint32_t*)r->d_lazy;
     r->buf.tile_big = u;
     r->buf.big_len = u + TT;
@@ -741,6 +742,8 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     r->buf.big_flag = u + 4 * TT;
     r->buf.cont_flag = u + 5 * TT;  // 4 per slot: [5 T, 9 T)
     r->buf.cont_state = (float*)(u + 9 * TT);
+    r->buf.cont_box = (uint2*)(((uintptr_t)(r->buf.cont_state + TT * 4 * 6 * 64) + 7) & ~(uintptr_t)7);
+    r->buf.cont_len = (uint32_t*)(r->buf.cont_box + TT * 4);
     if ((e = hipMemset(r->d_lazy, 0, TT * 9 * 4)) != hipSuccess) return fail(hip_fail(e, "hipMemset(lazy)"));
   }
 

@@ -69,7 +69,7 @@ def main():
     pick = np.unique(np.concatenate([rng.choice(T, a.tiles // 2, replace=False),
                                      rng.choice(T, a.tiles // 2, p=lens / lens.sum())]))
     acc = dict(iters=0, iters1=0, batches=0, evals=0, idle_mask=0, idle_sat=0, staged=0, binned=0,
-               dense=0, ref=0, hits=0)
+               dense=0, ref=0, hits=0, empty_batches=0)
     live_hist = np.zeros(65, np.int64)  # wave iterations by live lanes at batch start
     tail_evals = np.zeros(65, np.int64)
     for t in pick:
@@ -116,6 +116,8 @@ def main():
                         brk = h & (tT < np.float32(1e-4))
                         Tt = np.where(h & ~brk, tT, Tt)
                         done |= brk
+                    if k.max() == 0:
+                        acc["empty_batches"] += 1  # no live lane has a record of this batch
                     it = int(np.max((k + 1) // 2))
                     acc["iters"] += it
                     live_hist[nlive] += it
@@ -142,6 +144,7 @@ def main():
     for thr in (4, 8, 16, 24, 32, 48):
         print(f"  iterations with <= {thr:2d} live lanes at batch start: {cum[thr] / max(it, 1):.3f} "
               f"(their lane evals: {cev[thr] / max(e, 1):.3f} of all)")
+    print(f"batches in which no live lane has a record: {acc['empty_batches']} of {b} ({acc['empty_batches'] / max(b, 1):.3f})")
     print(f"hits (power in range, alpha >= 1/255) among lane evals: {acc['hits'] / max(e, 1):.3f}")
     print(f"whole frame (scaled): iters {it * scale:.0f} batches {b * scale:.0f} evals {e * scale:.0f}")
 
