@@ -362,6 +362,10 @@ def main():
         kern["blend"]["pairs_binned"] = int(P_b)
     if "blend_cont" in kern:
         kern["blend_cont"]["records_staged"] = int(rec_cont)
+        kern["blend_cont"]["lists"] = int(st_view["cont_lists"])
+        kern["blend_cont"]["keys_sorted"] = int(st_view["cont_keys"])
+        kern["blend_cont"]["longest_list"] = int(st_view["cont_max"])
+        kern["blend_cont"]["prefix_overflows"] = int(st_view["prefix_overflows"])
         kern["blend_cont"]["note"] = ("full sample sort of the big lists the blend flagged + the continued blend; "
                                       "alg_bytes counts the continued records only")
     stage = {k: v for k, v in kern.items() if k != "gather"}

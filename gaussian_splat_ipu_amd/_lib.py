@@ -115,6 +115,11 @@ class FrameStats(C.Structure):
         ("reserved0", C.c_uint32),
         ("blend_records", C.c_uint64),
         ("blend_cont_records", C.c_uint64),
+        ("cont_keys", C.c_uint64),
+        ("cont_lists", C.c_uint32),
+        ("cont_max", C.c_uint32),
+        ("prefix_overflows", C.c_uint32),
+        ("reserved1", C.c_uint32),
     ]
 
     def as_dict(self):

@@ -857,6 +857,10 @@ int get_stats(Group* g, gs_frame_stats* st) {
   // the profiled band renderer's own counts (this rank's band)
   st->blend_records = g->mem[0].slot[0]->stats.blend_records;
   st->blend_cont_records = g->mem[0].slot[0]->stats.blend_cont_records;
+  st->cont_keys = g->mem[0].slot[0]->stats.cont_keys;
+  st->cont_lists = g->mem[0].slot[0]->stats.cont_lists;
+  st->cont_max = g->mem[0].slot[0]->stats.cont_max;
+  st->prefix_overflows = g->mem[0].slot[0]->stats.prefix_overflows;
   uint64_t cap = ~0ull;
   for (Member& m : g->mem)
     for (gs_renderer* c : m.slot) cap = std::min<uint64_t>(cap, c->pair_cap);

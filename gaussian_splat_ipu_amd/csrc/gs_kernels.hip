@@ -2171,9 +2171,9 @@ __device__ __forceinline__ void blend_count_store(const FrameParams& fp, const B
 }
 
 template <int BQW, bool HWEXP>
-__device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers& b) {
+__device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers& b, int blk) {
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wid = blockIdx.x * GS_BLEND_WPG + wave;
+  const int wid = blk * GS_BLEND_WPG + wave;
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
   if (slot >= fp.n_tiles) return;
@@ -2420,14 +2420,18 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
 // HWEXP: GS_FLAG_FAST_EXP (its own kernel: the default path's code is unchanged)
 template <int BQW, bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
-  blend_body<BQW, HWEXP>(fp, b);
+  blend_body<BQW, HWEXP>(fp, b, blockIdx.x);
 }
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
-// the prefix blend)
+// the prefix blend).  A grid-stride loop over the waves of the big lists
+// only: a grid of every tile's waves, nearly all of which exit at once, cost
+// ~70 us at config 5 (32 400 short-lived workgroups, each waiting on its
+// counters load, 4 resident per CU).
 template <bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_cont_kernel(FrameParams fp, Buffers b) {
-  blend_body<4, HWEXP>(fp, b);
+  const int nblk = (int)((b.counters[0] * (uint32_t)fp.chunks_per_tile + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) blend_body<4, HWEXP>(fp, b, blk);
 }
 
 
@@ -2537,7 +2541,7 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
   if (waves == 0 || !fp.lazy) return;
-  const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
+  const unsigned grid = (unsigned)std::min<long>((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG, 2048);
   const unsigned block = 64 * GS_BLEND_WPG;
   // the big lists whose blend outlived the prefix: sorted in full, then
   // their saved waves continue (nothing to do when none was flagged)

@@ -433,7 +433,8 @@ int finish_frame(gs_renderer* r) {
   r->stats.max_list = mx;
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
-  r->stats.blend_records = r->stats.blend_cont_records = 0;
+  r->stats.blend_records = r->stats.blend_cont_records = r->stats.cont_keys = 0;
+  r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = 0;
   if (r->last_counted && r->bcount_words) {
     // profiled frame: the list records the blend read.  The waves of a tile
     // each stage a prefix of the same list (the tile's records come from HBM
@@ -450,7 +451,22 @@ int finish_frame(gs_renderer* r) {
         m1 = std::max(m1, bc[nw + k]);
       }
       r->stats.blend_records += m0;
-      if (r->last_fp.lazy) r->stats.blend_cont_records += m1;  // (the continuation ran)
+      // (the continuation ran the waves of the c[0] big lists only)
+      if (r->last_fp.lazy && t < (size_t)c[0] * cpt) r->stats.blend_cont_records += m1;
+    }
+    if (r->last_fp.lazy && c[0] > 0) {
+      // the continuation's lists and their filtered key counts
+      std::vector<uint32_t> fl(c[0]), cl(c[0]), bl(c[0]);
+      GS_HIP(hipMemcpy(fl.data(), r->buf.big_flag, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
+      GS_HIP(hipMemcpy(cl.data(), r->buf.cont_len, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
+      GS_HIP(hipMemcpy(bl.data(), r->buf.big_len, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
+      for (uint32_t j = 0; j < c[0]; ++j)
+        if (fl[j]) {
+          r->stats.prefix_overflows += bl[j] == 0u ? 1u : 0u;
+          r->stats.cont_lists += 1;
+          r->stats.cont_keys += cl[j];
+          r->stats.cont_max = std::max(r->stats.cont_max, cl[j]);
+        }
     }
   }
   // the scan of EVERY frame ORs its overflow into the sticky word (several

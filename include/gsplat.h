@@ -177,6 +177,15 @@ typedef struct gs_frame_stats {
                                   saturated; lazy big lists: the sorted
                                   prefixes only)                             */
   uint64_t blend_cont_records; /* ... and the records the continuation staged */
+  uint64_t cont_keys;     /* ABI 8, profiled lazy frames: keys the continuation
+                             sorted (past the prefixes, alpha box meeting the
+                             saved waves' live pixels), summed over its lists */
+  uint32_t cont_lists;    /* big lists the continuation ran on             */
+  uint32_t cont_max;      /* the longest of their continuation key lists   */
+  uint32_t prefix_overflows; /* big lists whose keys below the depth bound
+                             outnumbered one workgroup's sort (the whole
+                             list went to the continuation)              */
+  uint32_t reserved1;
 } gs_frame_stats;
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */
