@@ -1705,7 +1705,7 @@ __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffe
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t B = big_buckets(L), bo = b.bk_off[j];
-    const uint32_t S = bound ? min((uint32_t)kSortLdsCap, L) : min((uint32_t)kSortLdsCap, 16u * B);  // sample size
+    const uint32_t S = min((uint32_t)kSortLdsCap, min(L, (bound ? 32u : 16u) * B));  // sample size
     for (uint32_t k = tid; k < S; k += 256u) {
       const uint32_t p = (uint32_t)(((2ull * k + 1ull) * L) / (2ull * S));
       keys[k] = b.pairs[s + p];
