@@ -183,6 +183,7 @@ _SIGS = {
     "gs_set_projection": (C.c_int, [_P, _FP]),
     "gs_set_focal": (C.c_int, [_P, C.c_float, C.c_float]),
     "gs_set_sh": (C.c_int, [_P, _FP, _FP, C.c_size_t, C.c_int]),
+    "gs_set_band_rows": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32]),
     "gs_set_stream": (C.c_int, [_P, _P]),
     "gs_get_stream": (C.c_int, [_P, C.POINTER(_P)]),
     "gs_render": (C.c_int, [_P]),

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -22,6 +23,13 @@
 #include "host/gs_host.hpp"
 
 using gsh::set_error;
+
+namespace {
+// scene allocation: the 64-B records (SoA), the permutation both ways, then
+// two float4 of block bounds per 256 Gaussians (16-B aligned)
+size_t block_box_offset(size_t nn) { return (nn * (64 + 8) + 15) / 16 * 16; }
+size_t scene_bytes(size_t nn) { return block_box_offset(nn) + (nn + 255) / 256 * 32; }
+}  // namespace
 
 namespace gsr {
 
@@ -178,6 +186,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
+  fp.block_cull = (fp.band_cull && r->buf.block_box && r->scale_div > 0.0f) ? 1 : 0;
   {
     double w2 = 0.0;  // squared Frobenius norm of the upper 3x3 of the mvp, rounded up
     for (int c = 0; c < 3; ++c)
@@ -646,15 +655,29 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     r->owns_scene = false;
   } else {
     r->perm = morton_order(g, n, (cfg->flags & GS_FLAG_INPUT_ORDER) != 0);
-    if ((e = hipMalloc(&r->d_scene, nn * (64 + 8))) != hipSuccess)
+    if ((e = hipMalloc(&r->d_scene, scene_bytes(nn))) != hipSuccess)
       return fail(hip_fail(e, "hipMalloc(scene)"));
     {
       // staged in pinned host memory (one DMA at full PCIe rate)
       float* soa = nullptr;
-      if ((e = hipHostMalloc((void**)&soa, nn * (64 + 8), hipHostMallocDefault)) != hipSuccess)
+      if ((e = hipHostMalloc((void**)&soa, scene_bytes(nn), hipHostMallocDefault)) != hipSuccess)
         return fail(hip_fail(e, "hipHostMalloc(scene staging)"));
-      std::memset(soa, 0, nn * (64 + 8));
+      std::memset(soa, 0, scene_bytes(nn));
       uint32_t* pi = (uint32_t*)(soa + nn * 16);
+      // the band cull's block bounds (gs_kernels.hip, block_band_culled): per
+      // 256 Gaussians of device order, the box of the live means and the
+      // largest log-scale; w = 1 cullable, 2 no live Gaussian, 0 never culled
+      float* bbox = soa + block_box_offset(nn) / 4;
+      const size_t nblk = (nn + 255) / 256;
+      for (size_t k = 0; k < nblk; ++k) {
+        float* lo = bbox + 8 * k;
+        for (int c = 0; c < 3; ++c) {
+          lo[c] = std::numeric_limits<float>::infinity();
+          lo[4 + c] = -std::numeric_limits<float>::infinity();
+        }
+        lo[3] = -std::numeric_limits<float>::infinity();
+        lo[7] = 2.0f;
+      }
       for (size_t i = 0; i < n; ++i) {
         const uint32_t o = r->perm[i];
         const float* s = reinterpret_cast<const float*>(&g[o]);
@@ -666,8 +689,23 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         }
         pi[i] = o;
         pi[nn + o] = (uint32_t)i;
+        if (!(s[15] <= 0.0f)) {  // live (codelets.cpp:456), as project_one tests it
+          float* lo = bbox + 8 * (i >> 8);
+          const float sm = std::max(std::max(s[12], s[13]), s[14]);
+          const bool fin = std::isfinite(s[0]) && std::isfinite(s[1]) && std::isfinite(s[2]) && std::isfinite(sm);
+          if (!fin || s[3] != 1.0f) {
+            lo[7] = 0.0f;  // non-finite, or a mean with w != 1: the block is never culled
+          } else if (lo[7] != 0.0f) {
+            lo[7] = 1.0f;
+            for (int c = 0; c < 3; ++c) {
+              lo[c] = std::min(lo[c], s[c]);
+              lo[4 + c] = std::max(lo[4 + c], s[c]);
+            }
+            lo[3] = std::max(lo[3], sm);
+          }
+        }
       }
-      e = hipMemcpy(r->d_scene, soa, nn * (64 + 8), hipMemcpyHostToDevice);
+      e = hipMemcpy(r->d_scene, soa, scene_bytes(nn), hipMemcpyHostToDevice);
       (void)hipHostFree(soa);
       if (e != hipSuccess) return fail(hip_fail(e, "hipMemcpy(scene)"));
     }
@@ -678,6 +716,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.rot = sc + 2 * nn;
   r->buf.scale_gid = sc + 3 * nn;
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
+  r->buf.block_box = (const float4*)((const char*)r->d_scene + block_box_offset(nn));
   r->buf.inv_perm = r->buf.perm + nn;
 
   // per Gaussian: 48-B record (what the blend reads), its 8-B readback tail,
@@ -1124,6 +1163,28 @@ int gs_set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, 
     return GS_EINVAL;
   }
   return gsr::set_sh(r, f_dc, f_rest, n, degree);
+}
+
+int gs_set_band_rows(gs_renderer* r, uint32_t row_begin, uint32_t row_end, uint32_t pad_rows) {
+  if (!r) return GS_EINVAL;
+  if (r->grp || r->lattice) {
+    set_error("gs_set_band_rows: a single-GPU frame renderer only (a group moves its own bands)");
+    return GS_EINVAL;
+  }
+  if (r->band_stride != 1) {
+    set_error("gs_set_band_rows: interleaved bands are fixed at creation");
+    return GS_EINVAL;
+  }
+  if (row_end > (uint32_t)r->tiles_y || row_begin >= row_end) {
+    set_error("gs_set_band_rows: rows outside the tile grid");
+    return GS_EINVAL;
+  }
+  if (r->frame_pending) {  // the frame in flight keeps the rows it was enqueued with
+    const int rc = gsr::finish_frame(r);
+    if (rc != GS_OK) return rc;
+  }
+  const int pad = std::max<int>((int)(row_end - row_begin), (int)pad_rows);
+  return gsr::set_band_rows(r, (int)row_begin, (int)row_end, pad);
 }
 
 int gs_set_stream(gs_renderer* r, void* hip_stream) {

@@ -211,6 +211,14 @@ class GpuSplatter:
         check(lib().gs_set_sh(self._h, fptr(dc), None if rest is None else fptr(rest), self.n, int(degree)),
               "gs_set_sh")
 
+    def set_band_rows(self, row_begin: int, row_end: int, pad_rows: int = 0) -> None:
+        """Move this renderer's contiguous band to tile rows [row_begin, row_end)
+        (gs_set_band_rows; the renderer must have been created with room for
+        them, e.g. band_rows=(0, tiles_y))."""
+        check(lib().gs_set_band_rows(self._h, int(row_begin), int(row_end), int(pad_rows)), "gs_set_band_rows")
+        st = self.stats()
+        self.n_tiles, self.band_y0, self.band_rows = st["n_tiles"], st["band_y0"], st["band_rows"]
+
     def set_stream(self, stream_ptr: int | None) -> None:
         check(lib().gs_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
 

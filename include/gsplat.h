@@ -309,6 +309,15 @@ int gs_set_focal(gs_renderer* r, float fov_rad, float scale_divisor);
  * the reference (it never evaluates SH); the oracle restates the same fp32
  * operations (or_sh_colours). */
 int gs_set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree);
+/* ABI 8: move a single-GPU renderer's contiguous band to tile rows
+ * [row_begin, row_end), padded to pad_rows tile rows in the BGR8 band (0 =
+ * no padding past the band).  The renderer must have been created with at
+ * least that many rows (band_row_begin/end or band_pad_rows) -- e.g. the whole
+ * frame, then moved per frame to a work-balanced split, as the row-band group
+ * does for its members.  A frame still in flight is completed first (its
+ * results stay readable).  GS_EINVAL for a group handle or rows outside the
+ * renderer's capacity. */
+int gs_set_band_rows(gs_renderer* r, uint32_t row_begin, uint32_t row_end, uint32_t pad_rows);
 /* HIP stream (hipStream_t as void*) the frame is enqueued on; NULL = the
  * renderer's own stream. */
 int gs_set_stream(gs_renderer* r, void* hip_stream);

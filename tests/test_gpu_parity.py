@@ -547,3 +547,37 @@ def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
         s.execute()  # big lists through the big-list sample sort
         _assert_parity(s, f, a)
     assert ref["stats"]["n_pairs"] > 0
+
+
+def test_set_band_rows_moves_one_renderer(pc12):
+    """gs_set_band_rows: one renderer created for the whole frame is moved over
+    a balanced 3-band split (async frames in flight between the moves, as a
+    group member is); each band equals the full frame's rows bit for bit."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd import dist as gdist
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    g, bb = pc12
+    W, H, TW, TH = 1920, 1080, 16, 16
+    view, proj = camera.headless(bb, W, H)
+    full, f = _frame_pair(g, view, proj, W, H, TW, TH, 1.0)
+    fb = TiledFramebuffer(W, H, TW, TH)
+    rgba, bgr = full.get_rgba(), full.get_frame_buffer()
+    hist = full.get_histogram().reshape(fb.tiles_down, fb.tiles_across)
+    bands = gdist.balanced_bands(gdist.row_work(hist, fb), 3)
+    with GpuSplatter(g, fb, device=0, band_rows=(0, fb.tiles_down), band_cull=True) as s:
+        s.set_view_wire(view)
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        s.execute()
+        for t0, t1 in bands + bands[::-1]:
+            s.execute_async()  # a frame of the previous rows still in flight
+            s.set_band_rows(t0, t1)
+            s.execute()
+            y0, y1 = t0 * TH, min(H, t1 * TH)
+            assert_same_bits(s.get_rgba(), rgba[y0:y1], f"moved band {t0}-{t1} rgba")
+            np.testing.assert_array_equal(s.get_frame_buffer(), bgr[y0:y1])
+            np.testing.assert_array_equal(s.get_histogram(), hist[t0:t1].reshape(-1))
+        with pytest.raises(Exception):
+            s.set_band_rows(0, fb.tiles_down + 1)

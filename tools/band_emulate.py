@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--bin-global", action="store_true", help="the bands bin with global atomics")
     ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
     ap.add_argument("--config5", action="store_true", help="bench.py --config5's scene, 4K, orbit views")
+    ap.add_argument("--rebalance", action="store_true",
+                    help="orbit views: move each band renderer (gs_set_band_rows) to the split the group "
+                         "would use -- re-cut every 8 frames from the histogram of 4 frames earlier")
     a = ap.parse_args()
     import torch
 
@@ -55,6 +58,7 @@ def main():
     fb = TiledFramebuffer(W, H, TW, TW)
     base = None
     hist = None
+    view_hist = None
     if a.balanced:
         from gaussian_splat_ipu_amd import dist as gdist
 
@@ -64,17 +68,32 @@ def main():
         cal.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
         cal.execute()
         hist = cal.get_histogram()
+        if a.rebalance and views is not None:
+            view_hist = []
+            for v in views:
+                cal.set_view_wire(v)
+                cal.execute()
+                view_hist.append(cal.get_histogram())
         cal.close()
     for N in [int(v) for v in a.bands.split(",")]:
-        per_band, stages = [], []
+        per_band, stages, host = [], [], []
         bands = gdist.balanced_bands(gdist.row_work(hist, fb), N) if hist is not None and N > 1 else None
         pad = max(t1 - t0 for t0, t1 in bands) if bands else 0
+        # the group's policy: frame k renders with the split cut at frame
+        # 8 (k // 8) from the footers of 4 frames before it
+        view_bands = None
+        if view_hist is not None and N > 1:
+            view_bands = [gdist.balanced_bands(gdist.row_work(h, fb), N) for h in view_hist]
+            pad = fb.tiles_down
         for r in range(N):
             if a.only_band >= 0 and r != a.only_band:
                 continue
             R, S = [], []
             for f in range(a.inflight):
-                if bands is not None:
+                if view_bands is not None:  # room for any band; moved per frame
+                    s = GpuSplatter(g, fb, device=0, band_rows=(0, fb.tiles_down), profile=(f == 0),
+                                    band_cull=not a.no_cull, write_rgba=False, bin_global=a.bin_global)
+                elif bands is not None:
                     s = GpuSplatter(g, fb, device=0, band_rows=bands[r], band_pad_rows=pad, profile=(f == 0),
                                     band_cull=not a.no_cull, write_rgba=False,
                                     bin_global=a.bin_global)
@@ -97,6 +116,9 @@ def main():
             def frame(k):
                 if views is not None:
                     R[k % len(R)].set_view_wire(views[k % 120])
+                if view_bands is not None:
+                    t0, t1 = view_bands[(8 * (k // 8) - 4) % 120][r]
+                    R[k % len(R)].set_band_rows(t0, t1)
                 R[k % len(R)].execute_async()
 
             for k in range(a.warmup):
@@ -106,8 +128,10 @@ def main():
             t0 = time.perf_counter()
             for k in range(a.steps):
                 frame(k)
+            th = (time.perf_counter() - t0) / a.steps  # host enqueue (returns before the GPU is done)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / a.steps
+            host.append(th * 1e6)
             for s in R:
                 s.sync()
             per_band.append(dt * 1e6)
@@ -117,6 +141,8 @@ def main():
             for k in range(12):
                 if views is not None:
                     R[0].set_view_wire(views[k % 120])
+                if view_bands is not None:
+                    R[0].set_band_rows(*view_bands[(8 * (k // 8) - 4) % 120][r])
                 R[0].execute_async()
             R[0].sync()
             stages.append({k: round(v[0] * 1e3, 1) for k, v in R[0].kernel_times().items()})
@@ -130,11 +156,13 @@ def main():
         i = per_band.index(worst)
         mean = sum(per_band) / len(per_band)
         print(json.dumps({"workload": "config5 8M/4K orbit" if a.config5 else f"config4 {a.n}/1080p",
-                          "bands": N, "inflight": a.inflight, "split": bands,
+                          "bands": N, "inflight": a.inflight,
+                          "split": "rebalanced per 8 frames (4-frame-old histogram)" if view_bands else bands,
                           "us_per_frame_by_band": [round(v, 1) for v in per_band],
                           "slowest_us": round(worst, 1), "fastest_us": round(min(per_band), 1),
                           "skew_slowest_over_mean": round(worst / mean, 3),
                           "speedup": round(base / worst, 2),
+                          "host_enqueue_us_by_band": [round(v, 1) for v in host],
                           "slowest_band_stage_us": stages[i]}), flush=True)
 
 
