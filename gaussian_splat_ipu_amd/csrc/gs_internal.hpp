@@ -81,6 +81,8 @@ struct gs_renderer {
   size_t lat_slots = 0;          // vertsIn slots over all tiles
   uint64_t lat_frames = 0;       // frames stepped (the exchange parity)
   int bin_global = 0, chunk_size = 0, n_chunks = 0;
+  size_t chunk_entries = 0;     // chunk table size (chunks x tiles)
+  bool chunk_adaptive = false;  // bands: more, smaller chunks (make_params)
   bool pair_cull = false;       // chunked binning into the alpha-box tiles only
   size_t zero_bytes = 0;
   size_t bgr_bytes = 0;

@@ -214,52 +214,6 @@ __device__ __forceinline__ bool band_culled_fast(const FrameParams& fp, float4 m
   return band_culled<P2>(fp, vy, m3_mul(W, J), sg, 1e-5f * __builtin_fabsf(vy) + 0.05f);
 }
 
-// The band cull per 256 Gaussians, before any of them is read: true when no
-// Gaussian of the block can have a tile row in the band.  The block's bounds
-// (gs_renderer.hip, at scene upload): the box of its live means (all with
-// w = 1) and the largest log-scale.  Over the box, cw > 0 at the 8 corners
-// keeps cw > 0 everywhere, and vy = H (cy / cw / 2 + 1/2) -- linear-fractional
-// in the mean -- takes its extremes at corners; tz (linear) keeps one sign, so
-// |tz| >= the corners' smallest.  band_culled's radius bound needs
-// ||T||_F^2 <= ||W||_F^2 ||J||_F^2 with ||J||_F^2 <= (fx^2 + fy^2)(1 + lim^2)
-// / tz^2 (the clamped tx/tz, ty/tz are at most lim), and the block's largest
-// scale.  The bound is inflated again (1 % on T, 1 px + 1e-4 |vy| on the
-// rows), so the block test never culls a Gaussian band_culled would keep.
-template <bool P2>
-__device__ __forceinline__ bool block_band_culled(const FrameParams& fp, float4 lo, float4 hi) {
-  if (hi.w != 1.0f) return hi.w == 2.0f;  // 2: no live Gaussian; 0: unbounded
-  const float* m = fp.mvp;
-  float vy0 = __builtin_huge_valf(), vy1 = -__builtin_huge_valf();
-  float tz0 = __builtin_huge_valf(), tz1 = -__builtin_huge_valf();
-  bool front = true;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const float x = (c & 1) ? hi.x : lo.x, y = (c & 2) ? hi.y : lo.y, z = (c & 4) ? hi.z : lo.z;
-    const float cy = mv_row(m, 1, x, y, z, 1.0f), cw = mv_row(m, 3, x, y, z, 1.0f);
-    const float tz = mv_row(m, 2, x, y, z, 1.0f);
-    front = front && cw > 0.0f;
-    const float vy = (cy * (0.5f / cw) + 0.5f) * fp.H;
-    vy0 = fminf(vy0, vy);
-    vy1 = fmaxf(vy1, vy);
-    tz0 = fminf(tz0, tz);
-    tz1 = fmaxf(tz1, tz);
-  }
-  if (!front || !(tz1 < 0.0f || tz0 > 0.0f)) return false;
-  const float atz = tz1 < 0.0f ? -tz1 : tz0;
-  const float lim = 1.3f * fp.tanfov;
-  const float j2 = (fp.focal_x * fp.focal_x + fp.focal_y * fp.focal_y) * (1.0f + lim * lim) / (atz * atz);
-  const float t2 = fp.wnorm2 * j2 * 1.01f;
-  const float lc = __expf(2.0f * (lo.w / fp.scale_div)) * 1.01f;
-  const float r = 3.0f * __builtin_sqrtf(1.05f * (2.0f * lc * t2) + 1.0f) + 3.0f;
-  const float pad = 1e-4f * fmaxf(__builtin_fabsf(vy0), __builtin_fabsf(vy1)) + 1.0f;
-  if (!(r < 1e30f) || !(__builtin_fabsf(vy0) < 1e30f) || !(__builtin_fabsf(vy1) < 1e30f)) return false;
-  const float fy0 = __builtin_floorf(div_p2<P2>(__builtin_floorf(vy0 - r - pad), fp.th, fp.inv_th));
-  const float fy1 = __builtin_floorf(div_p2<P2>(__builtin_ceilf(vy1 + r + pad), fp.th, fp.inv_th));
-  int yb0, yb1;
-  band_rows_of<P2>(fp, fy0, fy1, yb0, yb1);
-  return yb0 > yb1;
-}
-
 // gs_set_sh (opt-in, not in the reference: its loader reads
 // f_dc only, file_io.cpp:66-68): the view-dependent colour of the 3DGS
 // convention (degree <= 3) for the direction from the camera to the mean.
@@ -478,15 +432,11 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool rendered = false;
   if (fp.band_cull) {
-    // the block's bounds first (no Gaussian read when they miss the band),
-    // then the cheap per-Gaussian test; a block of 256 Gaussians culled
+    // the cheap band test first; a block of 256 Gaussians that it culls
     // entirely writes only its V (0): count and emit skip such blocks
-    // without reading their rectangles, so nothing else needs writing
-    if (fp.block_cull &&
-        block_band_culled<P2>(fp, b.block_box[2 * blockIdx.x], b.block_box[2 * blockIdx.x + 1])) {
-      if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = 0u;
-      return;
-    }
+    // without reading their rectangles, so nothing else needs writing.
+    // (A test of per-block bounds before any Gaussian is read was slower:
+    // DESIGN.md §8, "block bounds")
     bool culled = false;
     if (i < fp.n) {
       // both loads in one memory round trip (the test needs the mean unless
@@ -785,10 +735,15 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
     sum += v[k];
     hsum += fp.pair_cull ? e >> 16 : e;
   }
-  for (int cc = c0 + 16; cc < c1; ++cc) {  // (n_chunks > 256 only)
-    const uint32_t e = t < T ? b.chunk_off[(size_t)cc * T + t] : 0u;
-    sum += e & lo_mask;
-    hsum += fp.pair_cull ? e >> 16 : e;
+  for (int cc0 = c0 + 16; cc0 < c1; cc0 += 8) {  // (n_chunks > 256 only) 8 loads in flight
+    uint32_t e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = (t < T && cc0 + k < c1) ? b.chunk_off[(size_t)(cc0 + k) * T + t] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sum += e[k] & lo_mask;
+      hsum += fp.pair_cull ? e[k] >> 16 : e[k];
+    }
   }
   wsum[wave][lane] = sum;
   whsum[wave][lane] = hsum;
@@ -801,11 +756,15 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
       if (c0 + k < c1) b.chunk_off[(size_t)(c0 + k) * T + t] = run;
       run += v[k];
     }
-    for (int cc = c0 + 16; cc < c1; ++cc) {
-      uint32_t* const p = b.chunk_off + (size_t)cc * T + t;
-      const uint32_t e = *p & lo_mask;
-      *p = run;
-      run += e;
+    for (int cc0 = c0 + 16; cc0 < c1; cc0 += 8) {
+      uint32_t e[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = cc0 + k < c1 ? b.chunk_off[(size_t)(cc0 + k) * T + t] & lo_mask : 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (cc0 + k < c1) b.chunk_off[(size_t)(cc0 + k) * T + t] = run;
+        run += e[k];
+      }
     }
     if (wave == 15) b.tile_count[t] = run;
   }

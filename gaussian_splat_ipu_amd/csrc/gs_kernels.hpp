@@ -26,7 +26,6 @@ struct FrameParams {
   int tiles_y;        // tile rows of the whole frame
   int band_rows;      // pixel rows of this band's output
   int band_cull;      // skip Gaussians whose extent bound misses the band (GS_FLAG_BAND_CULL)
-  int block_cull;     // band_cull with the per-block bounds (scale_div > 0)
   float wnorm2;       // >= squared Frobenius norm of the mvp's upper 3x3 (band cull bound)
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
@@ -97,7 +96,6 @@ struct Buffers {
                             //   small | medium << 8 | big << 16 counts, max length;
                             //   then the reference list-length sum (lo, hi), 0, 0
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
-  const float4* block_box;  // [2 ceil(n / 256)] band-cull block bounds (lo xyz + max log-scale, hi xyz + state)
   uint32_t* host_counters;  // mapped pinned mirror of counters[16] + tile_count[n_tiles],
                             //   written by the chunked scan (no D2H copy per frame)
   uint32_t* host_sticky;    // mapped pinned word: set by the scan of any frame that

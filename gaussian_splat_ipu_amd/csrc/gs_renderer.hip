@@ -12,7 +12,6 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <limits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -25,10 +24,8 @@
 using gsh::set_error;
 
 namespace {
-// scene allocation: the 64-B records (SoA), the permutation both ways, then
-// two float4 of block bounds per 256 Gaussians (16-B aligned)
-size_t block_box_offset(size_t nn) { return (nn * (64 + 8) + 15) / 16 * 16; }
-size_t scene_bytes(size_t nn) { return block_box_offset(nn) + (nn + 255) / 256 * 32; }
+// scene allocation: the 64-B records (SoA) and the permutation both ways
+size_t scene_bytes(size_t nn) { return nn * (64 + 8); }
 }  // namespace
 
 namespace gsr {
@@ -153,6 +150,11 @@ void release(gs_renderer* r) {
   if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
 }
 
+// bands: the chunk count grows with the band's share of the tiles up to this
+// (gs_colscan_kernel walks a tile's chunk rows: past 256 of them it reads
+// them twice, in batches of 8)
+constexpr size_t kMaxBandChunks = 1024;
+
 gsk::FrameParams make_params(const gs_renderer* r) {
   gsk::FrameParams fp{};
   // mvp = projmatrix * viewmatrix, both from the row-major wire format
@@ -186,7 +188,6 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
-  fp.block_cull = (fp.band_cull && r->buf.block_box && r->scale_div > 0.0f) ? 1 : 0;
   {
     double w2 = 0.0;  // squared Frobenius norm of the upper 3x3 of the mvp, rounded up
     for (int c = 0; c < 3; ++c)
@@ -209,6 +210,16 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.bin_global = r->bin_global;
   fp.chunk_size = r->chunk_size;
   fp.n_chunks = r->n_chunks;
+  if (r->chunk_adaptive && r->n_chunks > 0 && r->n_tiles > 0 &&
+      (size_t)r->n_tiles * (size_t)r->n_chunks < r->chunk_entries) {
+    // a band: as many chunks as the table holds for its tiles, of >= 4096
+    // Gaussians (smaller ones made the 1M-Gaussian bands slower: 8 bands,
+    // 40.5 -> 48-51 us per frame; at 8 M, 8 bands, 287 -> 253 us)
+    const size_t nc = std::min<size_t>(r->chunk_entries / (size_t)r->n_tiles, kMaxBandChunks);
+    const size_t cs = std::min<size_t>(65535, std::max<size_t>(4096, (r->n + nc - 1) / nc));
+    fp.chunk_size = (int)cs;
+    fp.n_chunks = (int)((r->n + cs - 1) / cs);
+  }
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
   // the big-list launch only when the last frame the device completed had
@@ -664,20 +675,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         return fail(hip_fail(e, "hipHostMalloc(scene staging)"));
       std::memset(soa, 0, scene_bytes(nn));
       uint32_t* pi = (uint32_t*)(soa + nn * 16);
-      // the band cull's block bounds (gs_kernels.hip, block_band_culled): per
-      // 256 Gaussians of device order, the box of the live means and the
-      // largest log-scale; w = 1 cullable, 2 no live Gaussian, 0 never culled
-      float* bbox = soa + block_box_offset(nn) / 4;
-      const size_t nblk = (nn + 255) / 256;
-      for (size_t k = 0; k < nblk; ++k) {
-        float* lo = bbox + 8 * k;
-        for (int c = 0; c < 3; ++c) {
-          lo[c] = std::numeric_limits<float>::infinity();
-          lo[4 + c] = -std::numeric_limits<float>::infinity();
-        }
-        lo[3] = -std::numeric_limits<float>::infinity();
-        lo[7] = 2.0f;
-      }
       for (size_t i = 0; i < n; ++i) {
         const uint32_t o = r->perm[i];
         const float* s = reinterpret_cast<const float*>(&g[o]);
@@ -689,21 +686,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         }
         pi[i] = o;
         pi[nn + o] = (uint32_t)i;
-        if (!(s[15] <= 0.0f)) {  // live (codelets.cpp:456), as project_one tests it
-          float* lo = bbox + 8 * (i >> 8);
-          const float sm = std::max(std::max(s[12], s[13]), s[14]);
-          const bool fin = std::isfinite(s[0]) && std::isfinite(s[1]) && std::isfinite(s[2]) && std::isfinite(sm);
-          if (!fin || s[3] != 1.0f) {
-            lo[7] = 0.0f;  // non-finite, or a mean with w != 1: the block is never culled
-          } else if (lo[7] != 0.0f) {
-            lo[7] = 1.0f;
-            for (int c = 0; c < 3; ++c) {
-              lo[c] = std::min(lo[c], s[c]);
-              lo[4 + c] = std::max(lo[4 + c], s[c]);
-            }
-            lo[3] = std::max(lo[3], sm);
-          }
-        }
       }
       e = hipMemcpy(r->d_scene, soa, scene_bytes(nn), hipMemcpyHostToDevice);
       (void)hipHostFree(soa);
@@ -716,7 +698,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.rot = sc + 2 * nn;
   r->buf.scale_gid = sc + 3 * nn;
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
-  r->buf.block_box = (const float4*)((const char*)r->d_scene + block_box_offset(nn));
   r->buf.inv_perm = r->buf.perm + nn;
 
   // per Gaussian: 48-B record (what the blend reads), its 8-B readback tail,
@@ -763,7 +744,8 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     // second read of the extra rows.  Test hooks: GSPLAT_BIN_CHUNK_SIZE sets
     // the chunk size (many chunks at a small N); GSPLAT_BIN_MAX_CHUNKS sends
     // scenes of more chunks to the global-atomic path.
-    if (const char* ev = std::getenv("GSPLAT_BIN_CHUNK_SIZE")) cs = (size_t)std::max(64, std::min(65535, std::atoi(ev)));
+    const char* fixed_cs = std::getenv("GSPLAT_BIN_CHUNK_SIZE");
+    if (fixed_cs) cs = (size_t)std::max(64, std::min(65535, std::atoi(fixed_cs)));
     size_t max_chunks = SIZE_MAX;
     if (const char* ev = std::getenv("GSPLAT_BIN_MAX_CHUNKS")) max_chunks = (size_t)std::max(1, std::atoi(ev));
     if ((n + cs - 1) / cs > max_chunks) {
@@ -772,9 +754,15 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       if ((e = gsk::init_kernel_attributes()) != hipSuccess) return fail(hip_fail(e, "hipFuncSetAttribute"));
       r->chunk_size = (int)cs;
       r->n_chunks = (int)((n + cs - 1) / cs);
-      if ((e = hipMalloc(&r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4)) != hipSuccess)
+      // the chunk table holds the whole frame's chunks x tiles: a band (fewer
+      // tiles) cuts the scene into proportionally more, smaller chunks
+      // (make_params), so the densest chunk -- the binning's critical path --
+      // shrinks with the band instead of staying a whole-frame chunk
+      r->chunk_entries = (size_t)r->n_chunks * (size_t)std::max(r->n_tiles, r->tiles_x * r->tiles_y);
+      r->chunk_adaptive = fixed_cs == nullptr && max_chunks == SIZE_MAX;
+      if ((e = hipMalloc(&r->d_chunk, r->chunk_entries * 4)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
-      poison(r->d_chunk, (size_t)r->n_chunks * r->n_tiles * 4, "chunk");
+      poison(r->d_chunk, r->chunk_entries * 4, "chunk");
       r->buf.chunk_off = (uint32_t*)r->d_chunk;
     }
   }
