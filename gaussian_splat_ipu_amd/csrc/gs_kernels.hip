@@ -183,9 +183,15 @@ __device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, con
 // quotient within ~1 ulp; the bound's 5 % inflation covers T, and vy gets
 // 1e-5 |vy| + 0.05 px more).  Only a Gaussian this pass proves outside the
 // band is skipped; the exact test in project_one still runs for the rest.
+// From the band cull's 16-B record (gs_renderer.hip: the mean with w = 1 and
+// the largest log-scale; NaN for an empty slot, +inf for a mean with w != 1,
+// neither of which is culled): the same test as band_culled with the mean and
+// the scales, bit for bit.
 template <bool P2>
-__device__ __forceinline__ bool band_culled_fast(const FrameParams& fp, float4 mean, float4 sg) {
+__device__ __forceinline__ bool band_culled_fast(const FrameParams& fp, float4 cr) {
   const float* m = fp.mvp;
+  const float4 mean = make_float4(cr.x, cr.y, cr.z, 1.0f);
+  const float4 sg = make_float4(cr.w, cr.w, cr.w, 1.0f);
   const float cy = mv_row(m, 1, mean.x, mean.y, mean.z, mean.w);
   const float cw = mv_row(m, 3, mean.x, mean.y, mean.z, mean.w);
   const float vy = (cy * (0.5f * __builtin_amdgcn_rcpf(cw)) + 0.5f) * fp.H;
@@ -439,11 +445,9 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
     // DESIGN.md §8, "block bounds")
     bool culled = false;
     if (i < fp.n) {
-      // both loads in one memory round trip (the test needs the mean unless
-      // the slot is empty)
-      const float4 sg = b.scale_gid[i];
-      const float4 mean = b.mean[i];
-      culled = !(sg.w <= 0.0f) && band_culled_fast<P2>(fp, mean, sg);
+      // one 16-B load (the mean and the largest scale) instead of two
+      const float4 cr = b.cull[i];
+      culled = !__builtin_isnan(cr.w) && band_culled_fast<P2>(fp, cr);
     }
     if (__syncthreads_count(i < fp.n && !culled) == 0) {
       if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = 0u;

@@ -64,6 +64,7 @@ struct Buffers {
   const float4* colour;     // r g b opacity
   const float4* rot;        // quaternion (w x y z)
   const float4* scale_gid;  // sx sy sz gid
+  const float4* cull;       // band cull: mean xyz + largest log-scale (NaN: empty slot, inf: never culled)
   // device order: record i is the input Gaussian perm[i] (3D Morton order by
   // default); the depth sort breaks ties by the input index, as the reference
   const uint32_t* perm;     // [n] device index -> input index

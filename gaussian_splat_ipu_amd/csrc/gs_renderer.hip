@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -24,8 +25,10 @@
 using gsh::set_error;
 
 namespace {
-// scene allocation: the 64-B records (SoA) and the permutation both ways
-size_t scene_bytes(size_t nn) { return nn * (64 + 8); }
+// scene allocation: the 64-B records (SoA), the permutation both ways, then
+// the band cull's 16-B records (16-B aligned)
+size_t cull_offset(size_t nn) { return (nn * (64 + 8) + 15) / 16 * 16; }
+size_t scene_bytes(size_t nn) { return cull_offset(nn) + nn * 16; }
 }  // namespace
 
 namespace gsr {
@@ -686,6 +689,17 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         }
         pi[i] = o;
         pi[nn + o] = (uint32_t)i;
+        // the band cull's record: the mean and the largest log-scale -- all
+        // band_culled_fast reads -- in 16 B instead of the mean's and the
+        // scales' 32 (a mean with w != 1 is never culled: +inf; an empty slot
+        // goes to the full path as before: NaN)
+        float* cr = soa + cull_offset(nn) / 4 + 4 * i;
+        cr[0] = s[0];
+        cr[1] = s[1];
+        cr[2] = s[2];
+        cr[3] = (s[15] <= 0.0f) ? std::numeric_limits<float>::quiet_NaN()
+                : (s[3] != 1.0f ? std::numeric_limits<float>::infinity()
+                                : std::fmax(std::fmax(s[12], s[13]), s[14]));
       }
       e = hipMemcpy(r->d_scene, soa, scene_bytes(nn), hipMemcpyHostToDevice);
       (void)hipHostFree(soa);
@@ -698,6 +712,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.rot = sc + 2 * nn;
   r->buf.scale_gid = sc + 3 * nn;
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
+  r->buf.cull = (const float4*)((const char*)r->d_scene + cull_offset(nn));
   r->buf.inv_perm = r->buf.perm + nn;
 
   // per Gaussian: 48-B record (what the blend reads), its 8-B readback tail,
