@@ -366,6 +366,7 @@ def main():
         kern["blend_cont"]["keys_sorted"] = int(st_view["cont_keys"])
         kern["blend_cont"]["longest_list"] = int(st_view["cont_max"])
         kern["blend_cont"]["prefix_overflows"] = int(st_view["prefix_overflows"])
+        kern["blend_cont"]["full_sorts"] = int(st_view["cont_full_sorts"])
         kern["blend_cont"]["note"] = ("full sample sort of the big lists the blend flagged + the continued blend; "
                                       "alg_bytes counts the continued records only")
     stage = {k: v for k, v in kern.items() if k != "gather"}

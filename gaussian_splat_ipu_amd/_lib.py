@@ -119,7 +119,7 @@ class FrameStats(C.Structure):
         ("cont_lists", C.c_uint32),
         ("cont_max", C.c_uint32),
         ("prefix_overflows", C.c_uint32),
-        ("reserved1", C.c_uint32),
+        ("cont_full_sorts", C.c_uint32),
     ]
 
     def as_dict(self):

@@ -861,6 +861,7 @@ int get_stats(Group* g, gs_frame_stats* st) {
   st->cont_lists = g->mem[0].slot[0]->stats.cont_lists;
   st->cont_max = g->mem[0].slot[0]->stats.cont_max;
   st->prefix_overflows = g->mem[0].slot[0]->stats.prefix_overflows;
+  st->cont_full_sorts = g->mem[0].slot[0]->stats.cont_full_sorts;
   uint64_t cap = ~0ull;
   for (Member& m : g->mem)
     for (gs_renderer* c : m.slot) cap = std::min<uint64_t>(cap, c->pair_cap);

@@ -58,6 +58,29 @@ __device__ __forceinline__ uint32_t depth_key_of(float z) {
 }
 
 constexpr uint2 kEmptyRect = {1u, 1u};  // tx0 = 1 > tx1 = 0
+
+// the alpha box of record g (the z, w of its second float4)
+__device__ __forceinline__ uint2 rec_box(const Buffers& b, uint32_t g) {
+  return reinterpret_cast<const uint2*>(b.rec)[(2ull * g + 1ull) * 2ull + 1ull];
+}
+
+// FrameParams::rect8: a rectangle's four tile bounds, 8 bits each
+__device__ __forceinline__ uint32_t rect8_pack(uint2 r) {
+  return (r.x & 0xFFu) | ((r.x >> 16) & 0xFFu) << 8 | (r.y & 0xFFu) << 16 | (r.y >> 16) << 24;
+}
+__device__ __forceinline__ uint2 rect8_unpack(uint32_t v) {
+  return make_uint2((v & 0xFFu) | ((v >> 8) & 0xFFu) << 16, ((v >> 16) & 0xFFu) | (v >> 24) << 16);
+}
+// the rectangles of Gaussian i as the projection stored them
+__device__ __forceinline__ void store_rects(const FrameParams& fp, const Buffers& b, int i, uint2 rect, uint2 crect) {
+  if (fp.rect8) {
+    reinterpret_cast<uint32_t*>(b.rect)[i] = rect8_pack(rect);
+    reinterpret_cast<uint32_t*>(b.crect)[i] = rect8_pack(crect);
+  } else {
+    b.rect[i] = rect;
+    if (fp.pair_cull) b.crect[i] = crect;
+  }
+}
 constexpr uint32_t kEmptyBox = 0x80007FFFu;  // lo = +32767 > hi = -32768
 constexpr uint32_t kFullBox = 0x7FFF8000u;   // lo = -32768, hi = +32767
 
@@ -282,7 +305,8 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     col = b.colour[i];
     rot = b.rot[i];
   }
-  float4* rec = b.rec + 3 * (size_t)i;  // 48-B record
+  // the record: 32 B per Gaussian (48 B with the colour for the readback)
+  float4* rec = b.rec + (fp.full_record ? 3 : 2) * (size_t)i;
   uint2 rect = kEmptyRect, crect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
@@ -329,8 +353,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     const M3 T = m3_mul(W, J);
     if (fp.band_cull && band_culled<P2>(fp, vy, T, sg)) {
       // no tile row in this band: empty rectangle; the record is never read
-      b.rect[i] = rect;
-      if (fp.pair_cull) b.crect[i] = crect;
+      store_rects(fp, b, i, rect, crect);
       b.depth_key[i] = dkey;
       return false;
     }
@@ -369,8 +392,6 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     uint32_t b01, b23;
     alpha_footprint(vx, vy, k0, k1, k2, k3, fp, pcut, b01, b23);
     const float4 rec0 = make_float4(vx, vy, k0, k2);
-    const float4 rec1 = make_float4(k1, pcut, col.x, col.y);
-    const float4 rec2 = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
     if (fp.full_record) b.rec_tail[i] = make_float2(radius, cz);  // readback only
     if (within && cz < 0.0f) {  // codelets.cpp:493
       rendered = true;
@@ -415,20 +436,27 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     // the blend reads the records of binned Gaussians only: the others'
     // 48 B stay unwritten (off-screen, culled, outside the band, or no tile
     // met by the alpha box); the readback pass writes every record
+    // The blend takes the colour and opacity from the scene (or, with SH, from
+    // col_out): a record with an empty alpha box (k3 = 0 when the conic's
+    // determinant is 0, or opacity < 1/255) is never composited, so its
+    // opacity never matters, and otherwise k3 == col.w
     const uint2 binned = fp.pair_cull ? crect : rect;
-    if (fp.full_record || (binned.x & 0xFFFFu) <= (binned.x >> 16)) {
+    if (fp.full_record) {
       rec[0] = rec0;
-      rec[1] = rec1;
-      rec[2] = rec2;
+      rec[1] = make_float4(k1, pcut, col.x, col.y);
+      rec[2] = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
+    } else if ((binned.x & 0xFFFFu) <= (binned.x >> 16)) {
+      rec[0] = rec0;
+      rec[1] = make_float4(k1, pcut, __uint_as_float(b01), __uint_as_float(b23));
+      if (fp.sh_degree >= 0 && b.sh) b.col_out[i] = col;
     }
-  } else {  // empty slot: never binned; a neutral record for the readback
+  } else if (fp.full_record) {  // empty slot: never binned; a neutral record for the readback
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     rec[1] = make_float4(0.0f, __builtin_huge_valf(), 0.0f, 0.0f);
     rec[2] = make_float4(0.0f, 0.0f, __uint_as_float(kEmptyBox), __uint_as_float(kEmptyBox));
-    if (fp.full_record) b.rec_tail[i] = make_float2(0.0f, 0.0f);
+    b.rec_tail[i] = make_float2(0.0f, 0.0f);
   }
-  b.rect[i] = rect;
-  if (fp.pair_cull) b.crect[i] = crect;
+  store_rects(fp, b, i, rect, crect);
   b.depth_key[i] = dkey;
   return rendered;
 }
@@ -454,8 +482,7 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
       return;
     }
     if (culled) {  // no tile row in this band: empty rectangle, no record
-      b.rect[i] = kEmptyRect;
-      if (fp.pair_cull) b.crect[i] = kEmptyRect;
+      store_rects(fp, b, i, kEmptyRect, kEmptyRect);
       b.depth_key[i] = 0xFFFFFFFFu;
     } else if (i < fp.n) {
       rendered = project_one<P2>(fp, b, i);
@@ -665,8 +692,13 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int i = i00 + k * 1024 + (int)threadIdx.x;
-        rr[k] = live[k] ? b.rect[i] : kEmptyRect;
-        qq[k] = live[k] ? b.crect[i] : kEmptyRect;
+        if (fp.rect8) {
+          rr[k] = rect8_unpack(live[k] ? reinterpret_cast<const uint32_t*>(b.rect)[i] : 0x00010001u);
+          qq[k] = rect8_unpack(live[k] ? reinterpret_cast<const uint32_t*>(b.crect)[i] : 0x00010001u);
+        } else {
+          rr[k] = live[k] ? b.rect[i] : kEmptyRect;
+          qq[k] = live[k] ? b.crect[i] : kEmptyRect;
+        }
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -963,7 +995,10 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int i = i0 + k * 1024 + (int)threadIdx.x;
-        r[k] = live[k] ? rects[i] : kEmptyRect;
+        if (fp.rect8)
+          r[k] = rect8_unpack(live[k] ? reinterpret_cast<const uint32_t*>(b.crect)[i] : 0x00010001u);
+        else
+          r[k] = live[k] ? rects[i] : kEmptyRect;
         dk[k] = live[k] ? b.depth_key[i] : 0u;
       }
 #pragma unroll
@@ -1613,8 +1648,9 @@ constexpr int kBigSeg = 2048;
 // sample sort of the big lists: buckets of ~kBktAvg keys, at most kBktMax
 // per list (their splitters are staged in LDS)
 constexpr uint32_t kBktAvg = 1024, kBktMax = 2048;
-// lazy big lists: the sorted prefix holds ~this many keys (see gs_big_select_kernel)
-constexpr uint32_t kLazyPrefix = 1536;
+// lazy big lists: the sorted prefix holds ~this many keys (see gs_big_select_kernel);
+// the continuation's window the next ~kLazyWindow (gs_big_cont_kernel)
+constexpr uint32_t kLazyPrefix = 1536, kLazyWindow = 2560;
 __device__ __forceinline__ uint32_t big_buckets(uint32_t L) {
   return min(kBktMax, (L + kBktAvg - 1u) / kBktAvg);
 }
@@ -1625,7 +1661,12 @@ __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buf
   __shared__ uint32_t s_maxl;
   const uint32_t n_big = b.counters[0];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool keep_buckets = fp.lazy && fp.big_pass == 1;
+  const bool keep_buckets = fp.lazy && fp.big_pass != 0;
+  // pass 2: nothing to do unless a continuation wave outlived its window
+  if (fp.big_pass == 2 && b.counters[1] == 0u) {
+    if (tid == 0) b.counters[12] = 0u;
+    return;
+  }
   if (tid == 0) s_maxl = 0;
   uint32_t carry = 0, carry_b = 0, maxl = 0;
   for (uint32_t j0 = 0; j0 < n_big; j0 += 1024) {
@@ -1634,14 +1675,16 @@ __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buf
     if (j < n_big) {
       uint32_t s, L;
       tile_segment(fp, b, (int)b.big_tiles[j], s, L);
-      // pass 1 (lazy frames): only the lists whose blend outlived the prefix
-      const bool use = fp.big_pass == 0 || b.big_flag[j] != 0u;
+      // pass 2 (lazy frames): only the lists whose continuation outlived its window
+      const bool use = fp.big_pass == 0 || (fp.big_pass == 1 ? b.big_flag[j] : b.big_flag2[j]) != 0u;
       c = use ? (L + kBigSeg - 1) / kBigSeg : 0u;
       nb = (use || keep_buckets) ? big_buckets(L) : 0u;
       maxl = use ? max(maxl, L) : maxl;
       if (fp.lazy && fp.big_pass == 0) {
         b.big_flag[j] = 0u;
         b.big_cnt[j] = 0u;
+        b.big_flag2[j] = 0u;
+        b.big_cnt2[j] = 0u;
 #pragma unroll
         for (int q = 0; q < 4; ++q) b.cont_flag[4 * j + q] = 0u;
       }
@@ -1734,6 +1777,10 @@ __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffe
       if (tid == 0u) {
         const uint32_t q = (uint32_t)(((unsigned long long)kLazyPrefix * S) / L);
         b.big_thr[j] = (uint32_t)(keys[min(q, S - 1u)] >> 32);
+        // the continuation's window: up to the (prefix + window) / L quantile,
+        // or the list's end (~0) when that reaches past the sample
+        const uint32_t q2 = (uint32_t)(((unsigned long long)(kLazyPrefix + kLazyWindow) * S) / L);
+        b.big_thr2[j] = kLazyPrefix + kLazyWindow < L && q2 < S ? (uint32_t)(keys[q2] >> 32) : 0xFFFFFFFFu;
       }
       // and the buckets of the full sort the continuation may need, from this
       // (larger) sample: the continuation's sample sort then needs no split
@@ -1770,9 +1817,12 @@ __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffe
 // the same bit for bit.
 // one workgroup per 2048-key work item (pass 0: every big list): append the
 // item's keys below the list's bound to the list's prefix (pairs_alt[s, ...))
+// The keys of the continuation's window [bound, bound2) go to the END of the
+// list's pairs_alt region (from s + L - 1 down): the prefix takes at most the
+// keys below the bound from the front, so the two never meet.
 __global__ __launch_bounds__(256) void gs_big_select_kernel(FrameParams fp, Buffers b) {
-  __shared__ uint32_t s_par[5];
-  __shared__ uint32_t s_n, s_base;
+  __shared__ uint32_t s_par[6];
+  __shared__ uint32_t s_n, s_base, s_n2, s_base2;
   const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
   const uint32_t tid = threadIdx.x;
   constexpr int Q = kBigSeg / 256;
@@ -1787,12 +1837,14 @@ __global__ __launch_bounds__(256) void gs_big_select_kernel(FrameParams fp, Buff
       s_par[2] = c;
       s_par[3] = b.big_thr[j];
       s_par[4] = j;
+      s_par[5] = b.big_thr2[j];
       s_n = 0u;
+      s_n2 = 0u;
     }
     __syncthreads();
-    const uint32_t s = s_par[0], L = s_par[1], c = s_par[2], thr = s_par[3], j = s_par[4];
+    const uint32_t s = s_par[0], L = s_par[1], c = s_par[2], thr = s_par[3], j = s_par[4], thr2 = s_par[5];
     unsigned long long key[Q];
-    uint32_t rk[Q];
+    uint32_t rk[Q], rk2[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
@@ -1801,15 +1853,22 @@ __global__ __launch_bounds__(256) void gs_big_select_kernel(FrameParams fp, Buff
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const uint32_t i = c * (uint32_t)kBigSeg + (uint32_t)q * 256u + tid;
-      rk[q] = (i < L && (uint32_t)(key[q] >> 32) < thr) ? atomicAdd(&s_n, 1u) : 0xFFFFFFFFu;
+      const uint32_t z = (uint32_t)(key[q] >> 32);
+      rk[q] = (i < L && z < thr) ? atomicAdd(&s_n, 1u) : 0xFFFFFFFFu;
+      rk2[q] = (fp.lazy && i < L && z >= thr && (thr2 == 0xFFFFFFFFu || z < thr2)) ? atomicAdd(&s_n2, 1u)
+                                                                                 : 0xFFFFFFFFu;
     }
     __syncthreads();
-    if (tid == 0) s_base = s_n ? atomicAdd(&b.big_cnt[j], s_n) : 0u;
+    if (tid == 0) {
+      s_base = s_n ? atomicAdd(&b.big_cnt[j], s_n) : 0u;
+      s_base2 = s_n2 ? atomicAdd(&b.big_cnt2[j], s_n2) : 0u;
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const uint32_t pos = s_base + rk[q];
       if (rk[q] != 0xFFFFFFFFu && pos < (uint32_t)kSortLdsCap) b.pairs_alt[s + pos] = key[q];
+      if (rk2[q] != 0xFFFFFFFFu) b.pairs_alt[s + L - 1u - (s_base2 + rk2[q])] = key[q];
     }
     __syncthreads();
   }
@@ -1829,6 +1888,88 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       merge_sort_tile<256, 2, kOutInput, kSrcAltRekey>(b, s, n, keys);
     }
     if (threadIdx.x == 0) b.big_len[j] = ok ? n : 0u;
+    __syncthreads();
+  }
+}
+
+// the box of the live pixels of a big list's saved waves (the union of their boxes)
+__device__ __forceinline__ void cont_live_box(const Buffers& b, uint32_t j, int& x0, int& x1, int& y0, int& y1) {
+  x0 = 0x7FFFFFFF, x1 = -1, y0 = 0x7FFFFFFF, y1 = -1;
+  for (int w = 0; w < 4; ++w)
+    if (b.cont_flag[4 * j + w]) {
+      const uint2 cb = b.cont_box[4 * j + w];
+      x0 = min(x0, (int)(cb.x & 0xFFFFu));
+      x1 = max(x1, (int)(cb.x >> 16));
+      y0 = min(y0, (int)(cb.y & 0xFFFFu));
+      y1 = max(y1, (int)(cb.y >> 16));
+    }
+}
+
+// Lazy continuation, pass 1: one workgroup per big list the blend flagged.
+// The window's keys (depth in [bound, bound2), kept by the prefix select)
+// whose alpha box meets the saved waves' live pixels are sorted into the
+// list's front; the continued blend walks them.  The list is complete when
+// the window reached its end (bound2 = ~0); otherwise a wave that outlives
+// the window flags the list for pass 2, the full sample sort of the keys of
+// depth >= cont_thr.  A window whose filtered keys overflow one workgroup's
+// sort is skipped (cont_len 0): pass 2 then takes every key past the prefix.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_cont_kernel(FrameParams fp, Buffers b) {
+  __shared__ unsigned long long keys[kSortLdsCap];
+  __shared__ uint32_t s_m;
+  const uint32_t n_big = b.counters[0];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t j = blockIdx.x; j < n_big; j += gridDim.x) {
+    if (b.big_flag[j] == 0u) continue;  // (uniform)
+    uint32_t s, L;
+    tile_segment(fp, b, (int)b.big_tiles[j], s, L);
+    // the prefix was sorted (else the keys past it start at depth 0)
+    const bool pre = b.big_len[j] != 0u;
+    const uint32_t thr = pre ? b.big_thr[j] : 0u, thr2 = b.big_thr2[j];
+    const uint32_t n2 = pre ? min(b.big_cnt2[j], L) : 0u;
+    int lx0, lx1, ly0, ly1;
+    cont_live_box(b, j, lx0, lx1, ly0, ly1);
+    if (tid == 0u) s_m = 0u;
+    __syncthreads();
+    // U keys per thread in flight: all key loads, then all box gathers
+    constexpr int U = 8;
+    for (uint32_t k0 = 0; k0 < n2; k0 += 256u * U) {
+      unsigned long long key[U];
+      uint2 bx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t k = k0 + (uint32_t)u * 256u + tid;
+        key[u] = k < n2 ? b.pairs_alt[s + L - 1u - k] : ~0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        bx[u] = key[u] != ~0ull ? rec_box(b, (uint32_t)key[u])
+                                : make_uint2(kEmptyBox, kEmptyBox);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rx0 = (int)(bx[u].x << 16) >> 16, rx1 = (int)bx[u].x >> 16;
+        const int ry0 = (int)(bx[u].y << 16) >> 16, ry1 = (int)bx[u].y >> 16;
+        if (rx0 <= lx1 && rx1 >= lx0 && ry0 <= ly1 && ry1 >= ly0) {
+          const uint32_t p = atomicAdd(&s_m, 1u);
+          if (p < (uint32_t)kSortLdsCap) keys[p] = key[u];
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t m = s_m;
+    const bool ok = pre && m <= (uint32_t)kSortLdsCap;
+    if (ok && m > 0u && !merge_sort_tile<256, 2, kOutDevice, kSrcLds>(b, s, m, keys)) {
+      // equal depths: the sorted device-index keys are in keys[0, m); again
+      // with input-index keys
+      __syncthreads();
+      for (uint32_t k = tid; k < m; k += 256u) keys[k] = rekey_input(b, keys[k]);
+      __syncthreads();
+      merge_sort_tile<256, 2, kOutInput, kSrcLds>(b, s, m, keys);
+    }
+    if (tid == 0u) {
+      b.cont_len[j] = ok ? m : 0u;
+      b.cont_full[j] = ok && thr2 == 0xFFFFFFFFu ? 1u : 0u;
+      b.cont_thr[j] = ok ? thr2 : thr;  // where pass 2 starts
+    }
     __syncthreads();
   }
 }
@@ -1859,9 +2000,9 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
   const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
   const uint32_t tid = threadIdx.x;
   constexpr int Q = kBigSeg / 256;
-  // lazy continuation (pass 1): only the keys past the prefix whose alpha box
-  // meets the list's live pixels (the saved waves' boxes) are sorted
-  const bool filt = fp.lazy && fp.big_pass == 1;
+  // lazy continuation (pass 2): only the keys past the window (cont_thr) whose
+  // alpha box meets the list's live pixels (the saved waves' boxes) are sorted
+  const bool filt = fp.lazy && fp.big_pass == 2;
   for (uint32_t k = blockIdx.x; k < total; k += gridDim.x) {
     if (tid == 0) {
       uint32_t j, c;
@@ -1873,23 +2014,15 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
       s_par[2] = c;
       s_par[3] = b.bk_off[j];
       if (filt) {
-        int bx0 = 0x7FFFFFFF, bx1 = -1, by0 = 0x7FFFFFFF, by1 = -1;
-        for (int w = 0; w < 4; ++w)
-          if (b.cont_flag[4 * j + w]) {
-            const uint2 cb = b.cont_box[4 * j + w];
-            bx0 = min(bx0, (int)(cb.x & 0xFFFFu));
-            bx1 = max(bx1, (int)(cb.x >> 16));
-            by0 = min(by0, (int)(cb.y & 0xFFFFu));
-            by1 = max(by1, (int)(cb.y >> 16));
-          }
+        int bx0, bx1, by0, by1;
+        cont_live_box(b, j, bx0, bx1, by0, by1);
         s_par[4] = (uint32_t)bx0;
         s_par[5] = (uint32_t)bx1;
         s_par[6] = (uint32_t)by0;
         s_par[7] = (uint32_t)by1;
-        // keys below the bound were composited by the prefix blend -- unless
-        // the prefix was not sorted (big_len 0: more than kSortLdsCap keys
-        // below the bound), when the continuation walks the whole list
-        s_par[8] = b.big_len[j] ? b.big_thr[j] : 0u;
+        // keys below cont_thr were composited by the prefix blend and the
+        // window's continuation (gs_big_cont_kernel)
+        s_par[8] = b.cont_thr[j];
       }
     }
     __syncthreads();
@@ -1916,7 +2049,7 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
 #pragma unroll
       for (int q = 0; q < Q; ++q)  // the record's alpha box (its 3rd float4's z, w)
         bx[q] = (use[q] && (uint32_t)(key[q] >> 32) >= thr)
-                    ? reinterpret_cast<const uint2*>(b.rec)[(3ull * (uint32_t)key[q] + 2ull) * 2ull + 1ull]
+                    ? rec_box(b, (uint32_t)key[q])
                     : make_uint2(kEmptyBox, kEmptyBox);
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
@@ -1961,8 +2094,9 @@ __global__ __launch_bounds__(256) void gs_big_bscan_kernel(FrameParams fp, Buffe
   const uint32_t n_big = b.counters[0];
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * 4u;
+  if (fp.big_pass == 2 && b.counters[1] == 0u) return;  // no list outlived its window
   for (uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6); j < n_big; j += nw) {
-    if (fp.big_pass == 1 && b.big_flag[j] == 0u) continue;  // (wave-uniform)
+    if (fp.big_pass == 2 && b.big_flag2[j] == 0u) continue;  // (wave-uniform)
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t B = big_buckets(L), bo = b.bk_off[j];
@@ -1981,7 +2115,7 @@ __global__ __launch_bounds__(256) void gs_big_bscan_kernel(FrameParams fp, Buffe
       }
       carry += (uint32_t)__shfl(inc, 63, 64);
     }
-    if (fp.lazy && fp.big_pass == 1 && lane == 0) b.cont_len[j] = carry;  // the filtered keys
+    if (fp.lazy && fp.big_pass == 2 && lane == 0) b.cont_len[j] = carry;  // the filtered keys
   }
 }
 
@@ -1994,14 +2128,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   uint32_t* const r_hist = (uint32_t*)keys;
   uint32_t* const r_base = r_hist + 8 * 256;
   uint32_t(*const r_wcnt)[256] = (uint32_t(*)[256])(r_hist + 9 * 256);
-  const uint32_t n_bk = b.counters[0] ? b.counters[14] : 0u;
+  const uint32_t n_bk = (b.counters[0] && (fp.big_pass != 2 || b.counters[1])) ? b.counters[14] : 0u;
   for (uint32_t k = blockIdx.x; k < n_bk; k += gridDim.x) {
     const uint32_t j = b.bk_list[k];
-    if (fp.big_pass == 1 && b.big_flag[j] == 0u) continue;  // (uniform) lazy continuation: flagged lists only
+    if (fp.big_pass == 2 && b.big_flag2[j] == 0u) continue;  // (uniform) lazy continuation: flagged lists only
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t bo = b.bk_off[j], B = big_buckets(L);
-    const uint32_t Lk = (fp.lazy && fp.big_pass == 1) ? b.cont_len[j] : L;  // (pass 1: the filtered keys)
+    const uint32_t Lk = (fp.lazy && fp.big_pass == 2) ? b.cont_len[j] : L;  // (pass 2: the filtered keys)
     const uint32_t st = b.bk_start[k], en = k + 1u < bo + B ? b.bk_start[k + 1u] : Lk;
     const uint32_t n = en - st;
     if (n == 0u) continue;  // (uniform)
@@ -2181,8 +2315,10 @@ __device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t 
 // staged, for the bench's algorithmic bytes (lane 0 of the wave)
 __device__ __forceinline__ void blend_count_store(const FrameParams& fp, const Buffers& b, int wid,
                                                   uint32_t staged) {
-  if (fp.count_records && (threadIdx.x & 63) == 0)
-    (fp.blend_cont ? b.blend_count_cont : b.blend_count)[wid] = staged;
+  if (fp.count_records && (threadIdx.x & 63) == 0) {
+    if (fp.blend_cont && fp.big_pass == 2) b.blend_count_cont[wid] += staged;  // (after pass 1's)
+    else (fp.blend_cont ? b.blend_count_cont : b.blend_count)[wid] = staged;
+  }
 }
 
 template <int BQW, bool HWEXP>
@@ -2196,8 +2332,11 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
   // are (slot, chunk) of the flagged lists whose state was saved.
   uint32_t jb = 0xFFFFFFFFu;
   if (fp.blend_cont) {
-    if ((uint32_t)slot >= b.counters[0] || b.cont_flag[4 * slot + chunk] == 0u) {
-      blend_count_store(fp, b, wid, 0u);
+    // pass 1: the waves the prefix blend saved; pass 2: those of them that
+    // outlived their window too
+    if ((uint32_t)slot >= b.counters[0] || b.cont_flag[4 * slot + chunk] == 0u ||
+        (fp.big_pass == 2 && b.big_flag2[slot] == 0u)) {
+      if (fp.big_pass == 1) blend_count_store(fp, b, wid, 0u);
       return;
     }
     jb = (uint32_t)slot;
@@ -2282,7 +2421,7 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
   const uint32_t* __restrict__ list = b.list + s + k0;
   L -= k0;
 
-  // wave-private staging of one batch of 64 records (48 B each) in LDS
+  // wave-private staging of one batch of 64 records (48 B each with the colour) in LDS
   __shared__ float4 s_rec[GS_BLEND_WPG][3][64];
   float4(*const st)[64] = s_rec[wave];
 
@@ -2292,14 +2431,20 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
     if (k < L) g = list[k];
     return g < (uint32_t)fp.n ? g : 0xFFFFFFFFu;  // defensive: never read past the records
   };
+  // a record (32 B) and its colour + opacity (the scene's, or gs_set_sh's
+  // view-dependent one), assembled as the staged 48-B layout
+  const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
+  auto load_rec = [&](uint32_t g, float4& r0, float4& r1, float4& r2) {
+    const float4* qq = b.rec + 2 * (size_t)g;
+    r0 = qq[0];
+    const float4 t = qq[1];    // k1 pcut boxx boxy
+    const float4 c = ccol[g];  // r g b opacity
+    r1 = make_float4(t.x, t.y, c.x, c.y);
+    r2 = make_float4(c.z, c.w, t.z, t.w);
+  };
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
   uint32_t g_cur = load_idx(lane);
-  if (g_cur != 0xFFFFFFFFu) {
-    const float4* qq = b.rec + 3 * (size_t)g_cur;
-    a0 = qq[0];
-    a1 = qq[1];
-    a2 = qq[2];
-  }
+  if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
   uint32_t g_next = load_idx(64 + lane);
 
   uint32_t staged = 0;  // records staged (profiled frames)
@@ -2322,12 +2467,7 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
     // prefetch the next batch
     g_cur = g_next;
     a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g_cur != 0xFFFFFFFFu) {
-      const float4* qq = b.rec + 3 * (size_t)g_cur;
-      a0 = qq[0];
-      a1 = qq[1];
-      a2 = qq[2];
-    }
+    if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
     g_next = load_idx(base + 128 + lane);
 
     // m = the batch's records whose box touches this lane's quad (bit k =
@@ -2406,8 +2546,12 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
     // the next batch's LDS stores come after every lane's reads of this one
     __builtin_amdgcn_wave_barrier();
   }
-  if (jb != 0xFFFFFFFFu && !fp.blend_cont && L < Lfull && ballot64(!q.done) != 0ull) {
-    // the prefix ended with live pixels: save the wave's state, flag the list
+  // the list goes on past what this pass walked: the prefix blend's sorted
+  // prefix, or a continuation window that did not reach the list's end
+  bool more = false;
+  if (jb != 0xFFFFFFFFu) more = fp.blend_cont ? (fp.big_pass == 1 && b.cont_full[jb] == 0u) : L < Lfull;
+  if (more && ballot64(!q.done) != 0ull) {
+    // the walk ended with live pixels: save the wave's state, flag the list
     float* sv = b.cont_state + (size_t)(4 * jb + chunk) * 6 * 64 + lane;
     sv[0] = q.T;
     sv[64] = q.c01.x;
@@ -2423,11 +2567,17 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
     if (lane == 0) {
       b.cont_box[4 * jb + chunk] = make_uint2((blo & 0xFFFFu) | (bhi << 16), (blo >> 16) | (bhi & 0xFFFF0000u));
       b.cont_flag[4 * jb + chunk] = 1u;
-      b.big_flag[jb] = 1u;
+      if (!fp.blend_cont) {
+        b.big_flag[jb] = 1u;
+      } else {  // pass 1 -> pass 2
+        b.big_flag2[jb] = 1u;
+        b.counters[1] = 1u;
+      }
     }
     blend_count_store(fp, b, wid, staged);
     return;  // the continuation stores these pixels
   }
+  if (fp.blend_cont && lane == 0) b.cont_flag[4 * jb + chunk] = 0u;  // this wave is done
   blend_count_store(fp, b, wid, staged);
   if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
@@ -2445,6 +2595,7 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
 // counters load, 4 resident per CU).
 template <bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_cont_kernel(FrameParams fp, Buffers b) {
+  if (fp.big_pass == 2 && b.counters[1] == 0u) return;  // no list outlived its window
   const int nblk = (int)((b.counters[0] * (uint32_t)fp.chunks_per_tile + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) blend_body<4, HWEXP>(fp, b, blk);
 }
@@ -2560,16 +2711,27 @@ void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const unsigned block = 64 * GS_BLEND_WPG;
   // the big lists whose blend outlived the prefix: sorted in full, then
   // their saved waves continue (nothing to do when none was flagged)
+  // pass 1: the flagged lists' windows, sorted, then their saved waves
+  // continue; pass 2 (no-ops unless a wave outlived its window): those lists
+  // sorted in full past the window, and their waves continue again
   FrameParams f1 = fp;
   f1.big_pass = 1;
-  gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f1, b);
-  // (the splitters of every big list were chosen by the frame's first split pass)
-  launch_big_buckets(f1, b, s);
+  gs_big_cont_kernel<<<2048, 256, 0, s>>>(f1, b);
   f1.blend_cont = 1;
   if (fp.fast_exp)
     gs_blend_cont_kernel<true><<<grid, block, 0, s>>>(f1, b);
   else
     gs_blend_cont_kernel<false><<<grid, block, 0, s>>>(f1, b);
+  FrameParams f2 = fp;
+  f2.big_pass = 2;
+  gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f2, b);
+  // (the splitters of every big list were chosen by the frame's first split pass)
+  launch_big_buckets(f2, b, s);
+  f2.blend_cont = 1;
+  if (fp.fast_exp)
+    gs_blend_cont_kernel<true><<<grid, block, 0, s>>>(f2, b);
+  else
+    gs_blend_cont_kernel<false><<<grid, block, 0, s>>>(f2, b);
 }
 
 }  // namespace gsk

@@ -42,10 +42,13 @@ struct FrameParams {
   int full_record;    // also write the readback-only record tail (radius, clip z)
   int pair_cull;      // bin only the tiles the alpha box meets (crect); the
                       // reference list lengths are counted alongside
+  int rect8;          // pair_cull with <= 256 tile columns and band rows: rect and crect hold
+                      //   4 B per Gaussian, 8 bits per bound (rect8_pack)
   int big_separate;   // big lists sorted by gs_sort_big_kernel (launched before the tile sort)
   int lazy;           // big lists: only their nearest keys are sorted before the blend; the
                       //   blocks whose pixels outlive that prefix continue after a full sort
-  int big_pass;       // big-list kernels: 0 = every big list, 1 = the lists flagged by the blend
+  int big_pass;       // big-list kernels: 0 = every big list; lazy continuation: 1 = the lists
+                      //   flagged by the blend (window), 2 = those flagged again (full sort)
   int blend_cont;     // blend: 1 = the continuation of the flagged big-list blocks
   int count_records;  // blend: each wave writes the records it composited to blend_count
   int fast_exp;       // blend: hardware exp2 (GS_FLAG_FAST_EXP, within a stated tolerance)
@@ -70,10 +73,15 @@ struct Buffers {
   const uint32_t* perm;     // [n] device index -> input index
   const uint32_t* inv_perm; // [n] input index -> device index
   // per-Gaussian projection outputs
-  float4* rec;              // 3 x float4 (48 B): mx my k0 k2 | k1 pcut r g | b op boxx boxy
+  float4* rec;              // frames: 2 x float4 (32 B): mx my k0 k2 | k1 pcut boxx boxy (the colour
+                            //   is the scene's, or col_out); full_record (readback): 3 x float4
+                            //   (48 B): mx my k0 k2 | k1 pcut r g | b op boxx boxy
+  float4* col_out;          // [n] gs_set_sh frames: the view-dependent colour + opacity (in the
+                            //   record region past the 32-B records)
   float2* rec_tail;         // radius, clip z: readback only (written with full_record)
   uint32_t* depth_key;      // order-preserving key of clip z
   uint2* rect;              // (tx0 | tx1 << 16, ty0 | ty1 << 16), band-relative rows
+                            //   (rect8: a u32 per Gaussian, tx0 | tx1 << 8 | ty0 << 16 | ty1 << 24)
   uint2* crect;             // rect cut to the tiles the alpha box meets (pair_cull)
   // binning
   uint32_t* tile_count;     // [n_tiles]      (memset 0 each frame)
@@ -121,6 +129,13 @@ struct Buffers {
                             //   (x0 | x1 << 16, y0 | y1 << 16)
   uint32_t* cont_len;       // [n_tiles] keys the continuation walks (the list's keys past the
                             //   prefix whose alpha box meets its live pixels, sorted)
+  // the continuation's window (pass 1): keys of depth in [big_thr, big_thr2), kept unsorted at
+  // the end of the list's pairs_alt region by the prefix select
+  uint32_t* big_thr2;       // [n_tiles] the window's depth bound (~0: to the end of the list)
+  uint32_t* big_cnt2;       // [n_tiles] keys in the window
+  uint32_t* big_flag2;      // [n_tiles] 1: a pixel outlived the window too (full sort, pass 2)
+  uint32_t* cont_full;      // [n_tiles] 1: the window's sorted keys are the rest of the list
+  uint32_t* cont_thr;       // [n_tiles] pass 2 takes the keys of depth >= this
   uint32_t* footer;         // row-band group: counters[16] + reference list lengths[n_tiles]
                             //   of this frame, next to its BGR8 band in the all-gather slot
                             //   (written by the chunked scan; nullptr = none)

@@ -207,6 +207,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
                        : fp.blend_bqw == 8 ? (int)((tw / 16) * (th / 4))
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) fp.blend_lpt = std::atoi(ev);  // (A/B)
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
@@ -225,6 +226,9 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   }
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
+  // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
+  fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256) ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_RECT8")) fp.rect8 = fp.rect8 && std::atoi(ev) != 0;  // (A/B)
   // the big-list launch only when the last frame the device completed had
   // big lists (a hint read from the mapped counters: either choice sorts
   // every list, the other launch handles them otherwise)
@@ -457,7 +461,7 @@ int finish_frame(gs_renderer* r) {
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
   r->stats.blend_records = r->stats.blend_cont_records = r->stats.cont_keys = 0;
-  r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = 0;
+  r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = r->stats.cont_full_sorts = 0;
   if (r->last_counted && r->bcount_words) {
     // profiled frame: the list records the blend read.  The waves of a tile
     // each stage a prefix of the same list (the tile's records come from HBM
@@ -479,13 +483,15 @@ int finish_frame(gs_renderer* r) {
     }
     if (r->last_fp.lazy && c[0] > 0) {
       // the continuation's lists and their filtered key counts
-      std::vector<uint32_t> fl(c[0]), cl(c[0]), bl(c[0]);
+      std::vector<uint32_t> fl(c[0]), cl(c[0]), bl(c[0]), f2(c[0]);
       GS_HIP(hipMemcpy(fl.data(), r->buf.big_flag, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
+      GS_HIP(hipMemcpy(f2.data(), r->buf.big_flag2, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       GS_HIP(hipMemcpy(cl.data(), r->buf.cont_len, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       GS_HIP(hipMemcpy(bl.data(), r->buf.big_len, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       for (uint32_t j = 0; j < c[0]; ++j)
         if (fl[j]) {
           r->stats.prefix_overflows += bl[j] == 0u ? 1u : 0u;
+          r->stats.cont_full_sorts += f2[j] != 0u ? 1u : 0u;
           r->stats.cont_lists += 1;
           r->stats.cont_keys += cl[j];
           r->stats.cont_max = std::max(r->stats.cont_max, cl[j]);
@@ -715,15 +721,17 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.cull = (const float4*)((const char*)r->d_scene + cull_offset(nn));
   r->buf.inv_perm = r->buf.perm + nn;
 
-  // per Gaussian: 48-B record (what the blend reads), its 8-B readback tail,
-  // 8-B tile rectangle and its alpha-box cut, 4-B depth key; plus V per
-  // project workgroup
+  // per Gaussian: 48 B of record (frames: the 32-B record the blend reads and,
+  // with gs_set_sh, the 16-B view-dependent colour; the readback: the 48-B
+  // record), its 8-B readback tail, 8-B tile rectangle and its alpha-box cut
+  // (rect8: 4 B each), 4-B depth key; plus V per project workgroup
   const size_t nblk = (nn + 255) / 256;
   if ((e = hipMalloc(&r->d_gauss, nn * (48 + 8 + 8 + 8 + 4) + nblk * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(per-Gaussian)"));
   poison(r->d_gauss, nn * (48 + 8 + 8 + 8 + 4) + nblk * 4, "gauss");
   r->buf.rec = (float4*)r->d_gauss;
   r->buf.rec_tail = (float2*)((char*)r->d_gauss + nn * 48);
+  r->buf.col_out = (float4*)((char*)r->d_gauss + nn * 32);  // (frames: the record region past the 32-B records)
   r->buf.rect = (uint2*)((char*)r->d_gauss + nn * 56);
   r->buf.crect = (uint2*)((char*)r->d_gauss + nn * 64);
   r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
@@ -785,10 +793,10 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
 
   // lazy big lists (gs_kernels.hip, kLazyPrefix): with the chunked binning
   // and 16x16 tiles (four 8x8 blend waves per tile); per tile 9 u32 + the
-  // saved state of 4 waves (6 x 64 floats each)
+  // saved state of 4 waves (6 x 64 floats each) + their boxes + 6 u32
   if (!r->bin_global && r->n_chunks > 0 && cfg->tile_width == 16 && cfg->tile_height == 16) {
     const size_t TT = (size_t)r->t_cap;
-    const size_t lazy_bytes = TT * (9 * 4 + 4 * 6 * 64 * 4 + 4 * 8 + 4) + 8;
+    const size_t lazy_bytes = TT * (9 * 4 + 4 * 6 * 64 * 4 + 4 * 8 + 4 + 5 * 4) + 8;
     if ((e = hipMalloc(&r->d_lazy, lazy_bytes)) != hipSuccess)
       return fail(hip_fail(e, "hipMalloc(lazy big lists)"));
     poison(r->d_lazy, lazy_bytes, "lazy");
@@ -802,6 +810,11 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     r->buf.cont_state = (float*)(u + 9 * TT);
     r->buf.cont_box = (uint2*)(((uintptr_t)(r->buf.cont_state + TT * 4 * 6 * 64) + 7) & ~(uintptr_t)7);
     r->buf.cont_len = (uint32_t*)(r->buf.cont_box + TT * 4);
+    r->buf.big_thr2 = r->buf.cont_len + TT;
+    r->buf.big_cnt2 = r->buf.cont_len + 2 * TT;
+    r->buf.big_flag2 = r->buf.cont_len + 3 * TT;
+    r->buf.cont_full = r->buf.cont_len + 4 * TT;
+    r->buf.cont_thr = r->buf.cont_len + 5 * TT;
     if ((e = hipMemset(r->d_lazy, 0, TT * 9 * 4)) != hipSuccess) return fail(hip_fail(e, "hipMemset(lazy)"));
   }
 
@@ -974,6 +987,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
     // the BGR8 target, the stats and the histogram snapshot are untouched.
     gsk::FrameParams fp = r->last_fp;
     fp.pair_cull = 0;
+    fp.rect8 = 0;
     gsk::Buffers bb = r->buf;
     bb.footer = nullptr;        // (a group's all-gather slot belongs to the frame)
     bb.group_sticky = nullptr;  // (this re-binning's overflow is handled here, not by the group)
@@ -1047,6 +1061,7 @@ int read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     fp.band_cull = 0;
     fp.bin_global = 0;  // (no tile_count atomics)
     fp.full_record = 1;
+    fp.rect8 = 0;  // (the readback takes the 16-bit reference rectangle)
     gsk::launch_project(fp, r->buf, r->stream);
     GS_HIP(hipGetLastError());
     GS_HIP(hipStreamSynchronize(r->stream));

@@ -185,7 +185,9 @@ typedef struct gs_frame_stats {
   uint32_t prefix_overflows; /* big lists whose keys below the depth bound
                              outnumbered one workgroup's sort (the whole
                              list went to the continuation)              */
-  uint32_t reserved1;
+  uint32_t cont_full_sorts; /* of the continued lists, those whose live pixels
+                             outlived the sorted window past the prefix (the
+                             full sample sort of the rest ran for them)   */
 } gs_frame_stats;
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */

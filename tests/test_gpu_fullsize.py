@@ -337,10 +337,12 @@ def test_ref_tile_major_readback(built, tw, th):
 @pytest.mark.parametrize("op_lo,op_hi", [(0.004, 0.02), (0.02, 0.3)])
 def test_lazy_big_lists_continuation(built, op_lo, op_hi):
     """Big lists (> 2048 keys) of faint Gaussians: pixels outlive the sorted
-    prefix of ~1.5 k keys, so their blend waves save their state, the lists are
-    sorted in full and the waves continue (gs_kernels.hip, lazy big lists).
-    The second frame of the renderer takes that path; the frame must equal the
-    oracle's bit for bit.  op 0.004-0.02: nearly every big tile continues;
+    prefix of ~1.5 k keys, so their blend waves save their state and continue
+    over the sorted window of the next keys (pass 1); waves that outlive the
+    window too continue over the rest of the list, sorted in full (pass 2;
+    gs_kernels.hip, lazy big lists).  The second frame of the renderer takes
+    that path; the frame must equal the oracle's bit for bit.  op 0.004-0.02:
+    nearly every big tile continues, and some pixels never saturate (pass 2);
     0.02-0.3: some do."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
@@ -352,12 +354,16 @@ def test_lazy_big_lists_continuation(built, op_lo, op_hi):
         opacity_hi=op_hi)))
     W, H = 1920, 1080
     view, proj = camera.headless(bb, W, H)
-    s = _splatter(g, view, proj, W, H, 16)
+    s = _splatter(g, view, proj, W, H, 16, profile=True)
     f = O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0)
     ref = O.render(g, f)
     s.execute()
     s.execute()  # with the big-list hint: lazy prefixes + continuation
-    assert s.stats()["n_big_tiles"] > 10
+    st = s.stats()
+    assert st["n_big_tiles"] > 10
+    assert st["cont_lists"] > 0
+    if op_hi <= 0.02:
+        assert st["cont_full_sorts"] > 0  # pixels that never saturate: pass 2 ran
     _check_frame(s, g, f, ref, lists=False)
     s.execute()  # the lists that continued are now sorted in full up front
     _check_frame(s, g, f, ref, lists=False)
