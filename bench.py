@@ -284,8 +284,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    enq = []
     for _ in range(a.steps):
+        te = time.perf_counter()
         one_frame()
+        enq.append(time.perf_counter() - te)
     t_enq = time.perf_counter()  # host time to enqueue the K frames
     sync_all()  # raises (on every rank) on pair overflow
     torch.cuda.synchronize()
@@ -456,6 +459,8 @@ def main():
             "ms_per_step": round(ms_per_step, 4),
             "frame_latency_ms": latency_ms,
             "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / a.steps, 4),
+            # per-frame enqueue time percentiles (a long tail = the host waited on the GPU)
+            "host_enqueue_ms_p50_p90_max": [round(1e3 * float(np.percentile(enq, q)), 4) for q in (50, 90, 100)],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

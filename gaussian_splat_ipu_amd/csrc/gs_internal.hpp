@@ -66,6 +66,7 @@ struct gs_renderer {
   // device memory
   void* d_scene = nullptr;      // 4 x float4 x n + perm, inv_perm
   bool owns_scene = true;       // false: shares another renderer's scene on this device
+  bool scene_w1 = false;        // every mean has w == 1: the projection reads mean_op (xyz + opacity)
   void* d_gauss = nullptr;      // rec (48 B) + tail, rect, crect (8 B each) + depth key (4 B) per Gaussian
   void* d_zero = nullptr;       // counters[16] + tile_count[t_cap] (memset every frame)
   void* d_tiles = nullptr;      // tile_start[t_cap+1], tile_cursor, big_tiles

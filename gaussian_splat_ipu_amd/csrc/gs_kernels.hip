@@ -296,13 +296,21 @@ __device__ __forceinline__ void sh_colour(const FrameParams& fp, const Buffers& 
 template <bool P2>
 __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i) {
   bool rendered = false;
-  const float4 mean = b.mean[i];
+  // mean_w1: the mean's w is 1 and the colour's rgb is not needed (the blend
+  // reads it from the scene): one 16-B load of xyz + opacity instead of 32 B
+  float4 mean, col = make_float4(0.f, 0.f, 0.f, 0.f), rot = col;
+  if (fp.mean_w1) {
+    const float4 mo = b.mean_op[i];
+    mean = make_float4(mo.x, mo.y, mo.z, 1.0f);
+    col.w = mo.w;
+  } else {
+    mean = b.mean[i];
+  }
   const float4 sg = b.scale_gid[i];
   // without the band cull every live Gaussian needs its colour and rotation:
   // load them with the mean (one memory round trip instead of two)
-  float4 col = make_float4(0.f, 0.f, 0.f, 0.f), rot = col;
   if (!fp.band_cull) {
-    col = b.colour[i];
+    if (!fp.mean_w1) col = b.colour[i];
     rot = b.rot[i];
   }
   // the record: 32 B per Gaussian (48 B with the colour for the readback)
@@ -358,7 +366,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       return false;
     }
     if (fp.band_cull) {
-      col = b.colour[i];
+      if (!fp.mean_w1) col = b.colour[i];
       rot = b.rot[i];
     }
     if (fp.sh_degree >= 0 && b.sh) sh_colour(fp, b, i, mean, col);
@@ -2664,6 +2672,11 @@ void launch_big_buckets(const FrameParams& fp, const Buffers& b, hipStream_t s) 
 }
 
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  launch_sort_big(fp, b, s);
+  launch_sort_tiles(fp, b, s);
+}
+
+void launch_sort_big(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n_tiles == 0) return;
   if (fp.big_separate) {
     // work items = 2048-key segments of the big lists; the passes run until a
@@ -2678,6 +2691,10 @@ void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s) {
       launch_big_buckets(fp, b, s);
     }
   }
+}
+
+void launch_sort_tiles(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (fp.n_tiles == 0) return;
   // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
 }

@@ -42,6 +42,8 @@ struct FrameParams {
   int full_record;    // also write the readback-only record tail (radius, clip z)
   int pair_cull;      // bin only the tiles the alpha box meets (crect); the
                       // reference list lengths are counted alongside
+  int mean_w1;        // every mean has w == 1: the projection reads mean_op (xyz + opacity,
+                      //   16 B) and neither the mean nor the colour (32 B)
   int rect8;          // pair_cull with <= 256 tile columns and band rows: rect and crect hold
                       //   4 B per Gaussian, 8 bits per bound (rect8_pack)
   int big_separate;   // big lists sorted by gs_sort_big_kernel (launched before the tile sort)
@@ -68,6 +70,7 @@ struct Buffers {
   const float4* rot;        // quaternion (w x y z)
   const float4* scale_gid;  // sx sy sz gid
   const float4* cull;       // band cull: mean xyz + largest log-scale (NaN: empty slot, inf: never culled)
+  const float4* mean_op;    // mean xyz + opacity (FrameParams::mean_w1: every mean's w is 1)
   // device order: record i is the input Gaussian perm[i] (3D Morton order by
   // default); the depth sort breaks ties by the input index, as the reference
   const uint32_t* perm;     // [n] device index -> input index
@@ -164,6 +167,9 @@ void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s);
+// launch_sort's two independent halves: the big lists (big_separate) and the others
+void launch_sort_big(const FrameParams& fp, const Buffers& b, hipStream_t s);
+void launch_sort_tiles(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s);
 // lazy big lists: the full sort of the lists the blend flagged + the continued blend (no-op otherwise)
 void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s);

@@ -28,7 +28,8 @@ namespace {
 // scene allocation: the 64-B records (SoA), the permutation both ways, then
 // the band cull's 16-B records (16-B aligned)
 size_t cull_offset(size_t nn) { return (nn * (64 + 8) + 15) / 16 * 16; }
-size_t scene_bytes(size_t nn) { return cull_offset(nn) + nn * 16; }
+// + the band cull's records (16 B) + mean xyz with the opacity (16 B)
+size_t scene_bytes(size_t nn) { return cull_offset(nn) + nn * 32; }
 }  // namespace
 
 namespace gsr {
@@ -226,6 +227,8 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   }
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
+  fp.mean_w1 = r->scene_w1 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) fp.mean_w1 = fp.mean_w1 && std::atoi(ev) != 0;  // (A/B)
   // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
   fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256) ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_RECT8")) fp.rect8 = fp.rect8 && std::atoi(ev) != 0;  // (A/B)
@@ -673,6 +676,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     r->perm = share->perm;
     r->d_scene = share->d_scene;
     r->owns_scene = false;
+    r->scene_w1 = share->scene_w1;
   } else {
     r->perm = morton_order(g, n, (cfg->flags & GS_FLAG_INPUT_ORDER) != 0);
     if ((e = hipMalloc(&r->d_scene, scene_bytes(nn))) != hipSuccess)
@@ -684,6 +688,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         return fail(hip_fail(e, "hipHostMalloc(scene staging)"));
       std::memset(soa, 0, scene_bytes(nn));
       uint32_t* pi = (uint32_t*)(soa + nn * 16);
+      bool w1 = true;
       for (size_t i = 0; i < n; ++i) {
         const uint32_t o = r->perm[i];
         const float* s = reinterpret_cast<const float*>(&g[o]);
@@ -706,7 +711,15 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         cr[3] = (s[15] <= 0.0f) ? std::numeric_limits<float>::quiet_NaN()
                 : (s[3] != 1.0f ? std::numeric_limits<float>::infinity()
                                 : std::fmax(std::fmax(s[12], s[13]), s[14]));
+        // the projection's 16-B read when every w is 1 (clip = mvp (xyz, 1))
+        float* mo = soa + cull_offset(nn) / 4 + 4 * nn + 4 * i;
+        mo[0] = s[0];
+        mo[1] = s[1];
+        mo[2] = s[2];
+        mo[3] = s[7];  // opacity
+        w1 = w1 && s[3] == 1.0f;
       }
+      r->scene_w1 = w1;
       e = hipMemcpy(r->d_scene, soa, scene_bytes(nn), hipMemcpyHostToDevice);
       (void)hipHostFree(soa);
       if (e != hipSuccess) return fail(hip_fail(e, "hipMemcpy(scene)"));
@@ -719,6 +732,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.scale_gid = sc + 3 * nn;
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
   r->buf.cull = (const float4*)((const char*)r->d_scene + cull_offset(nn));
+  r->buf.mean_op = r->buf.cull + nn;
   r->buf.inv_perm = r->buf.perm + nn;
 
   // per Gaussian: 48 B of record (frames: the 32-B record the blend reads and,
@@ -1062,6 +1076,7 @@ int read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     fp.bin_global = 0;  // (no tile_count atomics)
     fp.full_record = 1;
     fp.rect8 = 0;  // (the readback takes the 16-bit reference rectangle)
+    fp.mean_w1 = 0;  // (and the 48-B record with the colour)
     gsk::launch_project(fp, r->buf, r->stream);
     GS_HIP(hipGetLastError());
     GS_HIP(hipStreamSynchronize(r->stream));
