@@ -2329,10 +2329,9 @@ __device__ __forceinline__ void blend_count_store(const FrameParams& fp, const B
   }
 }
 
+// wid = the wave's (tile slot, 8x8 block) item; wave = its LDS staging slot
 template <int BQW, bool HWEXP>
-__device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers& b, int blk) {
-  const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wid = blk * GS_BLEND_WPG + wave;
+__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wave, int wid) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
   if (slot >= fp.n_tiles) return;
@@ -2591,6 +2590,12 @@ __device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers&
 }
 
 // HWEXP: GS_FLAG_FAST_EXP (its own kernel: the default path's code is unchanged)
+template <int BQW, bool HWEXP>
+__device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers& b, int blk) {
+  const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  blend_wave<BQW, HWEXP>(fp, b, wave, blk * GS_BLEND_WPG + wave);
+}
+
 template <int BQW, bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
   blend_body<BQW, HWEXP>(fp, b, blockIdx.x);

@@ -11,7 +11,7 @@ for w in ${WORKLOADS:-c3 c5}; do
     c3) EXTRA=""; BSTEPS=600 ;;
     c5) EXTRA="--config5"; BSTEPS=240 ;;
   esac
-  NAME=$w BENCH_ARGS="--inflight 1 $EXTRA" PASSES="stats fetch write sq1" STEPS=20 bash tools/profile.sh > gpurun_out/profile_$w.log 2>&1
+  NAME=$w BENCH_ARGS="--inflight 1 $EXTRA" PASSES="${PASSES:-stats fetch write sq1}" STEPS=20 bash tools/profile.sh > gpurun_out/profile_$w.log 2>&1
   python3 tools/pmc_summary.py gpurun_out/prof_$w --json gpurun_out/pmc_$w.json > gpurun_out/pmc_summary_$w.txt
   timeout -k 10 600 python3 bench.py $EXTRA --steps $BSTEPS --pmc-json gpurun_out/pmc_$w.json > gpurun_out/bench_$w.json.log 2>&1
   grep '"metric"' gpurun_out/bench_$w.json.log | cut -c1-300

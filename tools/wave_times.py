@@ -33,11 +33,16 @@ print("end time us at fraction 0.5/0.9/0.99/1.0:", [ends[int(f * (ends.size - 1)
 starts = np.sort(t0.ravel()) / 100.0
 print("start time us at fraction 0.25/0.5/0.9/1.0:", [starts[int(f * (starts.size - 1))] for f in (0.25, 0.5, 0.9, 1.0)])
 np.save("gpurun_out/wave_times.npy", np.stack([t0, t1]))
+tt = np.arange(0, t1.max() / 100.0 + 1, 2.0)
+print("live waves over time (2 us steps):", [int(((t0 / 100.0 <= t) & (t1 / 100.0 > t)).sum()) for t in tt])
+print("mean live waves over the span:", ((t1 - t0).sum() / 100.0) / (t1.max() / 100.0))
 # duration map, coarse
 dm = (d / 1000.0)
 
 nb = blk[..., 2].astype(np.int64)
 it = blk[..., 3].astype(np.int64)
+if not it.any():
+    raise SystemExit(0)
 mi, su = it & 0xFFF, it >> 12
 print("batches per wave pctl 50/90/max", np.percentile(nb, [50, 90, 100]))
 print("max-lane iterations per wave pctl 50/90/max", np.percentile(mi, [50, 90, 100]), "total", mi.sum())
