@@ -95,12 +95,11 @@ STAGE_KERNELS = {
     "project": ["gs_project"],
     "scan": ["gs_count", "gs_colscan", "gs_scan_multi", "gs_scan"],
     "emit": ["gs_emit_chunk", "gs_emit"],
-    "sort": ["gs_sort_tiles", "gs_big_prefix", "gs_big_split", "gs_big_count", "gs_big_bscan",
-             "gs_big_scatter", "gs_big_bsort"],
+    "sort": ["gs_sort_tiles", "gs_big_prefix", "gs_big_split", "gs_big_select", "gs_big_psort"],
     "blend": ["gs_blend"],
-    # lazy big lists (config 5): the full sort of the flagged lists + the
-    # continued blend; its PMC counters are the continued blend's
-    "blend_cont": ["gs_blend_cont"],
+    # lazy big lists (config 5): the windows of the flagged lists sorted, the
+    # continued blend (PMC: its per-launch average over the frame's two launches)
+    "blend_cont": ["gs_big_cont", "gs_blend_cont"],
 }
 
 
@@ -129,22 +128,51 @@ def measured_copy_peak(torch, min_s: float = 0.06) -> float:
     return round(2 * n / best / 1e9, 1)
 
 
-def alg_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int) -> float:
-    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md §4).
-    P = the pairs actually binned and sorted (the reference rectangle's pairs
-    minus those the alpha box culls); T = tiles; px = pixels written; rec =
-    the tile-list records the blend staged (gs_frame_stats.blend_records: a
-    wave stops when its pixels have saturated, and lazy big lists stage only
-    their sorted prefixes), rec_cont = the records the continuation staged."""
+def alg_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int, st: dict,
+              n_chunks: int, rect_b: int, share: float = 1.0, band: bool = False) -> float:
+    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md §4):
+    the bytes each stage must move, per the layouts of DESIGN §3.
+    P = the pairs binned and sorted (the reference rectangle's pairs minus
+    those the alpha box culls); T = tiles; px = pixels written; rec = the
+    tile-list records the blend staged (gs_frame_stats.blend_records: a wave
+    stops when its pixels have saturated; lazy big lists stage only their
+    sorted prefixes); rec_cont = the records the continuation staged;
+    st = the frame stats (big-list pairs, prefix / window keys); rect_b = the
+    bytes of a Gaussian's two rectangles (8 with 8-bit bounds, else 16);
+    share / band = a row band's share of the frame's pairs (the group)."""
+    rendered = st["n_rendered"] * share
+    big = st["big_pairs"]
+    pre, win = st["big_prefix_keys"], st["big_window_keys"]
+    if band:  # band cull: every Gaussian's 16-B cull record, the band's Gaussians in full
+        project = n * 16 + rendered * (48 + 4 + 32) + n * rect_b
+    else:  # mean + opacity, scales + gid, rotation (48 B); rectangles, depth key; the binned records
+        project = n * (48 + rect_b + 4) + rendered * 32
+    chunk_matrix = n_chunks * T * 4
+    if pre or win:  # lazy big lists: the select reads every big-list key once,
+        # writes the prefixes and windows, and the prefixes are sorted into the lists
+        big_sort = big * 8 + (pre + win) * 8 + pre * 12
+    else:  # the sample sort over every big-list key
+        big_sort = big * (8 + 8 + 16 + 12)
     return {
-        "project": n * (56 + 52),
-        "scan": n * 16 + T * 12,  # count reads each Gaussian's two rectangles; tile starts
-        "emit": n * 12 + P * 12,
-        "sort": P * 24,
+        "project": project,
+        # count: both rectangles; count writes the chunk matrix, colscan reads
+        # and rewrites it; tile starts, queues and counters
+        "scan": n * rect_b + 3 * chunk_matrix + T * 12,
+        # emit: the binned rectangle and depth key, its chunk row, the pairs
+        "emit": n * (rect_b // 2 + 4) + chunk_matrix + P * 8,
+        # small / medium lists: read the 8-B keys, write the 4-B list
+        "sort": (P - big) * 12 + big_sort,
         "blend": T * 8 + rec * (4 + 36) + px * (16 + 3),
-        # the continued records only (the flagged lists' full sort is not counted)
-        "blend_cont": rec_cont * (4 + 36),
+        # the continued records, and the window keys the continuation sorted
+        "blend_cont": rec_cont * (4 + 36) + st["cont_keys"] * 12,
     }[kernel]
+
+
+def bench_chunks(n: int) -> int:
+    """The renderer's binning chunk count for a whole frame (gs_renderer.hip:
+    chunks of max(4096, n / 256) Gaussians, at most 65 535)."""
+    cs = min(65535, max(4096, -(-n // 256)))
+    return -(-n // cs)
 
 
 def core_map():
@@ -354,6 +382,9 @@ def main():
         px = (min(H, b1 * TW) - b0 * TW) * W
     else:
         T_b, P_b, px = st_view["n_tiles"], st_view["n_pairs_binned"], st_view["band_rows"] * W
+    # two rectangles per Gaussian, 8-bit bounds when the grid has <= 256 tile
+    # columns and band rows (FrameParams::rect8)
+    rect_b = 8 if (fb.tiles_across <= 256 and fb.tiles_down <= 256) else 16
     rec, rec_cont = st_view["blend_records"], st_view["blend_cont_records"]
     kern = {}
     for name, (avg_ms, cnt) in kt.items():
@@ -365,7 +396,8 @@ def main():
             continue
         if name == "blend_cont" and (not cnt or not rec_cont):
             continue  # (no lazy continuation ran: its stage is two back-to-back events)
-        b = alg_bytes(name, T_b, P_b, a.n, px, rec, rec_cont)
+        b = alg_bytes(name, T_b, P_b, a.n, px, rec, rec_cont, st_view,
+                      0 if group else bench_chunks(a.n), rect_b, share if group else 1.0, group)
         kern[name] = {
             "avg_ms": round(avg_ms, 5),
             "launches": int(cnt),

@@ -120,6 +120,9 @@ class FrameStats(C.Structure):
         ("cont_max", C.c_uint32),
         ("prefix_overflows", C.c_uint32),
         ("cont_full_sorts", C.c_uint32),
+        ("big_pairs", C.c_uint64),
+        ("big_prefix_keys", C.c_uint64),
+        ("big_window_keys", C.c_uint64),
     ]
 
     def as_dict(self):

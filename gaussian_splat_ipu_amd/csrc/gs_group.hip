@@ -862,6 +862,9 @@ int get_stats(Group* g, gs_frame_stats* st) {
   st->cont_max = g->mem[0].slot[0]->stats.cont_max;
   st->prefix_overflows = g->mem[0].slot[0]->stats.prefix_overflows;
   st->cont_full_sorts = g->mem[0].slot[0]->stats.cont_full_sorts;
+  st->big_pairs = g->mem[0].slot[0]->stats.big_pairs;
+  st->big_prefix_keys = g->mem[0].slot[0]->stats.big_prefix_keys;
+  st->big_window_keys = g->mem[0].slot[0]->stats.big_window_keys;
   uint64_t cap = ~0ull;
   for (Member& m : g->mem)
     for (gs_renderer* c : m.slot) cap = std::min<uint64_t>(cap, c->pair_cap);

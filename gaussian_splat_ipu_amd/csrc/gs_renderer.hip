@@ -465,6 +465,7 @@ int finish_frame(gs_renderer* r) {
   r->stats.n_big_tiles = c[0];
   r->stats.blend_records = r->stats.blend_cont_records = r->stats.cont_keys = 0;
   r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = r->stats.cont_full_sorts = 0;
+  r->stats.big_pairs = r->stats.big_prefix_keys = r->stats.big_window_keys = 0;
   if (r->last_counted && r->bcount_words) {
     // profiled frame: the list records the blend read.  The waves of a tile
     // each stage a prefix of the same list (the tile's records come from HBM
@@ -484,13 +485,26 @@ int finish_frame(gs_renderer* r) {
       // (the continuation ran the waves of the c[0] big lists only)
       if (r->last_fp.lazy && t < (size_t)c[0] * cpt) r->stats.blend_cont_records += m1;
     }
+    if (c[0] > 0 && r->n_tiles > 0) {
+      // the big lists' binned pairs (bench.py's sort bytes)
+      std::vector<uint32_t> ts((size_t)r->n_tiles + 1), bt(c[0]);
+      GS_HIP(hipMemcpy(ts.data(), r->buf.tile_start, ts.size() * 4, hipMemcpyDeviceToHost));
+      GS_HIP(hipMemcpy(bt.data(), r->buf.big_tiles, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
+      for (uint32_t j = 0; j < c[0]; ++j)
+        if (bt[j] < (uint32_t)r->n_tiles) r->stats.big_pairs += ts[bt[j] + 1] - ts[bt[j]];
+    }
     if (r->last_fp.lazy && c[0] > 0) {
       // the continuation's lists and their filtered key counts
-      std::vector<uint32_t> fl(c[0]), cl(c[0]), bl(c[0]), f2(c[0]);
+      std::vector<uint32_t> fl(c[0]), cl(c[0]), bl(c[0]), f2(c[0]), w2(c[0]);
+      GS_HIP(hipMemcpy(w2.data(), r->buf.big_cnt2, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       GS_HIP(hipMemcpy(fl.data(), r->buf.big_flag, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       GS_HIP(hipMemcpy(f2.data(), r->buf.big_flag2, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       GS_HIP(hipMemcpy(cl.data(), r->buf.cont_len, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       GS_HIP(hipMemcpy(bl.data(), r->buf.big_len, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
+      for (uint32_t j = 0; j < c[0]; ++j) {
+        r->stats.big_prefix_keys += bl[j];
+        r->stats.big_window_keys += w2[j];
+      }
       for (uint32_t j = 0; j < c[0]; ++j)
         if (fl[j]) {
           r->stats.prefix_overflows += bl[j] == 0u ? 1u : 0u;

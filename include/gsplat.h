@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 8
+#define GSPLAT_ABI_VERSION 9
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -188,6 +188,12 @@ typedef struct gs_frame_stats {
   uint32_t cont_full_sorts; /* of the continued lists, those whose live pixels
                              outlived the sorted window past the prefix (the
                              full sample sort of the rest ran for them)   */
+  uint64_t big_pairs;     /* ABI 9, profiled frames: binned pairs in the big
+                             lists (> 2048 keys; bench.py's sort bytes)    */
+  uint64_t big_prefix_keys; /* ABI 9, profiled lazy frames: keys the prefix
+                             select kept and sorted before the blend        */
+  uint64_t big_window_keys; /* ABI 9, profiled lazy frames: keys kept for the
+                             continuation's windows                        */
 } gs_frame_stats;
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */
