@@ -1658,7 +1658,7 @@ constexpr int kBigSeg = 2048;
 constexpr uint32_t kBktAvg = 1024, kBktMax = 2048;
 // lazy big lists: the sorted prefix holds ~this many keys (see gs_big_select_kernel);
 // the continuation's window the next ~kLazyWindow (gs_big_cont_kernel)
-constexpr uint32_t kLazyPrefix = 1536, kLazyWindow = 2560;
+constexpr uint32_t kLazyPrefix = 1024, kLazyWindow = 1536;
 __device__ __forceinline__ uint32_t big_buckets(uint32_t L) {
   return min(kBktMax, (L + kBktAvg - 1u) / kBktAvg);
 }
@@ -1771,7 +1771,7 @@ __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffe
     uint32_t s, L;
     tile_segment(fp, b, (int)b.big_tiles[j], s, L);
     const uint32_t B = big_buckets(L), bo = b.bk_off[j];
-    const uint32_t S = min((uint32_t)kSortLdsCap, min(L, (bound ? 32u : 16u) * B));  // sample size
+    const uint32_t S = min((uint32_t)kSortLdsCap, min(L, 16u * B));  // sample size
     for (uint32_t k = tid; k < S; k += 256u) {
       const uint32_t p = (uint32_t)(((2ull * k + 1ull) * L) / (2ull * S));
       keys[k] = b.pairs[s + p];

@@ -10,4 +10,4 @@ rm -rf $root && mkdir -p $root/gaussian_splat_ipu_amd
 cp -r include $root/ && cp -r gaussian_splat_ipu_amd/csrc $root/gaussian_splat_ipu_amd/ && rm -rf $root/gaussian_splat_ipu_amd/csrc/build
 (cd $root/gaussian_splat_ipu_amd/csrc && python3 "$edit")
 make -s -C $root/gaussian_splat_ipu_amd/csrc ../lib/libgsplat.so
-mkdir -p tmp_ab/$name && cp $root/gaussian_splat_ipu_amd/lib/libgsplat.so tmp_ab/$name/
+mkdir -p ${ABDIR:-tmp_ab}/$name && cp $root/gaussian_splat_ipu_amd/lib/libgsplat.so ${ABDIR:-tmp_ab}/$name/
