@@ -162,9 +162,11 @@ def alg_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: 
         "emit": n * (rect_b // 2 + 4) + chunk_matrix + P * 8,
         # small / medium lists: read the 8-B keys, write the 4-B list
         "sort": (P - big) * 12 + big_sort,
-        "blend": T * 8 + rec * (4 + 36) + px * (16 + 3),
+        # the tile's list bounds; per staged record its 4-B list entry, the
+        # 32-B record and the 16-B colour + opacity; RGBA f32 + BGR8 per pixel
+        "blend": T * 8 + rec * (4 + 32 + 16) + px * (16 + 3),
         # the continued records, and the window keys the continuation sorted
-        "blend_cont": rec_cont * (4 + 36) + st["cont_keys"] * 12,
+        "blend_cont": rec_cont * (4 + 32 + 16) + st["cont_keys"] * 12,
     }[kernel]
 
 
