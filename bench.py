@@ -11,11 +11,17 @@ Prints ONE JSON line on rank 0.  A "step" is one full frame.  The timed region
 covers K frames enqueued back to back (inputs resident in HBM), bracketed by a
 barrier + device synchronise; the value is K / max-over-ranks elapsed.
 
-N = 1: F renderers (frames in flight) take frames round-robin on their own
-streams.  N > 1: each rank is one member of a row-band group
-(gs_create_rank): it renders its band of every frame and joins that frame's
-ncclAllGather; torch.distributed (gloo, host only) carries the RCCL id, the
-barriers and the max-over-ranks reduction.
+How the N GPUs are driven (launch_mode):
+  N = 1 ("single"): F renderers (frames in flight) take frames round-robin on
+      their own streams.
+  N > 1, no launcher ("group"): ONE process drives the N devices as one
+      row-band group (gs_create with num_gpus = N: ncclCommInitAll, one host
+      thread per band enqueues its band and its ncclAllGather call).
+  N > 1 under torchrun ("ranks"): each rank is one member of the group
+      (gs_create_rank); torch.distributed (gloo, host only) carries the RCCL id,
+      the barriers and the max-over-ranks reduction.
+  --gather: the "group" path even at N = 1 (RCCL over one device).
+  --split S: S bands emulated on this one GPU (device-copy gather).
 """
 from __future__ import annotations
 
@@ -73,8 +79,8 @@ def parse():
                     "positions (N(0, 0.02) jitter, seed 8), 3840x2160, orbit camera (frame k: "
                     "mvpStart * Ry(360 k / 120)); the tile load-imbalance stress")
     ap.add_argument("--gather", action="store_true",
-                    help="N = 1 through the group path (gs_create_rank, world 1: one ncclAllGather per "
-                    "frame), to exercise the multi-GPU frame path on one GPU")
+                    help="the in-process group path (gs_create with num_gpus = --gpus: ncclCommInitAll, one "
+                    "ncclAllGather per frame) even at --gpus 1, to exercise the multi-GPU frame path on one GPU")
     ap.add_argument("--no-rebalance", action="store_true", help="group: keep the first (equal-rows) split")
     ap.add_argument("--sh", action="store_true",
                     help="opt-in view-dependent colour (gs_set_sh, SH degree 3 of the synthetic scene's f_dc / "
@@ -128,18 +134,40 @@ def measured_copy_peak(torch, min_s: float = 0.06) -> float:
     return round(2 * n / best / 1e9, 1)
 
 
-def alg_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int, st: dict,
-              n_chunks: int, rect_b: int, share: float = 1.0, band: bool = False) -> float:
-    """Algorithmic HBM bytes per launch (SURVEY §8 d, restated in DESIGN.md §4):
-    the bytes each stage must move, per the layouts of DESIGN §3.
+def survey_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int, st: dict,
+                 share: float = 1.0, band: bool = False) -> float:
+    """Algorithmic HBM bytes per launch by SURVEY §8(d)'s terms -- the
+    roofline's `achieved` (DESIGN.md §4): project N x (56 read + 52 write);
+    scan N x 8 plus the tile ranges P x 8 + T x 8; emit N x 12 + P x 12; sort
+    one pass, P x 24; blend T x 8 + P x (4 + 36) + Px x 16 with the pack's
+    Px x (16 + 3) fused in, where the blend's P is the records it staged (rec,
+    gs_frame_stats.blend_records: a wave stops when its pixels have saturated;
+    lazy big lists stage their sorted prefixes only).  P = the binned pairs;
+    share / band = a row band's share of the frame (band cull: every
+    Gaussian's 16-B cull record, the band's Gaussians in full)."""
+    rendered = st["n_rendered"] * share
+    return {
+        "project": n * 16 + rendered * 108 if band else n * 108,
+        "scan": n * 8 + P * 8 + T * 8,
+        "emit": n * 12 + P * 12,
+        "sort": P * 24,
+        "blend": T * 8 + rec * (4 + 36) + px * (16 + 3),
+        "blend_cont": rec_cont * (4 + 36) + st["cont_keys"] * 24,
+    }[kernel]
+
+
+def layout_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int, st: dict,
+                 n_chunks: int, rect_b: int, share: float = 1.0, band: bool = False) -> float:
+    """HBM bytes per launch of the layouts the kernels actually move (DESIGN
+    §3): the figure to hold against the PMC bytes of the same launch (reported
+    beside survey_bytes, labelled).
     P = the pairs binned and sorted (the reference rectangle's pairs minus
     those the alpha box culls); T = tiles; px = pixels written; rec = the
-    tile-list records the blend staged (gs_frame_stats.blend_records: a wave
-    stops when its pixels have saturated; lazy big lists stage only their
-    sorted prefixes); rec_cont = the records the continuation staged;
-    st = the frame stats (big-list pairs, prefix / window keys); rect_b = the
-    bytes of a Gaussian's two rectangles (8 with 8-bit bounds, else 16);
-    share / band = a row band's share of the frame's pairs (the group)."""
+    tile-list records the blend staged; rec_cont = the records the
+    continuation staged; st = the frame stats (big-list pairs, prefix / window
+    keys); rect_b = the bytes of a Gaussian's two rectangles (8 with 8-bit
+    bounds, else 16); share / band = a row band's share of the frame's pairs
+    (the group)."""
     rendered = st["n_rendered"] * share
     big = st["big_pairs"]
     pre, win = st["big_prefix_keys"], st["big_window_keys"]
@@ -199,6 +227,26 @@ def host_cpus():
     return len(cpus), phys
 
 
+def launch_mode(gpus: int, world_env: int, split: int = 0, gather: bool = False) -> str:
+    """How bench.py forms the frame path for --gpus N (module docstring):
+    "ranks" (one process per GPU, torchrun set WORLD_SIZE), "group" (one
+    process, N devices, ncclCommInitAll), "emulated" (--split S bands on one
+    GPU) or "single" (one GPU, independent renderers)."""
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if world_env > 1:
+        if world_env != gpus:
+            raise SystemExit(f"bench.py: launched with WORLD_SIZE={world_env} ranks but --gpus {gpus}")
+        return "ranks"
+    if split > 1:
+        if gpus > 1:
+            raise SystemExit("bench.py: --split emulates the bands on one GPU (use --gpus 1)")
+        return "emulated"
+    if gpus > 1 or gather:
+        return "group"
+    return "single"
+
+
 def frame_digest(bgr) -> str:
     return hashlib.sha1(bgr.tobytes()).hexdigest()[:16]
 
@@ -214,14 +262,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world == 1 and a.gpus > 1:
-        raise SystemExit("bench.py --gpus N>1 must be launched with torchrun / torch.distributed.run")
+    mode = launch_mode(a.gpus, world, a.split, a.gather)
+    # GPUs of the job: ranks x 1, or the devices one process drives
+    ngpu = world if mode == "ranks" else (a.gpus if mode == "group" else 1)
+    if mode == "group":
+        have = torch.cuda.device_count()  # (counts without initialising HIP)
+        if have < a.gpus:
+            raise SystemExit(f"bench.py --gpus {a.gpus}: only {have} HIP device(s) visible")
     torch.cuda.set_device(local)
     if world > 1:
         # host-side plumbing only (RCCL id, barriers, max over ranks); the
         # frame's all-gather is libgsplat's own RCCL call inside gs_render
         dist.init_process_group("gloo")
-    group = world > 1 or a.gather or a.split > 1
+    group = mode != "single"
 
     from gaussian_splat_ipu_amd import camera, scene
     from gaussian_splat_ipu_amd._lib import GsError
@@ -255,16 +308,16 @@ def main():
             r.set_sh(sh[0], sh[1], 3)
 
     # ------------------------------------------------------------ renderers
-    split = a.split if a.split > 1 else world
+    split = a.split if mode == "emulated" else ngpu
     if group:
-        if world > 1 or (a.gather and a.split <= 1):  # RCCL (--split S emulates S bands with copies)
-            if world > 1:
-                from gaussian_splat_ipu_amd import dist as gdist
+        if mode == "ranks":  # one process per GPU: ncclCommInitRank
+            from gaussian_splat_ipu_amd import dist as gdist
 
-                cid = gdist.share_comm_id(rank, comm_id_create)
-            else:
-                cid = comm_id_create()
+            cid = gdist.share_comm_id(rank, comm_id_create)
             R = [GpuSplatter(g, fb, device=local, comm_id=cid, rank=rank, world=world, frames_in_flight=F,
+                             profile=True, rebalance=not a.no_rebalance, fast_exp=a.fast_exp)]
+        elif mode == "group":  # one process, N devices: ncclCommInitAll, a host thread per band
+            R = [GpuSplatter(g, fb, num_gpus=ngpu, device_ids=list(range(ngpu)), frames_in_flight=F,
                              profile=True, rebalance=not a.no_rebalance, fast_exp=a.fast_exp)]
         else:  # --split S: S bands emulated on this GPU
             R = [GpuSplatter(g, fb, num_gpus=split, device_ids=[local] * split, frames_in_flight=F,
@@ -398,13 +451,15 @@ def main():
             continue
         if name == "blend_cont" and (not cnt or not rec_cont):
             continue  # (no lazy continuation ran: its stage is two back-to-back events)
-        b = alg_bytes(name, T_b, P_b, a.n, px, rec, rec_cont, st_view,
-                      0 if group else bench_chunks(a.n), rect_b, share if group else 1.0, group)
+        b = survey_bytes(name, T_b, P_b, a.n, px, rec, rec_cont, st_view, share if group else 1.0, group)
+        lb = layout_bytes(name, T_b, P_b, a.n, px, rec, rec_cont, st_view,
+                          0 if group else bench_chunks(a.n), rect_b, share if group else 1.0, group)
         kern[name] = {
             "avg_ms": round(avg_ms, 5),
             "launches": int(cnt),
             "alg_bytes": int(b),
             "alg_GBps": round(b / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None,
+            "layout_bytes": int(lb),
         }
     if "blend" in kern:
         kern["blend"]["records_staged"] = int(rec)
@@ -419,52 +474,85 @@ def main():
         kern["blend_cont"]["note"] = ("the flagged big lists' windows sorted, the continued blend, and the full "
                                       "sample sort of the lists that outlive their window (8 launches, a latency "
                                       "chain); alg_bytes: the continued records and the window keys sorted")
-    # the dominant kernel's stage: the longest stage whose time is its
-    # kernels' work.  The lazy continuation (blend_cont: the window sort, the
-    # continued blend and the full sort of the lists that outlive their window,
-    # eight launches, most of them no-ops) is a latency chain that overlaps the
-    # other frames in flight; its own numbers stay in kernels.blend_cont.
-    stage = {k: v for k, v in kern.items() if k not in ("gather", "blend_cont")}
+    # the dominant kernel's stage: the longest stage of the one-in-flight
+    # kernel table, every stage included.  The lazy continuation (blend_cont,
+    # config 5: the flagged big lists' window sort, the continued blend and the
+    # full sort of the lists that outlive their window) is a chain of short
+    # launches: when it is the longest, the line says it is latency-bound and
+    # carries the blend's own figure beside it.
+    stage = {k: v for k, v in kern.items() if k != "gather"}
     dom = max(stage, key=lambda k: stage[k]["avg_ms"])
     # PMC counters are per launch (kernel properties): the key names the
     # workload, the split and the band, not the frames in flight
-    pmc_key = f"{'c5' if a.config5 else 'c3'}:{a.n}@{W}x{H}/t{TW}/world{world}/split{split}/band{rank}"
+    pmc_key = f"{'c5' if a.config5 else 'c3'}:{a.n}@{W}x{H}/t{TW}/world{ngpu}/split{split}/band{rank}"
     # HBM bytes per launch of the same stage, from the committed PMC summary of
     # this exact workload (tools/profile.sh + tools/pmc_summary.py), if any
-    pmc = None
-    valu = None
+    pm = None
     if os.path.exists(a.pmc_json):
         try:
             pm = json.load(open(a.pmc_json))
+            if pm.get("config") != pmc_key:
+                pm = None
+        except Exception:
+            pm = None
+
+    def roof(name):
+        k = kern[name]
+        pmc = valu = None
+        if pm is not None:
             ks = pm.get("kernels", {})
-            names = [k for k in STAGE_KERNELS[dom] if k in ks]
-            if pm.get("config") == pmc_key and names:
-                pmc = int(sum(ks[k]["hbm_bytes_per_launch"] for k in names))
+            names = [x for x in STAGE_KERNELS[name] if x in ks]
+            if names:
+                pmc = int(sum(ks[x]["hbm_bytes_per_launch"] for x in names))
                 # VALU issue-slot fraction beside the HBM fraction (SURVEY §8 d):
                 # wave64 VALU instructions x 2 cycles over 1024 SIMDs x 2.4 GHz
-                vi = sum(ks[k].get("SQ_INSTS_VALU", 0.0) for k in names)
+                vi = sum(ks[x].get("SQ_INSTS_VALU", 0.0) for x in names)
                 if vi:
-                    valu = round(min(1.0, vi * 2.0 / (1024 * 2.4e9 * kern[dom]["avg_ms"] * 1e-3)), 3)
-        except Exception:
-            pmc = None
-    dk = kern[dom]
-    achieved = dk["alg_GBps"]
+                    valu = round(min(1.0, vi * 2.0 / (1024 * 2.4e9 * k["avg_ms"] * 1e-3)), 3)
+        ach = k["alg_GBps"]
+        return {
+            "kernel": name,
+            "achieved": ach,
+            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+            "traffic": pmc,
+            "traffic_over_alg": round(pmc / k["alg_bytes"], 3) if pmc and k["alg_bytes"] else None,
+            "alg_bytes_per_launch": k["alg_bytes"],
+            "layout_bytes_per_launch": k["layout_bytes"],
+            "layout_frac": round(k["layout_bytes"] / (k["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            if k["avg_ms"] > 0 else None,
+            "avg_launch_ms": k["avg_ms"],
+            "valu_issue_frac": valu,
+        }
+
+    rd = roof(dom)
     roofline = {
         "bound": "hbm",
         "kernel": dom,
-        "achieved": achieved,
+        "achieved": rd["achieved"],
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-        "traffic": pmc,
+        "frac": rd["frac"],
+        "traffic": rd["traffic"],
         "traffic_key": pmc_key,
-        "alg_bytes_per_launch": dk["alg_bytes"],
-        "avg_launch_ms": dk["avg_ms"],
-        "valu_issue_frac": valu,
-        "selection": "longest stage of the one-in-flight kernel table, the lazy continuation's latency chain "
-                     "(kernels.blend_cont) excluded",
+        "traffic_over_alg": rd["traffic_over_alg"],
+        "alg_bytes_per_launch": rd["alg_bytes_per_launch"],
+        "alg_bytes_model": "SURVEY §8(d) terms (bench.survey_bytes); the blend's P = the records it staged, "
+                           "40 B each (4-B list entry + 36-B 2D record), plus T x 8 and Px x (16 + 3)",
+        "layout_bytes_per_launch": rd["layout_bytes_per_launch"],
+        "layout_frac": rd["layout_frac"],
+        "layout_bytes_model": "the bytes the kernels' layouts move (bench.layout_bytes; the blend: 52 B per staged "
+                              "record = list entry + 32-B record + 16-B colour)",
+        "avg_launch_ms": rd["avg_launch_ms"],
+        "valu_issue_frac": rd["valu_issue_frac"],
+        "selection": "longest stage of the one-in-flight kernel table (every stage, the lazy continuation included)",
+        "latency_bound": dom == "blend_cont",
         "peak_measured": peak_measured,
     }
+    if dom == "blend_cont":
+        roofline["note"] = ("the longest stage is the lazy continuation, a chain of short launches (latency-bound); "
+                            "the blend's own roofline is in roofline.blend")
+    if dom != "blend" and "blend" in kern:
+        roofline["blend"] = roof("blend")
 
     # single-frame latency (one frame in flight, blocking), for reference
     lat = []
@@ -476,7 +564,35 @@ def main():
     latency_ms = round(1e3 * sorted(lat)[len(lat) // 2], 4)
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    # the group's own account of its bands (RCCL rank count, host threads,
+    # per-band HIP-event times of the kernel-table frames and their skew)
+    ginfo = None
+    if group:
+        gi = s.group_info()
+        band_ms = gi["band_ms"]
+        gather_ms = gi["gather_ms"]
+        if world > 1:  # one band per rank: collect them on every rank
+            allb = [None] * world
+            dist.all_gather_object(allb, (band_ms, gather_ms))
+            band_ms = [v for b in allb for v in b[0]]
+            gather_ms = [v for b in allb for v in b[1]]
+        mean_b = sum(band_ms) / max(1, len(band_ms))
+        ginfo = {
+            "mode": mode,
+            "world": gi["world"],
+            "rccl_comm_ranks": gi["comm_ranks"],
+            "threaded_enqueue": gi["threaded"],
+            "bounds": gi["bounds"],
+            "rebalances": gi["rebalances"],
+            "timed_frames": gi["timed_frames"],
+            "band_ms": [round(v, 5) for v in band_ms],
+            "band_skew_max_over_mean": round(max(band_ms) / mean_b, 3) if mean_b > 0 else None,
+            "gather_ms": [round(v, 5) for v in gather_ms],
+            "note": "per-band HIP events over the kernel-table frames (one in flight): band = its first kernel "
+                    "to its last; gather = band written to frame gathered (includes waiting for the slowest band)",
+        }
+
+    if rank == 0 and ngpu == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, g, view, proj, W, H, TW, np)
 
     if rank == 0:
@@ -493,12 +609,13 @@ def main():
             metric += " [GS_FLAG_FAST_EXP: RGBA within tolerance, not bit-exact]"
         if a.sh:
             metric += " [gs_set_sh: view-dependent SH-3 colour]"
-        if world > 1:
+        if mode == "ranks":
             par = f"row-band x{world}: one process per GPU, work-balanced contiguous bands, one ncclAllGather/frame"
-        elif a.split > 1:
+        elif mode == "group":
+            par = (f"row-band x{ngpu}: one process, {ngpu} devices (ncclCommInitAll, one host thread per band), "
+                   f"work-balanced contiguous bands, one ncclAllGather/frame")
+        elif mode == "emulated":
             par = f"row-band x{a.split} emulated on one GPU (copy gather)"
-        elif a.gather:
-            par = "row-band group, world 1 (ncclAllGather over one rank)"
         else:
             par = "single GPU"
         out = {
@@ -507,7 +624,7 @@ def main():
             "unit": "frames/s",
             "gaussians_per_sec": round(fps * a.n, 1),
             "pairs_per_sec": round(fps * st["n_pairs"], 1),
-            "n_gpus": world,
+            "n_gpus": ngpu,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -541,6 +658,7 @@ def main():
         }
         if group:
             out["gather_ms_per_frame"] = kern.get("gather", {}).get("avg_ms")
+            out["group"] = ginfo
         print(json.dumps(out), flush=True)
     for r in R:
         r.close()

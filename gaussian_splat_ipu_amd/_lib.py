@@ -129,6 +129,46 @@ class FrameStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class GroupInfo(C.Structure):
+    """gs_group_info (ABI 10)."""
+
+    _fields_ = [
+        ("world", C.c_uint32),
+        ("local_bands", C.c_uint32),
+        ("comm_ranks", C.c_int32),
+        ("multi_process", C.c_uint32),
+        ("threaded", C.c_uint32),
+        ("frames_in_flight", C.c_uint32),
+        ("frames", C.c_uint64),
+        ("rebalances", C.c_uint64),
+        ("timed_frames", C.c_uint64),
+        ("bounds", C.c_uint32 * (GS_MAX_GPUS + 1)),
+        ("band_rank", C.c_int32 * GS_MAX_GPUS),
+        ("device", C.c_int32 * GS_MAX_GPUS),
+        ("band_ms", C.c_double * GS_MAX_GPUS),
+        ("gather_ms", C.c_double * GS_MAX_GPUS),
+    ]
+
+    def as_dict(self):
+        k = self.local_bands
+        return {
+            "world": self.world,
+            "local_bands": k,
+            "comm_ranks": self.comm_ranks,
+            "multi_process": bool(self.multi_process),
+            "threaded": bool(self.threaded),
+            "frames_in_flight": self.frames_in_flight,
+            "frames": self.frames,
+            "rebalances": self.rebalances,
+            "timed_frames": self.timed_frames,
+            "bounds": list(self.bounds[: self.world + 1]),
+            "band_rank": list(self.band_rank[:k]),
+            "device": list(self.device[:k]),
+            "band_ms": list(self.band_ms[:k]),
+            "gather_ms": list(self.gather_ms[:k]),
+        }
+
+
 class LatticeStats(C.Structure):
     _fields_ = [
         ("frames", C.c_uint64),
@@ -176,6 +216,7 @@ _SIGS = {
     "gs_create_rank": (C.c_int, [C.POINTER(Gaussian3D), C.c_size_t, C.POINTER(Config), C.POINTER(CommId),
                                  C.c_int, C.c_int, C.POINTER(_P)]),
     "gs_group_bands": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_size_t]),
+    "gs_group_get_info": (C.c_int, [_P, C.POINTER(GroupInfo)]),
     "gs_balanced_bands": (C.c_int, [C.POINTER(C.c_double), C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
     "gs_group_decide": (C.c_int, [C.POINTER(C.c_uint32), C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_uint32),

@@ -37,10 +37,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gsplat.h"
@@ -74,6 +78,7 @@ struct Rccl {
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclCommCount) CommCount = nullptr;  // (optional: the info call only)
   std::string error;
 };
 
@@ -104,6 +109,7 @@ const Rccl& rccl() {
     sym(R.GroupStart, "ncclGroupStart");
     sym(R.GroupEnd, "ncclGroupEnd");
     sym(R.GetErrorString, "ncclGetErrorString");
+    R.CommCount = reinterpret_cast<decltype(&ncclCommCount)>(dlsym(h, "ncclCommCount"));
     if (!ok) {
       R.error = "librccl.so.1 lacks an RCCL entry point";
       R.GetUniqueId = nullptr;
@@ -133,6 +139,24 @@ struct Member {
   // set by the scan of any of this GPU's band frames that overflowed since
   // the last sync; copied into footer word kFootSticky before every gather
   uint32_t* d_sticky = nullptr;
+  // GS_FLAG_PROFILE, per slot: before the band's first kernel, after its last
+  // (both on the band renderer's stream) and after the all-gather (comm stream)
+  std::vector<hipEvent_t> ev_t0, ev_t1, ev_t2;
+  double band_ms = 0.0, gather_ms = 0.0;  // summed over timed_n frames
+  uint64_t timed_n = 0;
+  // the status of this member's part of the last frame (worker thread)
+  int rc = GS_OK;
+  std::string err;
+};
+
+// One frame's decisions, the same for every member (enqueue -> the members)
+struct FrameCmd {
+  int i = 0;             // slot
+  int pad = 0;           // padded band tile rows
+  size_t bgr_part = 0;   // bytes of the padded BGR8 band
+  size_t bytes = 0;      // bytes per rank of the all-gather
+  bool was_used = false;  // the slot held an earlier frame (its gather must be done)
+  bool timed = false;     // per-member events
 };
 
 struct SlotInfo {
@@ -164,7 +188,6 @@ struct Group {
   hipEvent_t ev_snap = nullptr;  // the snapshot's copy is done (mem[0].comm_stream)
   bool snap_pending = false;
   std::vector<uint32_t> snap_bounds;
-  std::vector<hipEvent_t> ev_g0, ev_g1;  // per slot, on mem[0].comm_stream
   uint64_t frame = 0;
   int last_slot = -1;
   bool last_read = false;
@@ -177,11 +200,26 @@ struct Group {
   std::mutex hist_mu;
   std::vector<uint32_t> hist;
   gs_frame_stats stats{};
-  // gather timing (GS_FLAG_PROFILE)
+  // gather timing (GS_FLAG_PROFILE): member 0's all-gather (GS_K_GATHER)
   uint32_t profile_every = 1;
   double g_ms = 0.0;
   uint64_t g_n = 0;
   uint64_t rebalances = 0;
+  int comm_ranks = -1;  // ncclCommCount of member 0's communicator (-1: copy gather)
+  // one process driving several devices: members 1.. enqueue their band and
+  // its all-gather on host threads of their own, beside member 0 on the
+  // caller's thread, so a frame's host time is the slowest member's, not the
+  // sum (eight bands of ~20 us of launches each would otherwise cost more host
+  // time per frame than the GPUs take to render it)
+  bool threaded = false;
+  std::vector<std::thread> workers;
+  FrameCmd cmd;                       // the posted frame
+  std::atomic<uint64_t> post_seq{0};  // frames posted
+  std::atomic<uint32_t> done{0};      // workers finished with the posted frame
+  std::atomic<int> sleepers{0};
+  std::atomic<bool> stop{false};
+  std::mutex wmu;
+  std::condition_variable wcv;
 };
 
 void balanced_bands(const double* work, int rows, int world, uint32_t* bounds) {
@@ -332,6 +370,144 @@ int copy_footers(Group* g, int i, uint32_t* h, hipStream_t s, bool async) {
   return GS_OK;
 }
 
+// Per-member event timings of the frame in slot i (GS_FLAG_PROFILE frames):
+// band = its first kernel -> its last; gather = band written -> frame
+// gathered.  block: wait for the events (else a frame still running is
+// skipped).
+int harvest_timing(Group* g, int i, bool block) {
+  SlotInfo& si = g->sinfo[i];
+  if (!si.gather_timed) return GS_OK;
+  si.gather_timed = false;
+  for (Member& m : g->mem) {
+    int rc = set_dev(m.device);
+    if (rc != GS_OK) return rc;
+    if (!block && hipEventQuery(m.ev_t2[i]) != hipSuccess) return GS_OK;
+  }
+  for (size_t k = 0; k < g->mem.size(); ++k) {
+    Member& m = g->mem[k];
+    int rc = set_dev(m.device);
+    if (rc != GS_OK) return rc;
+    float band = 0.0f, gather = 0.0f;
+    GS_HIP(hipEventSynchronize(m.ev_t2[i]));
+    GS_HIP(hipEventElapsedTime(&band, m.ev_t0[i], m.ev_t1[i]));
+    GS_HIP(hipEventElapsedTime(&gather, m.ev_t1[i], m.ev_t2[i]));
+    m.band_ms += band;
+    m.gather_ms += gather;
+    m.timed_n += 1;
+    if (k == 0) {
+      g->g_ms += gather;
+      g->g_n += 1;
+    }
+  }
+  return GS_OK;
+}
+
+// Member m's band of the frame f: moved to the frame's split, rendered on
+// its band renderer's stream into its all-gather send slot.
+int member_render(Group* g, Member& m, const FrameCmd& f) {
+  int rc = set_dev(m.device);
+  if (rc != GS_OK) return rc;
+  gs_renderer* c = m.slot[f.i];
+  if ((rc = gsr::set_band_rows(c, (int)g->bounds[m.rank], (int)g->bounds[m.rank + 1], f.pad)) != GS_OK) return rc;
+  std::memcpy(c->view_rm, g->view, sizeof(g->view));
+  std::memcpy(c->proj_rm, g->proj, sizeof(g->proj));
+  c->fov = g->fov;
+  c->scale_div = g->sd;
+  c->bgr_target = m.d_send + (size_t)f.i * g->slot_cap;
+  c->buf.footer = (uint32_t*)(c->bgr_target + f.bgr_part);
+  // the gather of frame k - F read this send slot
+  if (f.was_used) GS_HIP(hipStreamWaitEvent(c->stream, m.ev_gathered[f.i], 0));
+  if (f.timed) GS_HIP(hipEventRecord(m.ev_t0[f.i], c->stream));
+  if ((rc = gsr::enqueue_frame(c)) != GS_OK) return rc;
+  GS_HIP(hipEventRecord(m.ev_render[f.i], c->stream));
+  if (f.timed) GS_HIP(hipEventRecord(m.ev_t1[f.i], c->stream));
+  return GS_OK;
+}
+
+// Member m's side of the frame's all-gather over RCCL, on its communication
+// stream after its band: grouped = inside the caller's ncclGroupStart/End
+// (one thread drives every member), else this thread's own call on m's
+// communicator (one thread per member).
+int member_gather_rccl(Group* g, Member& m, const FrameCmd& f) {
+  int rc = set_dev(m.device);
+  if (rc != GS_OK) return rc;
+  GS_HIP(hipStreamWaitEvent(m.comm_stream, m.ev_render[f.i], 0));
+  // the GPU's sticky overflow bit into the footer: every frame up to this
+  // one has finished its render here (the gathers run in frame order)
+  gsk::launch_copy_word(m.comm_stream, (uint32_t*)(m.d_send + (size_t)f.i * g->slot_cap + f.bgr_part) +
+                                           gsk::kFootSticky, m.d_sticky);
+  GS_NCCL(rccl().AllGather(m.d_send + (size_t)f.i * g->slot_cap, m.d_recv + (size_t)f.i * g->world * g->slot_cap,
+                           f.bytes, ncclUint8, m.comm, m.comm_stream));
+  return GS_OK;
+}
+
+int member_gathered(Group* g, Member& m, const FrameCmd& f) {
+  int rc = set_dev(m.device);
+  if (rc != GS_OK) return rc;
+  GS_HIP(hipEventRecord(m.ev_gathered[f.i], m.comm_stream));
+  if (f.timed) GS_HIP(hipEventRecord(m.ev_t2[f.i], m.comm_stream));
+  return GS_OK;
+}
+
+// A worker's (or the caller's) whole part of the frame: its band and, over
+// RCCL, its own all-gather call (no group call: one thread per communicator).
+int member_frame(Group* g, Member& m, const FrameCmd& f) {
+  int rc = member_render(g, m, f);
+  if (rc != GS_OK || !g->rccl) return rc;
+  if ((rc = member_gather_rccl(g, m, f)) != GS_OK) return rc;
+  return member_gathered(g, m, f);
+}
+
+inline void cpu_relax() {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  __builtin_ia32_pause();
+#endif
+}
+
+// Worker k (k >= 1): waits for posted frames and runs member k's part of each.
+// It spins for a while after a frame (frames arrive every ~0.1 ms while a
+// pipeline runs), then sleeps on the condition variable.
+void worker_main(Group* g, int k) {
+  Member& m = g->mem[(size_t)k];
+  (void)hipSetDevice(m.device);
+  uint64_t seen = 0;
+  for (;;) {
+    uint64_t s = g->post_seq.load(std::memory_order_acquire);
+    auto t_spin = std::chrono::steady_clock::now();
+    while (s == seen && !g->stop.load(std::memory_order_acquire)) {
+      if (std::chrono::steady_clock::now() - t_spin < std::chrono::microseconds(500)) {
+        cpu_relax();
+      } else {
+        g->sleepers.fetch_add(1);
+        {
+          std::unique_lock<std::mutex> lk(g->wmu);
+          g->wcv.wait(lk, [&] { return g->post_seq.load() != seen || g->stop.load(); });
+        }
+        g->sleepers.fetch_sub(1);
+        t_spin = std::chrono::steady_clock::now();
+      }
+      s = g->post_seq.load(std::memory_order_acquire);
+    }
+    if (s == seen) return;  // stop
+    seen = s;
+    const FrameCmd f = g->cmd;
+    m.rc = member_frame(g, m, f);
+    if (m.rc != GS_OK) m.err = gsh::last_error();
+    g->done.fetch_add(1, std::memory_order_acq_rel);
+  }
+}
+
+void stop_workers(Group* g) {
+  if (g->workers.empty()) return;
+  g->stop.store(true);
+  {
+    std::lock_guard<std::mutex> lk(g->wmu);
+    g->wcv.notify_all();
+  }
+  for (std::thread& t : g->workers) t.join();
+  g->workers.clear();
+}
+
 int enqueue(Group* g) {
   const int i = (int)(g->frame % (uint64_t)g->F);
   SlotInfo& si = g->sinfo[i];
@@ -343,90 +519,78 @@ int enqueue(Group* g) {
     g->snap_pending = false;
     parse_footers(g, g->h_snap, g->snap_bounds, false, true);
   }
-  // the gather timing of the frame this slot held (profiling only)
-  if (si.gather_timed) {
-    if (hipEventQuery(g->ev_g1[i]) == hipSuccess) {
-      float ms = 0.0f;
-      GS_HIP(hipEventElapsedTime(&ms, g->ev_g0[i], g->ev_g1[i]));
-      g->g_ms += ms;
-      g->g_n += 1;
+  // the timing of the frame this slot held (profiling only)
+  if ((rc = harvest_timing(g, i, false)) != GS_OK) return rc;
+  FrameCmd f;
+  f.i = i;
+  for (int r = 0; r < g->world; ++r) f.pad = std::max(f.pad, (int)(g->bounds[r + 1] - g->bounds[r]));
+  f.bgr_part = align256((size_t)f.pad * g->th * g->W * 3);
+  f.bytes = align256(f.bgr_part + (16 + (size_t)f.pad * g->tiles_x) * 4);
+  f.was_used = si.used;
+  f.timed = g->profile && g->frame % g->profile_every == 0;
+  if (g->threaded) {
+    // members 1.. on their worker threads, member 0 here; over RCCL each
+    // member's all-gather is its own thread's call
+    g->cmd = f;
+    g->done.store(0, std::memory_order_relaxed);
+    g->post_seq.fetch_add(1);
+    if (g->sleepers.load() > 0) {
+      std::lock_guard<std::mutex> lk(g->wmu);
+      g->wcv.notify_all();
     }
-    si.gather_timed = false;
-  }
-  int pad = 0;
-  for (int r = 0; r < g->world; ++r) pad = std::max(pad, (int)(g->bounds[r + 1] - g->bounds[r]));
-  const size_t bgr_part = align256((size_t)pad * g->th * g->W * 3);
-  const size_t bytes = align256(bgr_part + (16 + (size_t)pad * g->tiles_x) * 4);
-  const bool was_used = si.used;
-  for (Member& m : g->mem) {
-    if ((rc = set_dev(m.device)) != GS_OK) return rc;
-    gs_renderer* c = m.slot[i];
-    if ((rc = gsr::set_band_rows(c, (int)g->bounds[m.rank], (int)g->bounds[m.rank + 1], pad)) != GS_OK) return rc;
-    std::memcpy(c->view_rm, g->view, sizeof(g->view));
-    std::memcpy(c->proj_rm, g->proj, sizeof(g->proj));
-    c->fov = g->fov;
-    c->scale_div = g->sd;
-    c->bgr_target = m.d_send + (size_t)i * g->slot_cap;
-    c->buf.footer = (uint32_t*)(c->bgr_target + bgr_part);
-    // the gather of frame k - F read this send slot
-    if (was_used) GS_HIP(hipStreamWaitEvent(c->stream, m.ev_gathered[i], 0));
-    if ((rc = gsr::enqueue_frame(c)) != GS_OK) return rc;
-    GS_HIP(hipEventRecord(m.ev_render[i], c->stream));
-  }
-  for (Member& m : g->mem) {
-    if ((rc = set_dev(m.device)) != GS_OK) return rc;
-    if (g->rccl) {
-      GS_HIP(hipStreamWaitEvent(m.comm_stream, m.ev_render[i], 0));
-      // the GPU's sticky overflow bit into the footer: every frame up to this
-      // one has finished its render here (the gathers run in frame order)
-      gsk::launch_copy_word(m.comm_stream, (uint32_t*)(m.d_send + (size_t)i * g->slot_cap + bgr_part) +
-                                               gsk::kFootSticky, m.d_sticky);
-    } else {  // copies read every member's band
-      for (Member& o : g->mem) GS_HIP(hipStreamWaitEvent(m.comm_stream, o.ev_render[i], 0));
-    }
-  }
-  const bool timed = g->profile && g->frame % g->profile_every == 0;
-  if (timed) {
-    if ((rc = set_dev(g->mem[0].device)) != GS_OK) return rc;
-    GS_HIP(hipEventRecord(g->ev_g0[i], g->mem[0].comm_stream));
-  }
-  if (g->rccl) {
-    const bool grouped = g->mem.size() > 1;
-    if (grouped) GS_NCCL(rccl().GroupStart());
-    for (Member& m : g->mem) {
-      if (!grouped && (rc = set_dev(m.device)) != GS_OK) return rc;
-      GS_NCCL(rccl().AllGather(m.d_send + (size_t)i * g->slot_cap, m.d_recv + (size_t)i * g->world * g->slot_cap,
-                            bytes, ncclUint8, m.comm, m.comm_stream));
-    }
-    if (grouped) GS_NCCL(rccl().GroupEnd());
+    Member& m0 = g->mem[0];
+    m0.rc = member_frame(g, m0, f);
+    if (m0.rc != GS_OK) m0.err = gsh::last_error();
+    const uint32_t want = (uint32_t)g->mem.size() - 1;
+    while (g->done.load(std::memory_order_acquire) < want) cpu_relax();
+    for (Member& m : g->mem)
+      if (m.rc != GS_OK) {
+        set_error(m.err);
+        return m.rc;
+      }
   } else {
+    for (Member& m : g->mem)
+      if ((rc = member_render(g, m, f)) != GS_OK) return rc;
+    if (g->rccl) {
+      const bool grouped = g->mem.size() > 1;
+      if (grouped) GS_NCCL(rccl().GroupStart());
+      for (Member& m : g->mem) {
+        rc = member_gather_rccl(g, m, f);
+        if (rc != GS_OK) {
+          if (grouped) (void)rccl().GroupEnd();
+          return rc;
+        }
+      }
+      if (grouped) GS_NCCL(rccl().GroupEnd());
+    }
+  }
+  if (!g->rccl) {  // copies read every member's band (emulated bands on one device)
     for (Member& m : g->mem) {
       if ((rc = set_dev(m.device)) != GS_OK) return rc;
+      for (Member& o : g->mem) GS_HIP(hipStreamWaitEvent(m.comm_stream, o.ev_render[i], 0));
       uint8_t* recv = m.d_recv + (size_t)i * g->world * g->slot_cap;
       for (const Member& o : g->mem) {
-        GS_HIP(hipMemcpyAsync(recv + (size_t)o.rank * bytes, o.d_send + (size_t)i * g->slot_cap, bytes,
+        GS_HIP(hipMemcpyAsync(recv + (size_t)o.rank * f.bytes, o.d_send + (size_t)i * g->slot_cap, f.bytes,
                               hipMemcpyDeviceToDevice, m.comm_stream));
         // o's sticky bit into its gathered footer (this stream has waited for
         // every frame of o up to this one)
-        GS_HIP(hipMemcpyAsync((uint32_t*)(recv + (size_t)o.rank * bytes + bgr_part) + gsk::kFootSticky, o.d_sticky,
-                              4, hipMemcpyDeviceToDevice, m.comm_stream));
+        GS_HIP(hipMemcpyAsync((uint32_t*)(recv + (size_t)o.rank * f.bytes + f.bgr_part) + gsk::kFootSticky,
+                              o.d_sticky, 4, hipMemcpyDeviceToDevice, m.comm_stream));
       }
     }
   }
-  for (Member& m : g->mem) {
-    if ((rc = set_dev(m.device)) != GS_OK) return rc;
-    GS_HIP(hipEventRecord(m.ev_gathered[i], m.comm_stream));
-  }
+  if (!g->threaded || !g->rccl)
+    for (Member& m : g->mem)
+      if ((rc = member_gathered(g, m, f)) != GS_OK) return rc;
   Member& m0 = g->mem[0];
   if ((rc = set_dev(m0.device)) != GS_OK) return rc;
-  if (timed) GS_HIP(hipEventRecord(g->ev_g1[i], m0.comm_stream));
   si.used = true;
-  si.gather_timed = timed;
+  si.gather_timed = f.timed;
   si.frame = g->frame;
   si.bounds = g->bounds;
-  si.pad_rows = pad;
-  si.bgr_part = bgr_part;
-  si.bytes = bytes;
+  si.pad_rows = f.pad;
+  si.bgr_part = f.bgr_part;
+  si.bytes = f.bytes;
   // the footers of this frame for the re-balancing kRebalanceEvery / 2 frames on
   if (g->rebalance && g->world > 1 && g->frame % kRebalanceEvery == kRebalanceEvery / 2) {
     if ((rc = copy_footers(g, i, g->h_snap, m0.comm_stream, true)) != GS_OK) return rc;
@@ -464,6 +628,7 @@ int ensure_capacity(Group* g) {
 }
 
 void release(Group* g) {
+  stop_workers(g);
   for (Member& m : g->mem) {
     (void)hipSetDevice(m.device);
     if (m.comm_stream) (void)hipStreamSynchronize(m.comm_stream);
@@ -475,14 +640,12 @@ void release(Group* g) {
     if (m.d_sticky) (void)hipFree(m.d_sticky);
     for (hipEvent_t e : m.ev_render)
       if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : m.ev_gathered)
-      if (e) (void)hipEventDestroy(e);
+    for (auto* v : {&m.ev_gathered, &m.ev_t0, &m.ev_t1, &m.ev_t2})
+      for (hipEvent_t e : *v)
+        if (e) (void)hipEventDestroy(e);
     if (m.comm_stream) (void)hipStreamDestroy(m.comm_stream);
   }
   if (!g->mem.empty()) (void)hipSetDevice(g->mem[0].device);
-  for (auto* v : {&g->ev_g0, &g->ev_g1})
-    for (hipEvent_t e : *v)
-      if (e) (void)hipEventDestroy(e);
   if (g->ev_snap) (void)hipEventDestroy(g->ev_snap);
   if (g->h_snap) (void)hipHostFree(g->h_snap);
   if (g->h_last) (void)hipHostFree(g->h_last);
@@ -617,16 +780,17 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
           (e = hipEventCreateWithFlags(&m.ev_gathered[s], hipEventDisableTiming)) != hipSuccess)
         return fail(gsr::hip_fail(e, "hipEventCreate"));
     }
+    if (g->profile) {  // per-member band / gather timing
+      for (auto* v : {&m.ev_t0, &m.ev_t1, &m.ev_t2}) {
+        v->assign((size_t)g->F, nullptr);
+        for (int s = 0; s < g->F; ++s)
+          if ((e = hipEventCreate(&(*v)[s])) != hipSuccess) return fail(gsr::hip_fail(e, "hipEventCreate"));
+      }
+    }
   }
   if ((rc = set_dev(g->mem[0].device)) != GS_OK) return fail(rc);
   {
     hipError_t e;
-    g->ev_g0.assign((size_t)g->F, nullptr);
-    g->ev_g1.assign((size_t)g->F, nullptr);
-    for (int s = 0; s < g->F; ++s) {
-      if ((e = hipEventCreate(&g->ev_g0[s])) != hipSuccess || (e = hipEventCreate(&g->ev_g1[s])) != hipSuccess)
-        return fail(gsr::hip_fail(e, "hipEventCreate"));
-    }
     if ((e = hipEventCreateWithFlags(&g->ev_snap, hipEventDisableTiming)) != hipSuccess)
       return fail(gsr::hip_fail(e, "hipEventCreate"));
     const size_t fb = (size_t)g->world * g->foot_words * 4;
@@ -653,6 +817,17 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
       if (nr != ncclSuccess) return fail(nccl_fail(nr, "ncclCommInitAll"));
       for (size_t k = 0; k < devs.size(); ++k) g->mem[k].comm = comms[k];
     }
+    int cnt = -1;
+    if (rccl().CommCount && rccl().CommCount(g->mem[0].comm, &cnt) == ncclSuccess) g->comm_ranks = cnt;
+  }
+  // one enqueue thread per member past the first (GSPLAT_GROUP_THREADS=0: the
+  // caller's thread enqueues every member, A/B)
+  {
+    static const bool threads_env =
+        !(std::getenv("GSPLAT_GROUP_THREADS") && std::strcmp(std::getenv("GSPLAT_GROUP_THREADS"), "0") == 0);
+    g->threaded = threads_env && g->mem.size() > 1;
+    if (g->threaded)
+      for (size_t k = 1; k < g->mem.size(); ++k) g->workers.emplace_back(worker_main, g, (int)k);
   }
 
   {
@@ -723,15 +898,9 @@ int wait_frames(Group* g) {
     if ((rc = copy_footers(g, g->last_slot, g->h_last, nullptr, false)) != GS_OK) return rc;
     g->last_status = parse_footers(g, g->h_last, g->sinfo[g->last_slot].bounds, true, false);
     g->last_read = true;
-    SlotInfo& si = g->sinfo[g->last_slot];
-    if (si.gather_timed) {
-      float ms = 0.0f;
-      GS_HIP(hipEventElapsedTime(&ms, g->ev_g0[g->last_slot], g->ev_g1[g->last_slot]));
-      g->g_ms += ms;
-      g->g_n += 1;
-      si.gather_timed = false;
-    }
   }
+  for (int i = 0; i < g->F; ++i)  // every frame is done: its timings
+    if ((rc = harvest_timing(g, i, true)) != GS_OK) return rc;
   if (g->last_status == GS_EOVERFLOW) {
     set_error("pair list overflow: a band of a frame since the last gs_sync binned more pairs than its capacity");
     return GS_EOVERFLOW;
@@ -954,6 +1123,10 @@ int reset_kernel_times(Group* g) {
   }
   g->g_ms = 0.0;
   g->g_n = 0;
+  for (Member& m : g->mem) {
+    m.band_ms = m.gather_ms = 0.0;
+    m.timed_n = 0;
+  }
   return GS_OK;
 }
 
@@ -970,9 +1143,40 @@ int set_profile_interval(Group* g, uint32_t every) {
 int set_sh(Group* g, const float* f_dc, const float* f_rest, size_t n, int degree) {
   int rc = wait_frames(g);
   if (rc != GS_OK && rc != GS_EOVERFLOW) return rc;
+  // one copy of the coefficients per device: the first band renderer on it
+  // uploads, the others (frames in flight, emulated bands) share it
+  std::vector<const gs_renderer*> first;
   for (Member& m : g->mem)
-    for (gs_renderer* c : m.slot)
-      if ((rc = gsr::set_sh(c, f_dc, f_rest, n, degree)) != GS_OK) return rc;
+    for (gs_renderer* c : m.slot) {
+      const gs_renderer* share = nullptr;
+      for (const gs_renderer* o : first)
+        if (o->device == c->device) share = o;
+      if ((rc = gsr::set_sh(c, f_dc, f_rest, n, degree, share)) != GS_OK) return rc;
+      if (!share) first.push_back(c);
+    }
+  return GS_OK;
+}
+
+int info(Group* g, gs_group_info* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->world = (uint32_t)g->world;
+  out->local_bands = (uint32_t)g->mem.size();
+  out->comm_ranks = g->rccl ? g->comm_ranks : -1;
+  out->multi_process = g->multi_process ? 1u : 0u;
+  out->threaded = g->threaded ? 1u : 0u;
+  out->frames_in_flight = (uint32_t)g->F;
+  out->frames = g->frame;
+  out->rebalances = g->rebalances;
+  const std::vector<uint32_t>& b = g->last_slot >= 0 ? g->sinfo[g->last_slot].bounds : g->bounds;
+  for (size_t k = 0; k < b.size() && k <= GS_MAX_GPUS; ++k) out->bounds[k] = b[k];
+  for (size_t k = 0; k < g->mem.size() && k < GS_MAX_GPUS; ++k) {
+    const Member& m = g->mem[k];
+    out->band_rank[k] = m.rank;
+    out->device[k] = m.device;
+    out->band_ms[k] = m.timed_n ? m.band_ms / (double)m.timed_n : 0.0;
+    out->gather_ms[k] = m.timed_n ? m.gather_ms / (double)m.timed_n : 0.0;
+  }
+  out->timed_frames = g->mem.empty() ? 0 : g->mem[0].timed_n;
   return GS_OK;
 }
 
@@ -1007,6 +1211,15 @@ extern "C" int gs_group_decide(const uint32_t* footers, size_t foot_words, uint3
   }
   return gsg::decide(footers, foot_words, (int)world, (int)tiles_x, (int)tiles_y, frame_bounds, cur_bounds,
                      rebalance != 0, true, next_bounds, need_pairs, nullptr, nullptr);
+}
+
+extern "C" int gs_group_get_info(gs_renderer* r, gs_group_info* out) {
+  if (!r || !out) return GS_EINVAL;
+  if (!r->grp) {
+    set_error("gs_group_get_info: not a row-band group");
+    return GS_EINVAL;
+  }
+  return gsg::info(r->grp, out);
 }
 
 extern "C" int gs_comm_id_create(gs_comm_id* out) {

@@ -94,6 +94,12 @@ struct gs_renderer {
   std::vector<uint32_t> hist_snapshot;
   std::mutex hist_mu;
   bool frame_pending = false;
+  // gs_set_band_rows moved the band after the last enqueued frame: that
+  // frame's readbacks are refused (its geometry is not the renderer's now)
+  bool band_moved = false;
+  // A/B hooks, read once at gs_create (GSPLAT_BLEND_LPT 0 | 1, GSPLAT_MEAN_W1,
+  // GSPLAT_RECT8: 0 turns the layout off); -1 = unset
+  int env_blend_lpt = -1, env_mean_w1 = -1, env_rect8 = -1;
   uint8_t* own_bgr = nullptr;     // the renderer's BGR8 band buffer
   uint8_t* bgr_target = nullptr;  // gs_set_bgr8_target: frames write their BGR8 here instead
   uint8_t* last_bgr = nullptr;    // where the last enqueued frame wrote its BGR8
@@ -148,7 +154,10 @@ int profile_harvest(gs_renderer* r, ProfileSlot& s);
 int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* list, size_t n_list);
 int read_projected(gs_renderer* r, float* dst, size_t n_floats);
 int read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout);
-int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree);
+// share: a renderer on the same device whose coefficients (set by the same
+// call just before) this one uses instead of uploading its own copy
+int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree,
+           const gs_renderer* share = nullptr);
 // the camera position (scene frame) of a row-major view matrix: -A^-1 t, double, rounded once
 void camera_position(const float* view_rm, float* campos);
 // the IPU tile-major layout (codelets.cpp:174-176) of a row-major RGBA f32 band
@@ -180,6 +189,7 @@ int kernel_times(Group* grp, double* avg_ms, uint64_t* launches, int n);
 int reset_kernel_times(Group* grp);
 int set_profile_interval(Group* grp, uint32_t every);
 int bands(Group* grp, uint32_t* bounds, size_t n);
+int info(Group* grp, gs_group_info* out);
 int set_sh(Group* grp, const float* f_dc, const float* f_rest, size_t n, int degree);
 // the split rule (also exported as gs_balanced_bands)
 void balanced_bands(const double* work, int rows, int world, uint32_t* bounds);

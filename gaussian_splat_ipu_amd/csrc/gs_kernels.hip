@@ -2667,9 +2667,9 @@ void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   gs_emit_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
 }
 
-// the sample sort's bucket passes (every big list, or the flagged ones)
-void launch_big_buckets(const FrameParams& fp, const Buffers& b, hipStream_t s) {
-  const unsigned grid = 4096;
+// the sample sort's bucket passes (every big list, or the flagged ones);
+// grid-stride kernels, so any grid is correct
+void launch_big_buckets(const FrameParams& fp, const Buffers& b, hipStream_t s, unsigned grid) {
   gs_big_count_kernel<<<grid, 256, 0, s>>>(fp, b);
   gs_big_bscan_kernel<<<256, 256, 0, s>>>(fp, b);
   gs_big_scatter_kernel<<<grid, 256, 0, s>>>(fp, b);
@@ -2693,7 +2693,7 @@ void launch_sort_big(const FrameParams& fp, const Buffers& b, hipStream_t s) {
       gs_big_select_kernel<<<4096, 256, 0, s>>>(fp, b);
       gs_big_psort_kernel<<<2048, 256, 0, s>>>(fp, b);
     } else {
-      launch_big_buckets(fp, b, s);
+      launch_big_buckets(fp, b, s, 4096);
     }
   }
 }
@@ -2744,16 +2744,21 @@ void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     gs_blend_cont_kernel<true><<<grid, block, 0, s>>>(f1, b);
   else
     gs_blend_cont_kernel<false><<<grid, block, 0, s>>>(f1, b);
+  // Pass 2 runs for a few lists per frame at most (config 5: ~3 of ~110
+  // continued lists) and is a no-op on most frames: its grid-stride kernels
+  // get small grids, so the no-op dispatches are short (the kernels return at
+  // once when counters[1] says no list outlived its window)
   FrameParams f2 = fp;
   f2.big_pass = 2;
   gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f2, b);
   // (the splitters of every big list were chosen by the frame's first split pass)
-  launch_big_buckets(f2, b, s);
+  launch_big_buckets(f2, b, s, 256);
   f2.blend_cont = 1;
+  const unsigned grid2 = std::min(grid, 256u);
   if (fp.fast_exp)
-    gs_blend_cont_kernel<true><<<grid, block, 0, s>>>(f2, b);
+    gs_blend_cont_kernel<true><<<grid2, block, 0, s>>>(f2, b);
   else
-    gs_blend_cont_kernel<false><<<grid, block, 0, s>>>(f2, b);
+    gs_blend_cont_kernel<false><<<grid2, block, 0, s>>>(f2, b);
 }
 
 }  // namespace gsk

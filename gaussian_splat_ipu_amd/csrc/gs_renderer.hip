@@ -208,7 +208,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
                        : fp.blend_bqw == 8 ? (int)((tw / 16) * (th / 4))
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) fp.blend_lpt = std::atoi(ev);  // (A/B)
+  if (r->env_blend_lpt >= 0) fp.blend_lpt = r->env_blend_lpt;  // (A/B)
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
@@ -227,11 +227,9 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   }
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
-  fp.mean_w1 = r->scene_w1 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) fp.mean_w1 = fp.mean_w1 && std::atoi(ev) != 0;  // (A/B)
+  fp.mean_w1 = (r->scene_w1 && r->env_mean_w1 != 0) ? 1 : 0;  // (A/B: GSPLAT_MEAN_W1=0)
   // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
-  fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256) ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_RECT8")) fp.rect8 = fp.rect8 && std::atoi(ev) != 0;  // (A/B)
+  fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256 && r->env_rect8 != 0) ? 1 : 0;
   // the big-list launch only when the last frame the device completed had
   // big lists (a hint read from the mapped counters: either choice sorts
   // every list, the other launch handles them otherwise)
@@ -293,25 +291,39 @@ void camera_position(const float* v, float* campos) {
     campos[i] = (float)(-((inv[i][0] * t[0] + inv[i][1] * t[1]) + inv[i][2] * t[2]) / det);
 }
 
-int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree) {
-  if (degree < 0) {
+int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int degree, const gs_renderer* share) {
+  int rc = select_device(r);
+  if (rc != GS_OK) return rc;
+  // a frame in flight may still read the coefficients: done before they change
+  if (r->frame_pending) GS_HIP(hipStreamSynchronize(r->stream));
+  auto drop = [&] {
     if (r->d_sh && r->owns_sh) (void)hipFree(r->d_sh);
     r->d_sh = nullptr;
+    r->owns_sh = false;
     r->buf.sh = nullptr;
     r->sh_degree = -1;
+  };
+  if (degree < 0) {
+    drop();
     return GS_OK;
   }
   if (degree > 3 || n != r->n || !f_dc || (degree > 0 && !f_rest)) {
     set_error("gs_set_sh: need degree 0..3, n equal to the scene's Gaussians, f_dc and (degree > 0) f_rest");
     return GS_EINVAL;
   }
-  int rc = select_device(r);
-  if (rc != GS_OK) return rc;
-  if (r->frame_pending) GS_HIP(hipStreamSynchronize(r->stream));
+  if (share && share != r && share->device == r->device && share->n == r->n && share->d_sh &&
+      share->sh_degree == degree && share->d_scene == r->d_scene) {
+    drop();
+    r->d_sh = share->d_sh;  // the same coefficients in the same device order
+    r->buf.sh = (const float*)r->d_sh;
+    r->sh_degree = degree;
+    return GS_OK;
+  }
   const size_t nn = std::max<size_t>(n, 1);
   const int K = (degree + 1) * (degree + 1);
-  // [16 x 3][n], device order; unused coefficients zero
-  std::vector<float> h((size_t)48 * nn, 0.0f);
+  // [K x 3][n], device order: only the planes the degree reads
+  // (sh_colour reads coefficient k < (degree + 1)^2)
+  std::vector<float> h((size_t)K * 3 * nn, 0.0f);
   for (size_t i = 0; i < n; ++i) {
     const size_t o = r->perm[i];  // device index i holds input Gaussian o
     for (int c = 0; c < 3; ++c) {
@@ -319,11 +331,9 @@ int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int
       for (int k = 1; k < K; ++k) h[(size_t)(k * 3 + c) * nn + i] = f_rest[o * 45 + (size_t)c * 15 + (k - 1)];
     }
   }
-  if (!r->d_sh || !r->owns_sh) {
-    r->d_sh = nullptr;
-    GS_HIP(hipMalloc(&r->d_sh, h.size() * 4));
-    r->owns_sh = true;
-  }
+  drop();
+  GS_HIP(hipMalloc(&r->d_sh, h.size() * 4));
+  r->owns_sh = true;
   GS_HIP(hipMemcpy(r->d_sh, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   r->buf.sh = (const float*)r->d_sh;
   r->sh_degree = degree;
@@ -394,6 +404,7 @@ int enqueue_frame(gs_renderer* r) {
   const gsk::FrameParams fp = make_params(r);
   r->last_fp = fp;
   r->have_fp = true;
+  r->band_moved = false;
   hipStream_t s = r->stream;
   // BGR8 destination of this frame (gs_set_bgr8_target)
   r->buf.bgr = r->bgr_target ? r->bgr_target : r->own_bgr;
@@ -457,9 +468,11 @@ int finish_frame(gs_renderer* r) {
   r->stats.n_rendered = c[2];
   r->stats.n_pairs = P_ref;
   r->stats.n_pairs_binned = P;
-  // the longest reference list (the binned lists can be shorter)
+  // the longest reference list (the binned lists can be shorter), over the
+  // tiles of the frame (its band, even if the band has moved since)
+  const int nt = r->have_fp ? r->last_fp.n_tiles : r->n_tiles;
   uint32_t mx = 0;
-  for (int t = 0; t < r->n_tiles; ++t) mx = std::max(mx, c[16 + t]);
+  for (int t = 0; t < nt; ++t) mx = std::max(mx, c[16 + t]);
   r->stats.max_list = mx;
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
@@ -527,7 +540,7 @@ int finish_frame(gs_renderer* r) {
   }
   {
     std::lock_guard<std::mutex> lk(r->hist_mu);
-    r->hist_snapshot.assign(r->h_counters + 16, r->h_counters + 16 + r->n_tiles);
+    r->hist_snapshot.assign(r->h_counters + 16, r->h_counters + 16 + nt);
   }
   r->have_frame = true;
   return GS_OK;
@@ -609,6 +622,9 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->n = n;
   r->profile = (cfg->flags & GS_FLAG_PROFILE) != 0;
   r->pair_cull = (cfg->flags & GS_FLAG_NO_PAIR_CULL) == 0;
+  if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) r->env_blend_lpt = std::atoi(ev) != 0 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) r->env_mean_w1 = std::atoi(ev) != 0 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
@@ -942,7 +958,14 @@ int grow_pairs(gs_renderer* r, bool force) {
   return alloc_pairs(r, cap);
 }
 
+int refuse_moved(const gs_renderer* r, const char* what) {
+  if (!r->band_moved) return GS_OK;
+  set_error(std::string(what) + ": the band moved (gs_set_band_rows) after the last frame; render a frame first");
+  return GS_EINVAL;
+}
+
 int read_rgba32f(gs_renderer* r, float* dst, size_t n_floats, int layout) {
+  if (refuse_moved(r, "gs_read_rgba32f") != GS_OK) return GS_EINVAL;
   if (r->cfg.flags & GS_FLAG_NO_RGBA32F) {
     set_error("gs_read_rgba32f: renderer created with GS_FLAG_NO_RGBA32F");
     return GS_EINVAL;
@@ -996,6 +1019,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
     set_error("gs_read_bins: a lattice renderer has no converged tile lists (gs_read_lattice_slots)");
     return GS_EINVAL;
   }
+  if (refuse_moved(r, "gs_read_bins") != GS_OK) return GS_EINVAL;
   int rc = select_device(r);
   if (rc != GS_OK) return rc;
   if ((rc = finish_frame(r)) != GS_OK) return rc;
@@ -1226,12 +1250,14 @@ int gs_set_band_rows(gs_renderer* r, uint32_t row_begin, uint32_t row_end, uint3
     set_error("gs_set_band_rows: rows outside the tile grid");
     return GS_EINVAL;
   }
-  if (r->frame_pending) {  // the frame in flight keeps the rows it was enqueued with
-    const int rc = gsr::finish_frame(r);
-    if (rc != GS_OK) return rc;
-  }
+  // No wait: a frame in flight keeps the rows it was enqueued with (its
+  // parameters went with its launches), and its overflow stays in the sticky
+  // word for the next gs_sync.  Its readbacks are refused from here on (they
+  // would read it with the new band's geometry) until the next frame.
   const int pad = std::max<int>((int)(row_end - row_begin), (int)pad_rows);
-  return gsr::set_band_rows(r, (int)row_begin, (int)row_end, pad);
+  const int rc = gsr::set_band_rows(r, (int)row_begin, (int)row_end, pad);
+  if (rc == GS_OK && r->have_fp) r->band_moved = true;
+  return rc;
 }
 
 int gs_set_stream(gs_renderer* r, void* hip_stream) {
@@ -1291,6 +1317,7 @@ int gs_render(gs_renderer* r) {
 int gs_read_bgr8(gs_renderer* r, uint8_t* dst, size_t bytes) {
   if (!r || !dst) return GS_EINVAL;
   if (r->grp) return gsg::read_bgr8(r->grp, dst, bytes);
+  if (refuse_moved(r, "gs_read_bgr8") != GS_OK) return GS_EINVAL;
   const size_t need = (size_t)r->band_rows * r->cfg.width * 3;
   if (bytes < need) {
     set_error("gs_read_bgr8: destination too small");

@@ -40,6 +40,7 @@ from ._lib import (
     Config,
     FrameStats,
     Gaussian3D,
+    GroupInfo,
     LatticeStats,
     check,
     fptr,
@@ -323,6 +324,14 @@ class GpuSplatter:
         b = (C.c_uint32 * (self.world + 1))()
         check(lib().gs_group_bands(self._h, b, self.world + 1))
         return [(b[i], b[i + 1]) for i in range(self.world)]
+
+    def group_info(self) -> dict:
+        """Group: world, local bands, RCCL rank count (ncclCommCount), whether
+        one host thread per band enqueues, and each local band's average band
+        and all-gather times of the profiled frames (gs_group_get_info)."""
+        gi = GroupInfo()
+        check(lib().gs_group_get_info(self._h, C.byref(gi)), "gs_group_get_info")
+        return gi.as_dict()
 
     def kernel_times(self) -> dict:
         avg = (C.c_double * GS_K_COUNT)()

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 9
+#define GSPLAT_ABI_VERSION 10
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -256,6 +256,33 @@ int gs_create_rank(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const
 /* Group: the split of the last enqueued frame as world + 1 tile-row bounds
  * (band r = tile rows [bounds[r], bounds[r + 1])). */
 int gs_group_bands(gs_renderer* r, uint32_t* bounds, size_t n);
+/* ABI 10: what a group is and how its bands ran.  One process driving several
+ * devices (gs_create with num_gpus > 1) enqueues each member's band and its
+ * all-gather call on a host thread of its own (threaded = 1).  The per-band
+ * times are HIP events of GS_FLAG_PROFILE frames (every
+ * gs_set_profile_interval-th frame) since the last gs_reset_kernel_times:
+ * band_ms = the band's first kernel to its last (its renderer's stream),
+ * gather_ms = band written to frame gathered (its communication stream; this
+ * includes waiting for the slowest band).  A rank of a multi-process group
+ * (gs_create_rank) reports its own band only (local_bands = 1). */
+typedef struct gs_group_info {
+  uint32_t world;             /* bands of the frame (ranks)                     */
+  uint32_t local_bands;       /* bands this process renders                     */
+  int32_t comm_ranks;         /* ncclCommCount of this process's first
+                                 communicator; -1 = copy gather (no RCCL)       */
+  uint32_t multi_process;     /* 1 = gs_create_rank                             */
+  uint32_t threaded;          /* 1 = one host thread per local band             */
+  uint32_t frames_in_flight;
+  uint64_t frames;            /* frames enqueued                                */
+  uint64_t rebalances;        /* splits moved since gs_create                   */
+  uint64_t timed_frames;      /* frames behind band_ms / gather_ms             */
+  uint32_t bounds[GS_MAX_GPUS + 1]; /* split of the last enqueued frame (world + 1) */
+  int32_t band_rank[GS_MAX_GPUS];   /* local band k renders band band_rank[k]     */
+  int32_t device[GS_MAX_GPUS];      /* ... on this HIP device                     */
+  double band_ms[GS_MAX_GPUS];      /* local band k: average band time            */
+  double gather_ms[GS_MAX_GPUS];    /* local band k: average gather time          */
+} gs_group_info;
+int gs_group_get_info(gs_renderer* r, gs_group_info* out);
 /* The group's split rule (host only, no device): `world` contiguous bands of
  * nearly equal work over `rows` tile rows, every band at least one row;
  * bounds = world + 1 entries.  Deterministic, so every rank derives the same

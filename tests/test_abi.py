@@ -47,7 +47,7 @@ def test_abi_version_and_config_defaults(built):
     from gaussian_splat_ipu_amd import _lib
 
     L = _lib.lib()
-    assert L.gs_abi_version() == 9
+    assert L.gs_abi_version() == 10
     cfg = _lib.Config()
     assert L.gs_config_init(ctypes.byref(cfg)) == 0
     # tile_config.hpp:5-15 and codelets.cpp:622
@@ -95,14 +95,16 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
     src = tmp_path / "w.cpp"
     src.write_text(
         '#include "gsplat.hpp"\n'
+        "#include <cstddef>\n"
         "#include <cstdio>\n"
         "int main() {\n"
         "  gs_config c;\n"
         "  splat::gs_check(gs_config_init(&c), \"init\");\n"
         "  splat::GpuSplatter* p = nullptr;  // the class is instantiable\n"
         "  (void)p;\n"
-        "  std::printf(\"%d %u %zu %zu %zu %zu\\n\", gs_abi_version(), c.tile_width, sizeof(gs_config),\n"
-        "              sizeof(gs_frame_stats), sizeof(gs_comm_id), sizeof(gs_lattice_stats));\n"
+        "  std::printf(\"%d %u %zu %zu %zu %zu %zu %zu %zu\\n\", gs_abi_version(), c.tile_width, sizeof(gs_config),\n"
+        "              sizeof(gs_frame_stats), sizeof(gs_comm_id), sizeof(gs_lattice_stats), sizeof(gs_group_info),\n"
+        "              offsetof(gs_group_info, bounds), offsetof(gs_group_info, band_ms));\n"
         "  return 0;\n"
         "}\n"
     )
@@ -111,12 +113,15 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
                     "-L", libdir, "-lgsplat", f"-Wl,-rpath,{libdir}"], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    assert int(out[0]) == 9
+    assert int(out[0]) == 10
     # the ctypes mirrors have the C layouts
     assert int(out[2]) == ctypes.sizeof(_lib.Config)
     assert int(out[3]) == ctypes.sizeof(_lib.FrameStats)
     assert int(out[4]) == ctypes.sizeof(_lib.CommId) == 128
     assert int(out[5]) == ctypes.sizeof(_lib.LatticeStats)
+    assert int(out[6]) == ctypes.sizeof(_lib.GroupInfo)
+    assert int(out[7]) == _lib.GroupInfo.bounds.offset
+    assert int(out[8]) == _lib.GroupInfo.band_ms.offset
 
 
 def test_balanced_bands_matches_the_python_rule(built):

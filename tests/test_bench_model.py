@@ -1,8 +1,10 @@
-"""bench.py's algorithmic-byte model (SURVEY §8 d) on CPU: the
-per-stage bytes follow the layouts the kernels move, and the committed
-round-end bench lines stay within 1.1x of the PMC bytes of the same stages
-("algorithmic bytes <= PMC bytes x 1.1, or the difference is
-explained")."""
+"""bench.py's byte models (SURVEY §8 d) and launch modes on
+CPU: the roofline's algorithmic bytes are SURVEY §8(d)'s terms
+(survey_bytes), the layout bytes follow the layouts the kernels move and stay
+within 1.1x of the PMC bytes of the same stages in the committed round-end
+lines, and the committed lines' roofline is recomputable from their own
+fields."""
+import glob
 import json
 import os
 
@@ -34,7 +36,7 @@ def test_stage_bytes_from_the_layouts():
     st = _stats()
 
     def ab(k, **kw):
-        return bench.alg_bytes(k, T, P, n, px, rec, 0, st, nc, 8, **kw)
+        return bench.layout_bytes(k, T, P, n, px, rec, 0, st, nc, 8, **kw)
 
     # mean + opacity, scales + gid, rotation; two 4-B rectangles, depth key; 32-B records
     assert ab("project") == n * (48 + 8 + 4) + n * 32
@@ -49,13 +51,50 @@ def test_stage_bytes_from_the_layouts():
 def test_lazy_big_list_sort_bytes():
     n, T, P = 8_000_000, 32400, 26_000_000
     st = _stats(n_rendered=8_000_000, big_pairs=24_000_000, big_prefix_keys=1_800_000, big_window_keys=2_700_000)
-    b = bench.alg_bytes("sort", T, P, n, 3840 * 2160, 0, 0, st, 256, 8)
+    b = bench.layout_bytes("sort", T, P, n, 3840 * 2160, 0, 0, st, 256, 8)
     # small / medium lists; the select reads every big-list key once, writes the
     # prefixes and windows; the prefixes are sorted into the lists
     assert b == (P - 24_000_000) * 12 + 24_000_000 * 8 + (1_800_000 + 2_700_000) * 8 + 1_800_000 * 12
     # without lazy prefixes: the full sample sort of every big-list key
     st0 = _stats(big_pairs=24_000_000)
-    assert bench.alg_bytes("sort", T, P, n, 0, 0, 0, st0, 256, 8) == (P - 24_000_000) * 12 + 24_000_000 * 44
+    assert bench.layout_bytes("sort", T, P, n, 0, 0, 0, st0, 256, 8) == (P - 24_000_000) * 12 + 24_000_000 * 44
+
+
+def test_survey_bytes_are_section_8d_terms():
+    """SURVEY §8(d): project N x (56 + 52); scan N x 8 + ranges P x 8 + T x 8;
+    emit N x 12 + P x 12; sort P x 24 (one pass); blend T x 8 + P x (4 + 36)
+    + Px x 16 with the pack's Px x (16 + 3) fused (P = the records staged)."""
+    n, T, P, px, rec = 1_000_000, 8160, 1_990_107, 1920 * 1080, 1_334_875
+    st = _stats(cont_keys=1000)
+
+    def sb(k, **kw):
+        return bench.survey_bytes(k, T, P, n, px, rec, 77, st, **kw)
+
+    assert sb("project") == n * 108
+    assert sb("scan") == n * 8 + P * 8 + T * 8
+    assert sb("emit") == n * 12 + P * 12
+    assert sb("sort") == P * 24
+    assert sb("blend") == T * 8 + rec * 40 + px * 19
+    # the round-3 verdict's figure for config 3: 92.86 MB per blend launch
+    assert abs(sb("blend") - 92.86e6) < 0.01e6
+    assert sb("blend_cont") == 77 * 40 + 1000 * 24
+    assert sb("project", share=0.25, band=True) == n * 16 + 0.25 * n * 108
+
+
+def test_launch_modes():
+    assert bench.launch_mode(1, 1) == "single"
+    assert bench.launch_mode(1, 1, gather=True) == "group"
+    # no launcher: one process drives the N devices (ncclCommInitAll)
+    assert bench.launch_mode(8, 1) == "group"
+    assert bench.launch_mode(2, 1) == "group"
+    # torchrun: one rank per GPU
+    assert bench.launch_mode(8, 8) == "ranks"
+    assert bench.launch_mode(1, 1, split=8) == "emulated"
+    for bad in [(4, 8), (0, 1)]:
+        with pytest.raises(SystemExit):
+            bench.launch_mode(*bad)
+    with pytest.raises(SystemExit):
+        bench.launch_mode(2, 1, split=4)
 
 
 @pytest.mark.parametrize("line,pmc", [("bench_c3_pmc.json", "pmc_c3.json"), ("bench_c5.json", "pmc_c5.json")])
@@ -66,10 +105,43 @@ def test_committed_lines_within_pmc(line, pmc):
     d = json.loads(open(lp).read().strip().splitlines()[-1])
     kernels = json.load(open(pp))["kernels"]
     for stage, k in d["kernels"].items():
-        if "alg_bytes" not in k:
+        lb = k.get("layout_bytes", k.get("alg_bytes"))  # (round-3 lines: alg_bytes was the layout model)
+        if lb is None:
             continue
         names = [x for x in bench.STAGE_KERNELS.get(stage, []) if x in kernels]
         if not names:
             continue
         hbm = sum(kernels[x]["hbm_bytes_per_launch"] for x in names)
-        assert k["alg_bytes"] <= 1.1 * hbm, (stage, k["alg_bytes"], hbm)
+        assert lb <= 1.1 * hbm, (stage, lb, hbm)
+
+
+def _lines_with_survey_model():
+    out = []
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r0[4-9]*", "*.json"))):
+        try:
+            d = json.loads(open(p).read().strip().splitlines()[-1])
+        except Exception:
+            continue
+        if isinstance(d, dict) and "alg_bytes_model" in d.get("roofline", {}):
+            out.append((p, d))
+    return out
+
+
+def test_committed_lines_use_the_survey_terms():
+    """Every committed bench line of round 4 on: the blend's alg_bytes are
+    §8(d)'s T x 8 + rec x 40 + Px x 19 from the line's own fields, and the
+    roofline's frac = alg_bytes / avg launch time / 8 TB/s."""
+    lines = _lines_with_survey_model()
+    if not lines:
+        pytest.skip("no round-4 bench line committed yet")
+    for p, d in lines:
+        k = d["kernels"]["blend"]
+        W, H = d["config"]["resolution"]
+        if d["config"].get("bands") is None:
+            T = d["frame"]["n_tiles"]
+            px = W * H
+            assert k["alg_bytes"] == T * 8 + k["records_staged"] * 40 + px * 19, p
+        r = d["roofline"]
+        dk = d["kernels"][r["kernel"]]
+        assert r["alg_bytes_per_launch"] == dk["alg_bytes"], p
+        assert abs(r["frac"] - dk["alg_bytes"] / (dk["avg_ms"] * 1e-3) / 8e12) < 2e-3, p

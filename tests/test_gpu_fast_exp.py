@@ -5,21 +5,18 @@ per-pixel RGB within a stated float tolerance".  So:
 
 - tile lists, histogram and frame stats: bit-exact (the exponential is not on
   that path);
-- RGBA f32 against the oracle's exact frame: the stated tolerance below --
-  every pixel within TOL_MAX, and all but TOL_FRAC of the pixels within
-  TOL_TYPICAL (a record whose alpha sits within a few ulp of 1/255, or a pixel
-  whose transmittance lands within a few ulp of 1e-4, can take the other
-  branch of the reference's `continue` / `break`);
-- BGR8: every channel within 2 levels.
+- RGBA f32 against the oracle's exact frame: every channel of every pixel
+  within TOL_MAX = 1e-5 (measured on one MI355X: 1.9e-6 on the 1M scene, 2.9e-6
+  on point_cloud_12, DESIGN.md §5; README.md states the same contract);
+- BGR8: every channel within 1 level.
 The default (no flag) stays bit-exact; the other GPU tests check that."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-TOL_TYPICAL = 1e-4   # |d RGBA| of nearly every pixel
-TOL_FRAC = 1e-3      # share of pixels allowed past TOL_TYPICAL
-TOL_MAX = 0.1        # |d RGBA| of any pixel (a decision flip: one record's alpha * T * colour)
+TOL_MAX = 1e-5  # |d RGBA| of any channel of any pixel
+TOL_BGR8 = 1    # levels
 
 
 def _render(g, view, proj, W, H, T, fast):
@@ -37,7 +34,7 @@ def _render(g, view, proj, W, H, T, fast):
 
 def _errors(rgba, ref):
     d = np.abs(rgba.astype(np.float64) - ref.astype(np.float64)).max(axis=-1)
-    return float(d.max()), float((d > TOL_TYPICAL).mean())
+    return float(d.max()), float((d > 1e-6).mean())
 
 
 @pytest.mark.parametrize("scene_name", ["synthetic_1m", "point_cloud_12"])
@@ -60,11 +57,10 @@ def test_fast_exp_within_tolerance(built, scene_name):
     assert st["max_list"] == ref["stats"]["max_list"]
     dmax, frac = _errors(rgba, ref["rgba"])
     bdiff = np.abs(bgr.astype(np.int16) - ref["bgr"].astype(np.int16))
-    print(f"fast exp {scene_name}: max |dRGBA| {dmax:.3g}, pixels past {TOL_TYPICAL:g}: {frac:.2e}, "
+    print(f"fast exp {scene_name}: max |dRGBA| {dmax:.3g}, pixels past 1e-6: {frac:.2e}, "
           f"BGR8 max diff {int(bdiff.max())}, BGR8 channels off: {float((bdiff > 0).mean()):.2e}")
     assert dmax <= TOL_MAX
-    assert frac <= TOL_FRAC
-    assert bdiff.max() <= 2
+    assert bdiff.max() <= TOL_BGR8
     # and the default stays bit-exact on the same scene
     rgba0, bgr0, _, _ = _render(g, view, proj, W, H, T, fast=False)
     assert np.array_equal(rgba0.view(np.uint32), ref["rgba"].view(np.uint32)) or np.array_equal(

@@ -581,3 +581,35 @@ def test_set_band_rows_moves_one_renderer(pc12):
             np.testing.assert_array_equal(s.get_histogram(), hist[t0:t1].reshape(-1))
         with pytest.raises(Exception):
             s.set_band_rows(0, fb.tiles_down + 1)
+
+
+def test_set_band_rows_keeps_the_in_flight_frame(pc12):
+    """gs_set_band_rows does not wait for the frame in flight: that frame keeps
+    its rows, its pair overflow still reaches the next gs_sync (sticky), and
+    its readbacks are refused after the move (they would read it with the new
+    band's geometry) until the next frame renders."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd._lib import GsError
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    g, bb = pc12
+    W, H, TW, TH = 1920, 1080, 16, 16
+    view, proj = camera.headless(bb, W, H)
+    full, f = _frame_pair(g, view, proj, W, H, TW, TH, 1.0)
+    fb = TiledFramebuffer(W, H, TW, TH)
+    bgr = full.get_frame_buffer()
+    with GpuSplatter(g, fb, device=0, band_rows=(0, fb.tiles_down), band_cull=True, pair_capacity=1024) as s:
+        s.set_view_wire(view)
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        s.execute_async()  # overflows the 1024-pair capacity
+        s.set_band_rows(10, 30)
+        with pytest.raises(GsError) as e:
+            s.sync()
+        assert "overflow" in str(e.value).lower()
+        with pytest.raises(GsError):
+            s.get_frame_buffer()  # the frame before the move
+        s.execute()  # regrows, renders the moved band
+        np.testing.assert_array_equal(s.get_frame_buffer(), bgr[10 * TH:30 * TH])
+        assert s.stats()["pair_capacity"] > 1024

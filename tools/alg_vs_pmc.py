@@ -1,6 +1,7 @@
-"""Per-stage algorithmic bytes of a bench line against the PMC HBM bytes of
-the same stage's kernels (algorithmic bytes <= PMC bytes x 1.1,
-or the difference explained).
+"""Per-stage bytes of a bench line against the PMC HBM bytes of the same
+stage's kernels: the SURVEY §8(d) algorithmic bytes (the roofline's, bench.
+survey_bytes) and the layout bytes the kernels move (bench.layout_bytes,
+which should stay within 1.1x of the PMC bytes).
 
   python tools/alg_vs_pmc.py <bench line .json> <pmc summary .json>
 """
@@ -15,15 +16,18 @@ from bench import STAGE_KERNELS  # noqa: E402
 def main():
     line = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
     pmc = json.load(open(sys.argv[2]))["kernels"]
-    print(f"{'stage':12s} {'avg_us':>8s} {'alg MB':>9s} {'PMC MB':>9s} {'alg/PMC':>8s}")
+    print(f"{'stage':12s} {'avg_us':>8s} {'8d MB':>9s} {'layout MB':>10s} {'PMC MB':>9s} {'PMC/8d':>8s} "
+          f"{'layout/PMC':>10s}")
     for stage, k in line["kernels"].items():
         if "alg_bytes" not in k:
             continue
+        lb = k.get("layout_bytes", k["alg_bytes"])
         names = [n for n in STAGE_KERNELS.get(stage, []) if n in pmc]
         hbm = sum(pmc[n]["hbm_bytes_per_launch"] for n in names)
-        ratio = k["alg_bytes"] / hbm if hbm else float("nan")
-        print(f"{stage:12s} {1e3 * k['avg_ms']:8.1f} {k['alg_bytes'] / 1e6:9.1f} {hbm / 1e6:9.1f} {ratio:8.2f}"
-              f"  ({', '.join(names)})")
+        r8 = hbm / k["alg_bytes"] if k["alg_bytes"] else float("nan")
+        rl = lb / hbm if hbm else float("nan")
+        print(f"{stage:12s} {1e3 * k['avg_ms']:8.1f} {k['alg_bytes'] / 1e6:9.1f} {lb / 1e6:10.1f} {hbm / 1e6:9.1f} "
+              f"{r8:8.2f} {rl:10.2f}  ({', '.join(names)})")
 
 
 if __name__ == "__main__":
