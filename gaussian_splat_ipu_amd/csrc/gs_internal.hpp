@@ -84,6 +84,7 @@ struct gs_renderer {
   int bin_global = 0, chunk_size = 0, n_chunks = 0;
   size_t chunk_entries = 0;     // chunk table size (chunks x tiles)
   bool chunk_adaptive = false;  // bands: more, smaller chunks (make_params)
+  bool bin_agg = false;         // aggregated binning (gs_kernels.hip: agg_count, gs_agg_scan/emit)
   bool pair_cull = false;       // chunked binning into the alpha-box tiles only
   size_t zero_bytes = 0;
   size_t bgr_bytes = 0;

@@ -294,7 +294,8 @@ __device__ __forceinline__ void sh_colour(const FrameParams& fp, const Buffers& 
 }
 
 template <bool P2>
-__device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i) {
+__device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i, uint2& rect_out,
+                                            uint2& crect_out) {
   bool rendered = false;
   // mean_w1: the mean's w is 1 and the colour's rgb is not needed (the blend
   // reads it from the scene): one 16-B load of xyz + opacity instead of 32 B
@@ -363,6 +364,8 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       // no tile row in this band: empty rectangle; the record is never read
       store_rects(fp, b, i, rect, crect);
       b.depth_key[i] = dkey;
+      rect_out = rect;
+      crect_out = crect;
       return false;
     }
     if (fp.band_cull) {
@@ -466,13 +469,137 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   }
   store_rects(fp, b, i, rect, crect);
   b.depth_key[i] = dkey;
+  rect_out = rect;
+  crect_out = fp.pair_cull ? crect : rect;
   return rendered;
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// wave-wide min of lo and max of hi, each two packed u16 (v_pk_min / max_u16)
+__device__ __forceinline__ void wave_minmax_u16x2(uint32_t& lo, uint32_t& hi) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t ol = (uint32_t)__shfl_xor((int)lo, d, 64), oh = (uint32_t)__shfl_xor((int)hi, d, 64);
+    lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, lo), __builtin_bit_cast(u16x2, ol)));
+    hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hi), __builtin_bit_cast(u16x2, oh)));
+  }
+}
+
+// ----------------------------------------------------- aggregated binning
+// FrameParams::bin_agg: the per-tile list lengths are summed by the
+// projection's own workgroups and the pairs emitted with one returning
+// global atomic per (workgroup, tile) -- no chunk matrix, no column scan.
+// A workgroup's 256 Gaussians are neighbours (Morton device order), so their
+// rectangles fall in a small box of tiles: each workgroup histograms its
+// pairs over that box in LDS (the first lane of a run of equal rectangles
+// adds the run's length), then adds every non-zero entry to the tile's
+// 64-bit counter (binned count | reference count << 32).  A box larger than
+// kAggCap tiles (Gaussians spread far apart, rare) adds per pair instead.
+// gs_agg_scan_kernel turns the counters into tile starts and sort queues (and
+// zeroes them for the next frame); gs_agg_emit_kernel reserves each
+// (workgroup, tile) range with one returning atomic on the tile's cursor and
+// places the pairs by LDS cursors.  The pairs land in a tile's segment in an
+// order set by the atomics; the depth sort puts every list in its total
+// (z, input index) order, so the lists and the frame are unchanged.
+constexpr int kAggCap = 1024;  // LDS histogram entries per workgroup
+
+struct AggBox {
+  int x0, y0, w, area;  // area 0: nothing binned in the workgroup
+};
+
+// the workgroup's box of tiles over the non-empty rectangles r (every
+// thread of the 256-thread workgroup calls it)
+__device__ __forceinline__ AggBox agg_box(uint2 r, uint32_t* s_lo, uint32_t* s_hi) {
+  const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+  const bool ok = x0 <= x1 && y0 <= y1;
+  uint32_t lo = ok ? (x0 | (y0 << 16)) : 0xFFFFFFFFu, hi = ok ? (x1 | (y1 << 16)) : 0u;
+  wave_minmax_u16x2(lo, hi);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_lo[wave] = lo;
+    s_hi[wave] = hi;
+  }
+  __syncthreads();
+  lo = s_lo[0];
+  hi = s_hi[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) {
+    lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, lo),
+                                                                 __builtin_bit_cast(u16x2, s_lo[w])));
+    hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hi),
+                                                                 __builtin_bit_cast(u16x2, s_hi[w])));
+  }
+  AggBox bx;
+  bx.x0 = (int)(lo & 0xFFFFu);
+  bx.y0 = (int)(lo >> 16);
+  const int bx1 = (int)(hi & 0xFFFFu), by1 = (int)(hi >> 16);
+  const bool any = bx.x0 <= bx1 && bx.y0 <= by1;
+  bx.w = any ? bx1 - bx.x0 + 1 : 0;
+  bx.area = any ? bx.w * (by1 - bx.y0 + 1) : 0;
+  return bx;
+}
+
+// run of equal (r, q) rectangles in this wave: is this lane its first, and
+// the run's length
+__device__ __forceinline__ bool rect_run(uint2 r, uint2 q, uint32_t& len) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t px = (uint32_t)__shfl_up((int)r.x, 1, 64), py = (uint32_t)__shfl_up((int)r.y, 1, 64);
+  const uint32_t qx = (uint32_t)__shfl_up((int)q.x, 1, 64), qy = (uint32_t)__shfl_up((int)q.y, 1, 64);
+  const bool start = lane == 0 || r.x != px || r.y != py || q.x != qx || q.y != qy;
+  const unsigned long long st = ballot64(start);
+  const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
+  len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
+  return start;
+}
+
+// The projection workgroup's share of the per-tile counters: r = reference
+// rectangle, q = binned rectangle (q inside r) of this thread's Gaussian.
+__device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& b, uint2 r, uint2 q) {
+  __shared__ uint32_t cnt[kAggCap];
+  __shared__ uint32_t s_lo[4], s_hi[4];
+  const AggBox bx = agg_box(r, s_lo, s_hi);
+  if (bx.area == 0) return;  // (uniform)
+  uint32_t len;
+  const bool start = rect_run(r, q, len);
+  const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+  const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
+  const bool mine = start && x0 <= x1;
+  if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: per run, global adds
+    if (mine)
+      for (uint32_t y = y0; y <= y1; ++y) {
+        const bool yin = v0 <= y && y <= v1;
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const unsigned long long inc = ((unsigned long long)len << 32) | ((yin && u0 <= x && x <= u1) ? len : 0u);
+          atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x], inc);
+        }
+      }
+    return;
+  }
+  for (int k = threadIdx.x; k < bx.area; k += 256) cnt[k] = 0u;
+  __syncthreads();
+  if (mine)
+    for (uint32_t y = y0; y <= y1; ++y) {
+      const bool yin = v0 <= y && y <= v1;
+      const int row = ((int)y - bx.y0) * bx.w - bx.x0;
+      for (uint32_t x = x0; x <= x1; ++x)
+        atomicAdd(&cnt[row + (int)x], (len << 16) | ((yin && u0 <= x && x <= u1) ? len : 0u));
+    }
+  __syncthreads();
+  for (int k = threadIdx.x; k < bx.area; k += 256) {
+    const uint32_t v = cnt[k];
+    if (v) {
+      const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
+      atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x], ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
+    }
+  }
 }
 
 template <bool P2>
 __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool rendered = false;
+  uint2 rect = kEmptyRect, crect = kEmptyRect;
   if (fp.band_cull) {
     // the cheap band test first; a block of 256 Gaussians that it culls
     // entirely writes only its V (0): count and emit skip such blocks
@@ -493,11 +620,12 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
       store_rects(fp, b, i, kEmptyRect, kEmptyRect);
       b.depth_key[i] = 0xFFFFFFFFu;
     } else if (i < fp.n) {
-      rendered = project_one<P2>(fp, b, i);
+      rendered = project_one<P2>(fp, b, i, rect, crect);
     }
   } else if (i < fp.n) {
-    rendered = project_one<P2>(fp, b, i);
+    rendered = project_one<P2>(fp, b, i, rect, crect);
   }
+  if (fp.bin_agg) agg_count(fp, b, rect, crect);
   // V per workgroup (summed by the scan kernel): no single-address atomics
   const int v = __syncthreads_count(rendered);
   if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
@@ -640,6 +768,238 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
   }
 }
 
+// Aggregated binning (FrameParams::bin_agg): tile starts, the sort queues and
+// the frame counters from the projection's per-tile counters (binned |
+// reference << 32), which it resets to zero for the next frame.  One
+// workgroup of 1024 threads, rounds of 8192 tiles (8 per thread in
+// registers); the histogram (reference lengths) and the counters go straight
+// to the mapped host mirror and, in a row-band group, to the frame's footer.
+__global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffers b) {
+  // per wave of a round: pair sum, reference sum, queue counts; per wave the
+  // exclusive bases (computed by lanes 0..15 of wave 0), and the round totals
+  __shared__ unsigned long long wsum[16], wref[16], wbase[16];
+  __shared__ uint32_t wq[16], wqb[3][16], wvis[16], wmax[16];
+  __shared__ unsigned long long s_tot;
+  __shared__ uint32_t s_qt[3];
+  const int T = fp.n_tiles;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // V = the projection workgroups' counts (loads issued up front)
+  uint32_t vsum = 0;
+  {
+    const int nb = (fp.n + 255) / 256;
+    uint32_t vr[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = tid + k * 1024;
+      vr[k] = i < nb ? b.block_rendered[i] : 0u;
+    }
+    for (int i = tid + 8 * 1024; i < nb; i += 1024) vsum += b.block_rendered[i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) vsum += vr[k];
+  }
+  // (lanes 0..15 of wave 0) the running bases over the rounds
+  unsigned long long carry = 0, rcarry = 0;
+  uint32_t qcarry[3] = {0u, 0u, 0u};
+  uint32_t mx = 0;
+  for (int r0 = 0; r0 < T; r0 += 8192) {
+    const int i0 = r0 + tid * 8;
+    unsigned long long v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (i0 + j < T) ? b.tile_cnt64[i0 + j] : 0ull;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + j < T) b.tile_cnt64[i0 + j] = 0ull;  // zero for the next frame's projection
+    unsigned long long sum = 0, rsum = 0;
+    uint32_t q = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t c = (uint32_t)v[j];
+      sum += c;
+      rsum += v[j] >> 32;
+      mx = max(mx, c);
+      const int cl = sort_class(c);
+      if (i0 + j < T) q += cl == 0 ? 1u : (cl == 1 ? (1u << 10) : (1u << 20));
+    }
+    unsigned long long inc = sum;
+    uint32_t qinc = q;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long o = __shfl_up(inc, d, 64);
+      const uint32_t oq = __shfl_up(qinc, d, 64);
+      if (lane >= d) {
+        inc += o;
+        qinc += oq;
+      }
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) rsum += __shfl_xor(rsum, d, 64);
+    if (lane == 63) {
+      wsum[wave] = inc;
+      wq[wave] = qinc;
+    }
+    if (lane == 0) wref[wave] = rsum;
+    __syncthreads();
+    if (tid < 16) {  // exclusive scan over the 16 waves
+      const unsigned long long ws = wsum[tid];
+      const uint32_t wqv = wq[tid];
+      uint32_t qk[3] = {wqv & 1023u, (wqv >> 10) & 1023u, (wqv >> 20) & 1023u};
+      unsigned long long si = ws, ri = wref[tid];
+      uint32_t qi[3] = {qk[0], qk[1], qk[2]};
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) {
+        const unsigned long long o = __shfl_up(si, d, 64), orr = __shfl_up(ri, d, 64);
+        uint32_t oq[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) oq[k] = __shfl_up(qi[k], d, 64);
+        if (tid >= d) {
+          si += o;
+          ri += orr;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) qi[k] += oq[k];
+        }
+      }
+      wbase[tid] = carry + si - ws;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) wqb[k][tid] = qcarry[k] + qi[k] - qk[k];
+      const unsigned long long tot = __shfl(si, 15, 64), rtot = __shfl(ri, 15, 64);
+      uint32_t qt[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) qt[k] = __shfl(qi[k], 15, 64);
+      carry += tot;
+      rcarry += rtot;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) qcarry[k] += qt[k];
+      if (tid == 0) {
+        s_tot = carry;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s_qt[k] = qcarry[k];
+      }
+    }
+    __syncthreads();
+    unsigned long long run = wbase[wave] + inc - sum;
+    const uint32_t qx = qinc - q;  // this lane's exclusive counts in the wave
+    uint32_t sml = wqb[0][wave] + (qx & 1023u);
+    uint32_t med = wqb[1][wave] + ((qx >> 10) & 1023u);
+    uint32_t big = wqb[2][wave] + ((qx >> 20) & 1023u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = i0 + j;
+      const uint32_t c = (uint32_t)v[j];
+      if (i < T) {
+        const uint32_t st = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);
+        b.tile_start[i] = st;
+        b.tile_cursor[i] = st;  // gs_agg_emit_kernel's reservations
+        const uint32_t rf = (uint32_t)(v[j] >> 32);
+        b.host_counters[16 + i] = rf;  // the histogram (reference list lengths)
+        if (b.footer) b.footer[16 + i] = rf;
+        const int cl = sort_class(c);
+        if (cl == 0) b.small_tiles[sml++] = (uint32_t)i;
+        if (cl == 1) b.medium_tiles[med++] = (uint32_t)i;
+        if (b.tile_big) b.tile_big[i] = cl == 2 ? big : 0xFFFFFFFFu;
+        if (cl == 2) b.big_tiles[big++] = (uint32_t)i;
+      }
+      run += c;
+    }
+    __syncthreads();  // the wave tables are rewritten by the next round
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
+  if (lane == 0) {
+    wvis[wave] = vsum;
+    wmax[wave] = mx;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t vis = 0, m = 0;
+    for (int w = 0; w < 16; ++w) {
+      vis += wvis[w];
+      m = max(m, wmax[w]);
+    }
+    const unsigned long long total = T > 0 ? s_tot : 0ull;
+    b.counters[0] = T > 0 ? s_qt[2] : 0u;
+    b.counters[1] = 0;
+    b.counters[2] = vis;
+    b.counters[3] = total > fp.pair_cap ? 1u : 0u;
+    if (total > fp.pair_cap) {  // sticky until the host's sync
+      *b.host_sticky = 1u;
+      if (b.group_sticky) *b.group_sticky = 1u;
+    }
+    b.counters[4] = m;
+    b.counters[5] = (uint32_t)total;
+    b.counters[6] = (uint32_t)(total >> 32);
+    b.counters[7] = T > 0 ? s_qt[1] : 0u;
+    b.counters[8] = 0;
+    b.counters[9] = T > 0 ? s_qt[0] : 0u;
+    b.counters[10] = (uint32_t)rcarry;  // (tid 0 ran the wave scans: its rcarry is the frame's)
+    b.counters[11] = (uint32_t)(rcarry >> 32);
+    for (int k = 12; k < 16; ++k) b.counters[k] = 0;
+    b.tile_start[T] = (uint32_t)(total < 0xFFFFFFFFull ? total : 0xFFFFFFFFull);
+    for (int k = 0; k < 16; ++k) b.host_counters[k] = b.counters[k];
+    if (b.footer)
+      for (int k = 0; k < 16; ++k) b.footer[k] = b.counters[k];
+  }
+}
+
+// Aggregated binning's emit: one workgroup per projection block of 256
+// Gaussians.  Its binned pairs are counted per tile of its box in LDS (runs
+// of equal rectangles add once), each non-zero tile reserves the
+// workgroup's range with one returning atomic on the tile's cursor, and every
+// pair then takes the next slot of its tile's range from an LDS cursor.
+__global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffers b) {
+  __shared__ uint32_t cnt[kAggCap];
+  __shared__ uint32_t s_lo[4], s_hi[4];
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;
+  if (fp.band_cull && b.block_rendered[blockIdx.x] == 0u) return;  // (uniform) culled block: nothing binned
+  uint2 r = kEmptyRect;
+  uint32_t dk = 0u;
+  if (i < fp.n) {
+    r = fp.rect8 ? rect8_unpack(reinterpret_cast<const uint32_t*>(b.crect)[i]) : (fp.pair_cull ? b.crect[i] : b.rect[i]);
+    dk = b.depth_key[i];
+  }
+  const AggBox bx = agg_box(r, s_lo, s_hi);
+  if (bx.area == 0) return;  // (uniform)
+  const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+  const unsigned long long key = ((unsigned long long)dk << 32) | (uint32_t)i;
+  if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: a global cursor per pair
+    if (x0 <= x1)
+      for (uint32_t y = y0; y <= y1; ++y)
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const uint32_t pos = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], 1u);
+          if (pos < fp.pair_cap) b.pairs[pos] = key;
+        }
+    return;
+  }
+  for (int k = threadIdx.x; k < bx.area; k += 256) cnt[k] = 0u;
+  __syncthreads();
+  uint32_t len;
+  const bool start = rect_run(r, r, len);
+  if (start && x0 <= x1)
+    for (uint32_t y = y0; y <= y1; ++y) {
+      const int row = ((int)y - bx.y0) * bx.w - bx.x0;
+      for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&cnt[row + (int)x], len);
+    }
+  __syncthreads();
+  // the workgroup's range of every tile it has pairs in
+  for (int k = threadIdx.x; k < bx.area; k += 256) {
+    const uint32_t c = cnt[k];
+    if (c) {
+      const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
+      cnt[k] = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], c);
+    }
+  }
+  __syncthreads();
+  if (x0 <= x1)
+    for (uint32_t y = y0; y <= y1; ++y) {
+      const int row = ((int)y - bx.y0) * bx.w - bx.x0;
+      for (uint32_t x = x0; x <= x1; ++x) {
+        const uint32_t pos = atomicAdd(&cnt[row + (int)x], 1u);
+        if (pos < fp.pair_cap) b.pairs[pos] = key;
+      }
+    }
+}
+
 // ------------------------------------------------------------ chunked binning
 // The Gaussians are cut into chunks of fp.chunk_size; one 1024-thread
 // workgroup per chunk keeps a private histogram over all band tiles in LDS,
@@ -654,18 +1014,6 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
 // read such a block's rectangles
 __device__ __forceinline__ bool block_live(const FrameParams& fp, const Buffers& b, int i) {
   return !fp.band_cull || b.block_rendered[i >> 8] != 0u;
-}
-
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-// wave-wide min of lo and max of hi, each two packed u16 (v_pk_min / max_u16)
-__device__ __forceinline__ void wave_minmax_u16x2(uint32_t& lo, uint32_t& hi) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t ol = (uint32_t)__shfl_xor((int)lo, d, 64), oh = (uint32_t)__shfl_xor((int)hi, d, 64);
-    lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, lo), __builtin_bit_cast(u16x2, ol)));
-    hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, hi), __builtin_bit_cast(u16x2, oh)));
-  }
 }
 
 __device__ __forceinline__ void lds_zero(uint32_t* cnt, int words) {
@@ -2646,6 +2994,10 @@ hipError_t init_kernel_attributes() {
 }
 
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (fp.bin_agg) {
+    gs_agg_scan_kernel<<<1, 1024, 0, s>>>(fp, b);
+    return;
+  }
   if (!fp.bin_global && fp.n_chunks > 0 && fp.n_tiles > 0) {
     const size_t lds = fp.pair_cull ? (size_t)fp.n_tiles * 4 : bin_lds_bytes(fp.n_tiles);
     gs_count_kernel<<<fp.n_chunks, 1024, lds, s>>>(fp, b);
@@ -2658,6 +3010,10 @@ void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
+  if (fp.bin_agg) {
+    gs_agg_emit_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+    return;
+  }
   if (!fp.bin_global) {
     if (fp.n_chunks > 0 && fp.n_tiles > 0)
       gs_emit_chunk_kernel<<<fp.n_chunks, 1024,

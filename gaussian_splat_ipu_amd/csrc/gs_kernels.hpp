@@ -36,6 +36,8 @@ struct FrameParams {
   int write_rgba;
   int bgr_pitch;      // bytes per row of the BGR8 output
   int bin_global;     // 1: fallback binning with global atomics
+  int bin_agg;        // 1: aggregated binning (per-tile counters summed by the projection's
+                      //   workgroups, gs_agg_scan_kernel, gs_agg_emit_kernel): no chunk matrix
   int chunk_size;     // Gaussians per binning chunk (<= 65535)
   int n_chunks;
   int emit_wide;      // emit with one u32 LDS cursor per tile (n_tiles * 4 <= kBinLdsMax)
@@ -88,6 +90,8 @@ struct Buffers {
   uint2* crect;             // rect cut to the tiles the alpha box meets (pair_cull)
   // binning
   uint32_t* tile_count;     // [n_tiles]      (memset 0 each frame)
+  unsigned long long* tile_cnt64;  // [n_tiles] aggregated binning: binned | reference << 32 per
+                                   //   tile (zero between frames: the scan resets it)
   uint32_t* tile_start;     // [n_tiles + 1]
   uint32_t* tile_cursor;    // [n_tiles]
   unsigned long long* pairs;      // [pair_cap]  (depth_key << 32 | input index)

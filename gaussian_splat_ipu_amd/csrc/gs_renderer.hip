@@ -226,7 +226,8 @@ gsk::FrameParams make_params(const gs_renderer* r) {
     fp.n_chunks = (int)((r->n + cs - 1) / cs);
   }
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
-  fp.pair_cull = (r->pair_cull && !r->bin_global && r->n_chunks > 0 && fp.emit_wide) ? 1 : 0;
+  fp.bin_agg = r->bin_agg ? 1 : 0;
+  fp.pair_cull = (r->pair_cull && !r->bin_global && ((r->n_chunks > 0 && fp.emit_wide) || r->bin_agg)) ? 1 : 0;
   fp.mean_w1 = (r->scene_w1 && r->env_mean_w1 != 0) ? 1 : 0;  // (A/B: GSPLAT_MEAN_W1=0)
   // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
   fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256 && r->env_rect8 != 0) ? 1 : 0;
@@ -788,17 +789,21 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.counters = (uint32_t*)r->d_zero;
   r->buf.tile_count = (uint32_t*)r->d_zero + 16;
   const size_t n_agg = (T + 63) / 64;
-  if ((e = hipMalloc(&r->d_tiles, (T + 1 + 4 * T) * 4 + n_agg * 32 + 16)) != hipSuccess)
-    return fail(hip_fail(e, "hipMalloc(tiles)"));
-  poison(r->d_tiles, (T + 1 + 4 * T) * 4 + n_agg * 32 + 16, "tiles");
+  const size_t tiles_bytes = (T + 1 + 4 * T) * 4 + n_agg * 32 + 16 + T * 8 + 8;
+  if ((e = hipMalloc(&r->d_tiles, tiles_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(tiles)"));
+  poison(r->d_tiles, tiles_bytes, "tiles");
   r->buf.tile_start = (uint32_t*)r->d_tiles;
   r->buf.tile_cursor = r->buf.tile_start + T + 1;
   r->buf.big_tiles = r->buf.tile_cursor + T;
   r->buf.medium_tiles = r->buf.big_tiles + T;
   r->buf.small_tiles = r->buf.medium_tiles + T;
   r->buf.tile_agg = (uint4*)(((uintptr_t)(r->buf.small_tiles + T) + 15) & ~(uintptr_t)15);
+  // the aggregated binning's per-tile counters: zero between frames (the
+  // scan resets them)
+  r->buf.tile_cnt64 = (unsigned long long*)(((uintptr_t)(r->buf.tile_agg + 2 * n_agg) + 7) & ~(uintptr_t)7);
   if ((e = hipMemset(r->d_tiles, 0, (T + 1 + 4 * T) * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(tiles)"));
+  if ((e = hipMemset(r->buf.tile_cnt64, 0, T * 8)) != hipSuccess) return fail(hip_fail(e, "hipMemset(tile counters)"));
 
   // binning mode: chunked LDS histograms unless the band's tile grid is too
   // large for one CU's LDS (or the caller asks for the global-atomic path)
@@ -827,6 +832,10 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       // shrinks with the band instead of staying a whole-frame chunk
       r->chunk_entries = (size_t)r->n_chunks * (size_t)std::max(r->n_tiles, r->tiles_x * r->tiles_y);
       r->chunk_adaptive = fixed_cs == nullptr && max_chunks == SIZE_MAX;
+      // the aggregated binning (default; GSPLAT_BIN_AGG=0: the chunked
+      // count / column scan / emit, A/B)
+      const char* agg_env = std::getenv("GSPLAT_BIN_AGG");
+      r->bin_agg = !(agg_env && std::strcmp(agg_env, "0") == 0) && fixed_cs == nullptr;
       if ((e = hipMalloc(&r->d_chunk, r->chunk_entries * 4)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
       poison(r->d_chunk, r->chunk_entries * 4, "chunk");
@@ -1112,6 +1121,7 @@ int read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     gsk::FrameParams fp = r->last_fp;
     fp.band_cull = 0;
     fp.bin_global = 0;  // (no tile_count atomics)
+    fp.bin_agg = 0;     // (nor the aggregated binning's: this pass has no scan to reset them)
     fp.full_record = 1;
     fp.rect8 = 0;  // (the readback takes the 16-bit reference rectangle)
     fp.mean_w1 = 0;  // (and the 48-B record with the colour)
