@@ -631,6 +631,80 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
   if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
 }
 
+// GS_FLAG_BAND_CULL: one workgroup per kBandGpb blocks of 256 Gaussians.  The
+// cheap band test runs first on all of them (kBandGpb 16-B cull records per
+// thread, loaded up front); the survivors' indices are compacted into LDS in
+// device order and projected in dense passes of 256, so a block that straddles
+// the band's edge no longer runs the full projection on waves whose lanes are
+// mostly culled.  Every block keeps the one-Gaussian-per-thread kernel's
+// contract: a block with no survivor writes only its V (0) and nothing else
+// reads it; in any other block every Gaussian's rectangles and depth key are
+// written (empty for the culled ones).
+constexpr int kBandGpb = 4;
+
+template <bool P2>
+__global__ __launch_bounds__(256) void gs_project_band_kernel(FrameParams fp, Buffers b) {
+  __shared__ uint32_t s_list[kBandGpb * 256];
+  __shared__ uint32_t s_cnt[kBandGpb][4];  // survivors per (block, wave)
+  __shared__ uint32_t s_v[kBandGpb];       // rendered per block
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int base = blockIdx.x * (kBandGpb * 256);
+  bool culled[kBandGpb];
+  {
+    float4 cr[kBandGpb];
+#pragma unroll
+    for (int k = 0; k < kBandGpb; ++k) {
+      const int i = base + k * 256 + tid;
+      cr[k] = i < fp.n ? b.cull[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < kBandGpb; ++k) {
+      const int i = base + k * 256 + tid;
+      culled[k] = i >= fp.n || (!__builtin_isnan(cr[k].w) && band_culled_fast<P2>(fp, cr[k]));
+    }
+  }
+  unsigned long long live[kBandGpb];
+#pragma unroll
+  for (int k = 0; k < kBandGpb; ++k) {
+    live[k] = ballot64(!culled[k]);
+    if (lane == 0) s_cnt[k][wave] = (uint32_t)__popcll(live[k]);
+  }
+  if (tid < kBandGpb) s_v[tid] = 0u;
+  __syncthreads();
+  // survivors in device order: block k, then wave, then lane
+  uint32_t S = 0;
+  uint32_t blk_n[kBandGpb];
+#pragma unroll
+  for (int k = 0; k < kBandGpb; ++k) {
+    blk_n[k] = s_cnt[k][0] + s_cnt[k][1] + s_cnt[k][2] + s_cnt[k][3];
+    uint32_t before = S;
+    for (int w = 0; w < wave; ++w) before += s_cnt[k][w];
+    if (!culled[k]) s_list[before + (uint32_t)__popcll(live[k] & ((1ull << lane) - 1ull))] = (uint32_t)(base + k * 256 + tid);
+    S += blk_n[k];
+  }
+  // the culled Gaussians of live blocks: empty rectangles, no record
+#pragma unroll
+  for (int k = 0; k < kBandGpb; ++k) {
+    const int i = base + k * 256 + tid;
+    if (blk_n[k] != 0u && culled[k] && i < fp.n) {
+      store_rects(fp, b, i, kEmptyRect, kEmptyRect);
+      b.depth_key[i] = 0xFFFFFFFFu;
+    }
+  }
+  __syncthreads();
+  for (uint32_t p0 = 0; p0 < S; p0 += 256) {  // (uniform) dense passes over the survivors
+    uint2 rect = kEmptyRect, crect = kEmptyRect;
+    const uint32_t k = p0 + (uint32_t)tid;
+    if (k < S) {
+      const int i = (int)s_list[k];
+      if (project_one<P2>(fp, b, i, rect, crect)) atomicAdd(&s_v[(i - base) >> 8], 1u);
+    }
+    if (fp.bin_agg) agg_count(fp, b, rect, crect);
+    __syncthreads();  // (agg_count's LDS is reused by the next pass)
+  }
+  if (tid < kBandGpb && base + tid * 256 < fp.n) b.block_rendered[blockIdx.x * kBandGpb + tid] = s_v[tid];
+}
+
 // --------------------------------------------------------------------- scan
 // One workgroup of 1024 threads, rounds of 8192 tiles (8 per thread, held in
 // registers): tile_start = exclusive scan(tile_count), max list length, and
@@ -781,6 +855,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   __shared__ uint32_t wq[16], wqb[3][16], wvis[16], wmax[16];
   __shared__ unsigned long long s_tot;
   __shared__ uint32_t s_qt[3];
+  __shared__ uint32_t s_c[8192];  // a round's binned counts (striped in, blocked out)
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // V = the projection workgroups' counts (loads issued up front)
@@ -802,20 +877,42 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   uint32_t qcarry[3] = {0u, 0u, 0u};
   uint32_t mx = 0;
   for (int r0 = 0; r0 < T; r0 += 8192) {
+    // the round's counters, read striped (coalesced: lane-consecutive tiles);
+    // the histogram goes to the host mirror (and the footer) from here, the
+    // counters are zeroed for the next frame, and the binned counts are
+    // transposed through LDS so each thread scans 8 consecutive tiles
+    unsigned long long rsum = 0;
+    {
+      unsigned long long vs[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = r0 + j * 1024 + tid;
+        vs[j] = i < T ? b.tile_cnt64[i] : 0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = r0 + j * 1024 + tid;
+        const uint32_t rf = (uint32_t)(vs[j] >> 32);
+        rsum += rf;
+        s_c[j * 1024 + tid] = (uint32_t)vs[j];
+        if (i < T) {
+          b.tile_cnt64[i] = 0ull;  // zero for the next frame's projection
+          b.host_counters[16 + i] = rf;  // the histogram (reference list lengths)
+          if (b.footer) b.footer[16 + i] = rf;
+        }
+      }
+    }
+    __syncthreads();
     const int i0 = r0 + tid * 8;
-    unsigned long long v[8];
+    uint32_t v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (i0 + j < T) ? b.tile_cnt64[i0 + j] : 0ull;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (i0 + j < T) b.tile_cnt64[i0 + j] = 0ull;  // zero for the next frame's projection
-    unsigned long long sum = 0, rsum = 0;
+    for (int j = 0; j < 8; ++j) v[j] = s_c[tid * 8 + j];
+    unsigned long long sum = 0;
     uint32_t q = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint32_t c = (uint32_t)v[j];
+      const uint32_t c = v[j];
       sum += c;
-      rsum += v[j] >> 32;
       mx = max(mx, c);
       const int cl = sort_class(c);
       if (i0 + j < T) q += cl == 0 ? 1u : (cl == 1 ? (1u << 10) : (1u << 20));
@@ -881,17 +978,13 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     uint32_t sml = wqb[0][wave] + (qx & 1023u);
     uint32_t med = wqb[1][wave] + ((qx >> 10) & 1023u);
     uint32_t big = wqb[2][wave] + ((qx >> 20) & 1023u);
+    __syncthreads();  // (every thread has read its counts from s_c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = i0 + j;
-      const uint32_t c = (uint32_t)v[j];
+      const uint32_t c = v[j];
+      s_c[tid * 8 + j] = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);  // the tile start
       if (i < T) {
-        const uint32_t st = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);
-        b.tile_start[i] = st;
-        b.tile_cursor[i] = st;  // gs_agg_emit_kernel's reservations
-        const uint32_t rf = (uint32_t)(v[j] >> 32);
-        b.host_counters[16 + i] = rf;  // the histogram (reference list lengths)
-        if (b.footer) b.footer[16 + i] = rf;
         const int cl = sort_class(c);
         if (cl == 0) b.small_tiles[sml++] = (uint32_t)i;
         if (cl == 1) b.medium_tiles[med++] = (uint32_t)i;
@@ -900,7 +993,18 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       }
       run += c;
     }
-    __syncthreads();  // the wave tables are rewritten by the next round
+    __syncthreads();
+    // the tile starts back striped (coalesced stores)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = r0 + j * 1024 + tid;
+      if (i < T) {
+        const uint32_t st = s_c[j * 1024 + tid];
+        b.tile_start[i] = st;
+        b.tile_cursor[i] = st;  // gs_agg_emit_kernel's reservations
+      }
+    }
+    __syncthreads();  // the wave tables and s_c are rewritten by the next round
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
@@ -990,11 +1094,21 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
     }
   }
   __syncthreads();
+  // a run of equal rectangles takes its slots of each tile with one LDS
+  // atomic by its first lane (clustered scenes: the lanes of a wave would
+  // otherwise serialise on the same few tiles' cursors)
+  const int lane = threadIdx.x & 63;
+  const unsigned long long st = ballot64(start);
+  const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  const int lead = 63 - __builtin_clzll(st & upto);
+  const uint32_t rank = (uint32_t)(lane - lead);
   if (x0 <= x1)
     for (uint32_t y = y0; y <= y1; ++y) {
       const int row = ((int)y - bx.y0) * bx.w - bx.x0;
       for (uint32_t x = x0; x <= x1; ++x) {
-        const uint32_t pos = atomicAdd(&cnt[row + (int)x], 1u);
+        uint32_t base = 0u;
+        if (start) base = atomicAdd(&cnt[row + (int)x], len);
+        const uint32_t pos = (uint32_t)__shfl((int)base, lead, 64) + rank;
         if (pos < fp.pair_cap) b.pairs[pos] = key;
       }
     }
@@ -2975,6 +3089,14 @@ void launch_copy_word(hipStream_t s, uint32_t* dst, const uint32_t* src) {
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
+  if (fp.band_cull && fp.band_compact) {
+    const unsigned grid = (unsigned)((fp.n + kBandGpb * 256 - 1) / (kBandGpb * 256));
+    if (fp.pow2)
+      gs_project_band_kernel<true><<<grid, 256, 0, s>>>(fp, b);
+    else
+      gs_project_band_kernel<false><<<grid, 256, 0, s>>>(fp, b);
+    return;
+  }
   if (fp.pow2)
     gs_project_kernel<true><<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
   else

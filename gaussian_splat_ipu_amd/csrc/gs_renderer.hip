@@ -192,6 +192,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
+  fp.band_compact = r->env_band_compact != 0 ? 1 : 0;  // (A/B: GSPLAT_BAND_COMPACT=0)
   {
     double w2 = 0.0;  // squared Frobenius norm of the upper 3x3 of the mvp, rounded up
     for (int c = 0; c < 3; ++c)
@@ -626,6 +627,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) r->env_blend_lpt = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) r->env_mean_w1 = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_BAND_COMPACT")) r->env_band_compact = std::atoi(ev) != 0 ? 1 : 0;
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
