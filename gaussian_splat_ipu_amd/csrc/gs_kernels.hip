@@ -503,6 +503,10 @@ __device__ __forceinline__ void wave_minmax_u16x2(uint32_t& lo, uint32_t& hi) {
 // order set by the atomics; the depth sort puts every list in its total
 // (z, input index) order, so the lists and the frame are unchanged.
 constexpr int kAggCap = 1024;  // LDS histogram entries per workgroup
+// a box of at most this many tiles is counted by ballots instead of LDS
+// atomics (a clustered scene's workgroup puts all its pairs in a few tiles,
+// where the LDS atomics of a wave serialise on the same addresses)
+constexpr int kAggBallot = 16;
 
 struct AggBox {
   int x0, y0, w, area;  // area 0: nothing binned in the workgroup
@@ -565,6 +569,27 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
   const bool mine = start && x0 <= x1;
+  if (bx.area <= kAggBallot) {  // (uniform) small box: per tile, ballots of the rectangles covering it
+    __shared__ uint32_t s_wc[4][kAggBallot];
+    const int wave = threadIdx.x >> 6;
+    for (int k = 0; k < bx.area; ++k) {
+      const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
+      const bool in_r = x0 <= tx && tx <= x1 && y0 <= ty && ty <= y1;
+      const bool in_q = u0 <= tx && tx <= u1 && v0 <= ty && ty <= v1;
+      const uint32_t cr = (uint32_t)__popcll(ballot64(in_r)), cq = (uint32_t)__popcll(ballot64(in_q));
+      if ((threadIdx.x & 63) == 0) s_wc[wave][k] = (cr << 16) | cq;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < bx.area) {
+      const int k = threadIdx.x;
+      const uint32_t v = s_wc[0][k] + s_wc[1][k] + s_wc[2][k] + s_wc[3][k];
+      if (v) {
+        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
+        atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x], ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
+      }
+    }
+    return;
+  }
   if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: per run, global adds
     if (mine)
       for (uint32_t y = y0; y <= y1; ++y) {
@@ -1066,6 +1091,43 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
   if (bx.area == 0) return;  // (uniform)
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   const unsigned long long key = ((unsigned long long)dk << 32) | (uint32_t)i;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (bx.area <= kAggBallot) {  // (uniform) small box: ranks from ballots, no LDS atomics
+    __shared__ uint32_t s_wc[4][kAggBallot];
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int k = 0; k < bx.area; ++k) {
+      const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
+      const bool in = x0 <= tx && tx <= x1 && y0 <= ty && ty <= y1;
+      const uint32_t c = (uint32_t)__popcll(ballot64(in));
+      if (lane == 0) s_wc[wave][k] = c;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < bx.area) {  // the workgroup's range, split over its waves
+      const int k = threadIdx.x;
+      const uint32_t c0 = s_wc[0][k], c1 = s_wc[1][k], c2 = s_wc[2][k], c3 = s_wc[3][k];
+      const uint32_t tot = c0 + c1 + c2 + c3;
+      uint32_t base = 0u;
+      if (tot) {
+        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
+        base = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], tot);
+      }
+      s_wc[0][k] = base;
+      s_wc[1][k] = base + c0;
+      s_wc[2][k] = base + c0 + c1;
+      s_wc[3][k] = base + c0 + c1 + c2;
+    }
+    __syncthreads();
+    for (int k = 0; k < bx.area; ++k) {
+      const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
+      const bool in = x0 <= tx && tx <= x1 && y0 <= ty && ty <= y1;
+      const unsigned long long m = ballot64(in);
+      if (in) {
+        const uint32_t pos = s_wc[wave][k] + (uint32_t)__popcll(m & lt);
+        if (pos < fp.pair_cap) b.pairs[pos] = key;
+      }
+    }
+    return;
+  }
   if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: a global cursor per pair
     if (x0 <= x1)
       for (uint32_t y = y0; y <= y1; ++y)
@@ -1097,7 +1159,6 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
   // a run of equal rectangles takes its slots of each tile with one LDS
   // atomic by its first lane (clustered scenes: the lanes of a wave would
   // otherwise serialise on the same few tiles' cursors)
-  const int lane = threadIdx.x & 63;
   const unsigned long long st = ballot64(start);
   const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   const int lead = 63 - __builtin_clzll(st & upto);
