@@ -656,80 +656,6 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
   if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
 }
 
-// GS_FLAG_BAND_CULL: one workgroup per kBandGpb blocks of 256 Gaussians.  The
-// cheap band test runs first on all of them (kBandGpb 16-B cull records per
-// thread, loaded up front); the survivors' indices are compacted into LDS in
-// device order and projected in dense passes of 256, so a block that straddles
-// the band's edge no longer runs the full projection on waves whose lanes are
-// mostly culled.  Every block keeps the one-Gaussian-per-thread kernel's
-// contract: a block with no survivor writes only its V (0) and nothing else
-// reads it; in any other block every Gaussian's rectangles and depth key are
-// written (empty for the culled ones).
-constexpr int kBandGpb = 4;
-
-template <bool P2>
-__global__ __launch_bounds__(256) void gs_project_band_kernel(FrameParams fp, Buffers b) {
-  __shared__ uint32_t s_list[kBandGpb * 256];
-  __shared__ uint32_t s_cnt[kBandGpb][4];  // survivors per (block, wave)
-  __shared__ uint32_t s_v[kBandGpb];       // rendered per block
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int base = blockIdx.x * (kBandGpb * 256);
-  bool culled[kBandGpb];
-  {
-    float4 cr[kBandGpb];
-#pragma unroll
-    for (int k = 0; k < kBandGpb; ++k) {
-      const int i = base + k * 256 + tid;
-      cr[k] = i < fp.n ? b.cull[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int k = 0; k < kBandGpb; ++k) {
-      const int i = base + k * 256 + tid;
-      culled[k] = i >= fp.n || (!__builtin_isnan(cr[k].w) && band_culled_fast<P2>(fp, cr[k]));
-    }
-  }
-  unsigned long long live[kBandGpb];
-#pragma unroll
-  for (int k = 0; k < kBandGpb; ++k) {
-    live[k] = ballot64(!culled[k]);
-    if (lane == 0) s_cnt[k][wave] = (uint32_t)__popcll(live[k]);
-  }
-  if (tid < kBandGpb) s_v[tid] = 0u;
-  __syncthreads();
-  // survivors in device order: block k, then wave, then lane
-  uint32_t S = 0;
-  uint32_t blk_n[kBandGpb];
-#pragma unroll
-  for (int k = 0; k < kBandGpb; ++k) {
-    blk_n[k] = s_cnt[k][0] + s_cnt[k][1] + s_cnt[k][2] + s_cnt[k][3];
-    uint32_t before = S;
-    for (int w = 0; w < wave; ++w) before += s_cnt[k][w];
-    if (!culled[k]) s_list[before + (uint32_t)__popcll(live[k] & ((1ull << lane) - 1ull))] = (uint32_t)(base + k * 256 + tid);
-    S += blk_n[k];
-  }
-  // the culled Gaussians of live blocks: empty rectangles, no record
-#pragma unroll
-  for (int k = 0; k < kBandGpb; ++k) {
-    const int i = base + k * 256 + tid;
-    if (blk_n[k] != 0u && culled[k] && i < fp.n) {
-      store_rects(fp, b, i, kEmptyRect, kEmptyRect);
-      b.depth_key[i] = 0xFFFFFFFFu;
-    }
-  }
-  __syncthreads();
-  for (uint32_t p0 = 0; p0 < S; p0 += 256) {  // (uniform) dense passes over the survivors
-    uint2 rect = kEmptyRect, crect = kEmptyRect;
-    const uint32_t k = p0 + (uint32_t)tid;
-    if (k < S) {
-      const int i = (int)s_list[k];
-      if (project_one<P2>(fp, b, i, rect, crect)) atomicAdd(&s_v[(i - base) >> 8], 1u);
-    }
-    if (fp.bin_agg) agg_count(fp, b, rect, crect);
-    __syncthreads();  // (agg_count's LDS is reused by the next pass)
-  }
-  if (tid < kBandGpb && base + tid * 256 < fp.n) b.block_rendered[blockIdx.x * kBandGpb + tid] = s_v[tid];
-}
-
 // --------------------------------------------------------------------- scan
 // One workgroup of 1024 threads, rounds of 8192 tiles (8 per thread, held in
 // registers): tile_start = exclusive scan(tile_count), max list length, and
@@ -883,11 +809,11 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   __shared__ uint32_t s_c[8192];  // a round's binned counts (striped in, blocked out)
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // V = the projection workgroups' counts (loads issued up front)
-  uint32_t vsum = 0;
+  // V = the projection workgroups' counts, reduced per wave at once (kept
+  // live across the rounds they were spilled)
   {
     const int nb = (fp.n + 255) / 256;
-    uint32_t vr[8];
+    uint32_t vr[8], vsum = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int i = tid + k * 1024;
@@ -896,6 +822,9 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     for (int i = tid + 8 * 1024; i < nb; i += 1024) vsum += b.block_rendered[i];
 #pragma unroll
     for (int k = 0; k < 8; ++k) vsum += vr[k];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
+    if (lane == 0) wvis[wave] = vsum;
   }
   // (lanes 0..15 of wave 0) the running bases over the rounds
   unsigned long long carry = 0, rcarry = 0;
@@ -903,7 +832,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   uint32_t mx = 0;
   for (int r0 = 0; r0 < T; r0 += 8192) {
     // the round's counters, read striped (coalesced: lane-consecutive tiles);
-    // the histogram goes to the host mirror (and the footer) from here, the
+    // the histogram goes to tile_ref (and the group's footer) from here, the
     // counters are zeroed for the next frame, and the binned counts are
     // transposed through LDS so each thread scans 8 consecutive tiles
     unsigned long long rsum = 0;
@@ -922,7 +851,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
         s_c[j * 1024 + tid] = (uint32_t)vs[j];
         if (i < T) {
           b.tile_cnt64[i] = 0ull;  // zero for the next frame's projection
-          b.host_counters[16 + i] = rf;  // the histogram (reference list lengths)
+          b.tile_ref[i] = rf;      // the histogram (reference list lengths; the host reads it at sync)
           if (b.footer) b.footer[16 + i] = rf;
         }
       }
@@ -1033,12 +962,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
-  if (lane == 0) {
-    wvis[wave] = vsum;
-    wmax[wave] = mx;
-  }
+  if (lane == 0) wmax[wave] = mx;
   __syncthreads();
   if (tid == 0) {
     uint32_t vis = 0, m = 0;
@@ -3150,14 +3074,6 @@ void launch_copy_word(hipStream_t s, uint32_t* dst, const uint32_t* src) {
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
-  if (fp.band_cull && fp.band_compact) {
-    const unsigned grid = (unsigned)((fp.n + kBandGpb * 256 - 1) / (kBandGpb * 256));
-    if (fp.pow2)
-      gs_project_band_kernel<true><<<grid, 256, 0, s>>>(fp, b);
-    else
-      gs_project_band_kernel<false><<<grid, 256, 0, s>>>(fp, b);
-    return;
-  }
   if (fp.pow2)
     gs_project_kernel<true><<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
   else

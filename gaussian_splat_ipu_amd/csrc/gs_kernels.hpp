@@ -26,8 +26,6 @@ struct FrameParams {
   int tiles_y;        // tile rows of the whole frame
   int band_rows;      // pixel rows of this band's output
   int band_cull;      // skip Gaussians whose extent bound misses the band (GS_FLAG_BAND_CULL)
-  int band_compact;   // band cull: the survivors of 4 blocks compacted and projected densely
-                      //   (gs_project_band_kernel)
   float wnorm2;       // >= squared Frobenius norm of the mvp's upper 3x3 (band cull bound)
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
@@ -94,6 +92,8 @@ struct Buffers {
   uint32_t* tile_count;     // [n_tiles]      (memset 0 each frame)
   unsigned long long* tile_cnt64;  // [n_tiles] aggregated binning: binned | reference << 32 per
                                    //   tile (zero between frames: the scan resets it)
+  uint32_t* tile_ref;       // [n_tiles] aggregated binning: the reference list lengths (the
+                            //   histogram; copied to the host mirror at sync, not per frame)
   uint32_t* tile_start;     // [n_tiles + 1]
   uint32_t* tile_cursor;    // [n_tiles]
   unsigned long long* pairs;      // [pair_cap]  (depth_key << 32 | input index)

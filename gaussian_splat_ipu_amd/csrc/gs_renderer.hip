@@ -158,6 +158,8 @@ void release(gs_renderer* r) {
 // (gs_colscan_kernel walks a tile's chunk rows: past 256 of them it reads
 // them twice, in batches of 8)
 constexpr size_t kMaxBandChunks = 1024;
+// the aggregated binning up to this many tiles per frame (or band)
+constexpr int kAggMaxTiles = 16384;
 
 gsk::FrameParams make_params(const gs_renderer* r) {
   gsk::FrameParams fp{};
@@ -192,7 +194,6 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
-  fp.band_compact = r->env_band_compact != 0 ? 1 : 0;  // (A/B: GSPLAT_BAND_COMPACT=0)
   {
     double w2 = 0.0;  // squared Frobenius norm of the upper 3x3 of the mvp, rounded up
     for (int c = 0; c < 3; ++c)
@@ -227,8 +228,8 @@ gsk::FrameParams make_params(const gs_renderer* r) {
     fp.n_chunks = (int)((r->n + cs - 1) / cs);
   }
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
-  fp.bin_agg = r->bin_agg ? 1 : 0;
-  fp.pair_cull = (r->pair_cull && !r->bin_global && ((r->n_chunks > 0 && fp.emit_wide) || r->bin_agg)) ? 1 : 0;
+  fp.bin_agg = (r->bin_agg && (r->bin_agg_mode == 1 || r->n_tiles <= kAggMaxTiles)) ? 1 : 0;
+  fp.pair_cull = (r->pair_cull && !r->bin_global && ((r->n_chunks > 0 && fp.emit_wide) || fp.bin_agg)) ? 1 : 0;
   fp.mean_w1 = (r->scene_w1 && r->env_mean_w1 != 0) ? 1 : 0;  // (A/B: GSPLAT_MEAN_W1=0)
   // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
   fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256 && r->env_rect8 != 0) ? 1 : 0;
@@ -461,6 +462,13 @@ int finish_frame(gs_renderer* r) {
   if (!r->frame_pending) return GS_OK;
   GS_HIP(hipStreamSynchronize(r->stream));
   r->frame_pending = false;
+  const int nt0 = r->have_fp ? r->last_fp.n_tiles : r->n_tiles;
+  // the aggregated binning keeps the frame's histogram on the device (a
+  // per-frame copy into mapped memory from one workgroup cost the scan more
+  // than the rest of its work): one copy here, at sync.  A group member's
+  // histogram travels in its footer instead.
+  if (r->have_fp && r->last_fp.bin_agg && !r->buf.footer && nt0 > 0)
+    GS_HIP(hipMemcpy(r->h_counters + 16, r->buf.tile_ref, (size_t)nt0 * 4, hipMemcpyDeviceToHost));
   const uint32_t* c = r->h_counters;
   const uint64_t P = (uint64_t)c[5] | ((uint64_t)c[6] << 32);
   // the chunked scan also sums the reference (unculled) list lengths
@@ -627,7 +635,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) r->env_blend_lpt = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) r->env_mean_w1 = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_BAND_COMPACT")) r->env_band_compact = std::atoi(ev) != 0 ? 1 : 0;
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
@@ -791,7 +798,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.counters = (uint32_t*)r->d_zero;
   r->buf.tile_count = (uint32_t*)r->d_zero + 16;
   const size_t n_agg = (T + 63) / 64;
-  const size_t tiles_bytes = (T + 1 + 4 * T) * 4 + n_agg * 32 + 16 + T * 8 + 8;
+  const size_t tiles_bytes = (T + 1 + 4 * T) * 4 + n_agg * 32 + 16 + T * 8 + 8 + T * 4;
   if ((e = hipMalloc(&r->d_tiles, tiles_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(tiles)"));
   poison(r->d_tiles, tiles_bytes, "tiles");
   r->buf.tile_start = (uint32_t*)r->d_tiles;
@@ -803,6 +810,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   // the aggregated binning's per-tile counters: zero between frames (the
   // scan resets them)
   r->buf.tile_cnt64 = (unsigned long long*)(((uintptr_t)(r->buf.tile_agg + 2 * n_agg) + 7) & ~(uintptr_t)7);
+  r->buf.tile_ref = (uint32_t*)(r->buf.tile_cnt64 + T);
   if ((e = hipMemset(r->d_tiles, 0, (T + 1 + 4 * T) * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(tiles)"));
   if ((e = hipMemset(r->buf.tile_cnt64, 0, T * 8)) != hipSuccess) return fail(hip_fail(e, "hipMemset(tile counters)"));
@@ -834,10 +842,15 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       // shrinks with the band instead of staying a whole-frame chunk
       r->chunk_entries = (size_t)r->n_chunks * (size_t)std::max(r->n_tiles, r->tiles_x * r->tiles_y);
       r->chunk_adaptive = fixed_cs == nullptr && max_chunks == SIZE_MAX;
-      // the aggregated binning (default; GSPLAT_BIN_AGG=0: the chunked
-      // count / column scan / emit, A/B)
+      // the aggregated binning for grids of up to kAggMaxTiles tiles (frames
+      // at 1080p, any row band of a 4K frame split over >= 2 GPUs), the
+      // chunked count / column scan / emit beyond (config 5's 4K frame on one
+      // GPU: its clustered workgroups fill few tiles, whose LDS atomics cost
+      // the projection more than the chunked passes take).  GSPLAT_BIN_AGG=0 /
+      // 1 forces either (A/B, tests).
       const char* agg_env = std::getenv("GSPLAT_BIN_AGG");
-      r->bin_agg = !(agg_env && std::strcmp(agg_env, "0") == 0) && fixed_cs == nullptr;
+      r->bin_agg_mode = agg_env ? (std::strcmp(agg_env, "0") == 0 ? 0 : 1) : -1;
+      r->bin_agg = r->bin_agg_mode != 0 && fixed_cs == nullptr;
       if ((e = hipMalloc(&r->d_chunk, r->chunk_entries * 4)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
       poison(r->d_chunk, r->chunk_entries * 4, "chunk");
