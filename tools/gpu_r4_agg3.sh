@@ -36,4 +36,7 @@ for agg in 1 0; do
 done
 echo "== trace band 3 of 8 $(date +%T)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_band3 -o band3 --output-format csv -- python3 tools/band_emulate.py --balanced --inflight 3 --bands 8 --only-band 3 --steps 200 > $O/trace_band3.log 2>&1 || exit $?
+echo "== FETCH_SIZE calibration $(date +%T)"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/calib -o calib --output-format csv -- tools/hip/fetch_calib > $O/calib.log 2>&1 || exit $?
+python3 tools/fetch_calib.py $O/calib --json $O/fetch_calib.json
 echo "== done $(date +%T)"
