@@ -2777,7 +2777,8 @@ __device__ __forceinline__ void blend_count_store(const FrameParams& fp, const B
 }
 
 // wid = the wave's (tile slot, 8x8 block) item; wave = its LDS staging slot
-template <int BQW, bool HWEXP>
+// (of WPG: the waves of the workgroup)
+template <int BQW, bool HWEXP, int WPG = GS_BLEND_WPG>
 __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wave, int wid) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
@@ -2876,7 +2877,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   L -= k0;
 
   // wave-private staging of one batch of 64 records (48 B each with the colour) in LDS
-  __shared__ float4 s_rec[GS_BLEND_WPG][3][64];
+  __shared__ float4 s_rec[WPG][3][64];
   float4(*const st)[64] = s_rec[wave];
 
   // software pipeline: records of batch `base`, index of batch `base + 64`
@@ -3048,6 +3049,33 @@ __global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b
   blend_body<BQW, HWEXP>(fp, b, blockIdx.x);
 }
 
+// GSPLAT_BLEND_PERSIST=G (A/B): G resident workgroups of 16 waves; workgroup
+// k owns the tiles k, k + G, k + 2G, ... (spread over the frame, so every
+// workgroup gets a similar load) and its waves take that range's (tile,
+// block) items one after another from an LDS counter -- no workgroup
+// dispatch per item, and no contended global counter (the round-3
+// persistent blend's single returning atomic serialised).
+constexpr int kBlendPersistWaves = 16;
+
+template <int BQW, bool HWEXP>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_blend_persist_kernel(FrameParams fp, Buffers b) {
+  __shared__ uint32_t s_next;
+  if (threadIdx.x == 0) s_next = 0u;
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = (int)gridDim.x, cpt = fp.chunks_per_tile;
+  const int tiles_wg = fp.n_tiles > (int)blockIdx.x ? (fp.n_tiles - (int)blockIdx.x + G - 1) / G : 0;
+  const uint32_t items_wg = (uint32_t)(tiles_wg * cpt);
+  for (;;) {
+    uint32_t j = 0u;
+    if ((threadIdx.x & 63) == 0) j = atomicAdd(&s_next, 1u);
+    j = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl((int)j, 0, 64));
+    if (j >= items_wg) break;
+    const int m = (int)j / cpt, chunk = (int)j - m * cpt;
+    blend_wave<BQW, HWEXP, kBlendPersistWaves>(fp, b, wave, ((int)blockIdx.x + G * m) * cpt + chunk);
+  }
+}
+
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
 // the prefix blend).  A grid-stride loop over the waves of the big lists
 // only: a grid of every tile's waves, nearly all of which exit at once, cost
@@ -3162,6 +3190,11 @@ void launch_sort_tiles(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
   if (waves == 0) return;
+  if (fp.blend_persist > 0 && fp.blend_bqw == 4 && !fp.fast_exp) {
+    const unsigned g = (unsigned)std::min<long>(fp.blend_persist, fp.n_tiles);
+    gs_blend_persist_kernel<4, false><<<g, 64 * kBlendPersistWaves, 0, s>>>(fp, b);
+    return;
+  }
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
   if (fp.fast_exp) {

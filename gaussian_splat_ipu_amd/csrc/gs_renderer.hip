@@ -211,6 +211,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
   if (r->env_blend_lpt >= 0) fp.blend_lpt = r->env_blend_lpt;  // (A/B)
+  fp.blend_persist = r->env_blend_persist > 0 ? r->env_blend_persist : 0;  // (A/B: GSPLAT_BLEND_PERSIST=G)
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
@@ -635,6 +636,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) r->env_blend_lpt = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) r->env_mean_w1 = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_BLEND_PERSIST")) r->env_blend_persist = std::max(0, std::min(4096, std::atoi(ev)));
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
