@@ -2776,10 +2776,53 @@ __device__ __forceinline__ void blend_count_store(const FrameParams& fp, const B
   }
 }
 
+// The persistent blend's look-ahead: a (tile, block) item's list span and
+// the list entries of its first two batches, loaded while the wave still
+// blends the item before it (the prefix blend only, not the continuation).
+struct BlendPre {
+  int tile;           // -1: no item
+  uint32_t s, L;      // the walked span of the tile's list
+  uint32_t Lfull;     // the tile's whole list (lazy big lists: L is the sorted prefix)
+  uint32_t jb;        // the tile's big-list slot (~0: none)
+  uint32_t g0, g1;    // list entries of batches 0 and 1 (this lane's)
+};
+
+__device__ __forceinline__ uint32_t blend_idx(const FrameParams& fp, const uint32_t* list, uint32_t L, uint32_t k) {
+  uint32_t g = 0xFFFFFFFFu;
+  if (k < L) g = list[k];
+  return g < (uint32_t)fp.n ? g : 0xFFFFFFFFu;  // defensive: never read past the records
+}
+
+__device__ __forceinline__ BlendPre blend_prefetch(const FrameParams& fp, const Buffers& b, int wid, bool ok) {
+  BlendPre it;
+  it.tile = -1;
+  it.s = it.L = it.Lfull = 0u;
+  it.jb = 0xFFFFFFFFu;
+  it.g0 = it.g1 = 0xFFFFFFFFu;
+  const int slot = wid / fp.chunks_per_tile;
+  if (!ok || slot >= fp.n_tiles) return it;
+  int tile = slot;
+  if (fp.blend_lpt) {
+    const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
+    tile = (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
+  }
+  it.tile = tile;
+  tile_segment(fp, b, tile, it.s, it.L);
+  it.Lfull = it.L;
+  if (fp.lazy) it.jb = b.tile_big[tile];
+  if (it.jb != 0xFFFFFFFFu) it.L = min(b.big_len[it.jb], it.L);
+  const int lane = threadIdx.x & 63;
+  it.g0 = blend_idx(fp, b.list + it.s, it.L, (uint32_t)lane);
+  it.g1 = blend_idx(fp, b.list + it.s, it.L, 64u + (uint32_t)lane);
+  return it;
+}
+
 // wid = the wave's (tile slot, 8x8 block) item; wave = its LDS staging slot
-// (of WPG: the waves of the workgroup)
+// (of WPG: the waves of the workgroup); pre: the item's look-ahead (the
+// persistent blend), nullptr = load it here
 template <int BQW, bool HWEXP, int WPG = GS_BLEND_WPG>
-__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wave, int wid) {
+__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wave, int wid,
+                                           const BlendPre* pre = nullptr) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
   if (slot >= fp.n_tiles) return;
@@ -2802,7 +2845,9 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   // full frame keeps the tile order (neighbouring tiles share records in L2:
   // 75.1 against 76.1 us in queue order).
   int tile = slot;
-  if (fp.blend_cont) {
+  if (pre) {
+    tile = pre->tile;
+  } else if (fp.blend_cont) {
     tile = (int)b.big_tiles[jb];
   } else if (fp.blend_lpt) {
     const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
@@ -2852,12 +2897,20 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   q.done = !valid;
 
   uint32_t s, L;
-  tile_segment(fp, b, tile, s, L);
-  // lazy big list: this pass composites the sorted prefix [0, big_len), the
-  // continuation the rest [big_len, L) from the saved state
-  uint32_t k0 = 0u, Lfull = L;
-  if (fp.lazy && !fp.blend_cont) jb = b.tile_big[tile];
-  if (jb != 0xFFFFFFFFu) {
+  uint32_t k0 = 0u, Lfull;
+  if (pre) {
+    s = pre->s;
+    L = pre->L;
+    Lfull = pre->Lfull;
+    jb = pre->jb;
+  } else {
+    tile_segment(fp, b, tile, s, L);
+    Lfull = L;
+    // lazy big list: this pass composites the sorted prefix [0, big_len), the
+    // continuation the rest [big_len, L) from the saved state
+    if (fp.lazy && !fp.blend_cont) jb = b.tile_big[tile];
+  }
+  if (!pre && jb != 0xFFFFFFFFu) {
     const uint32_t np = min(b.big_len[jb], L);
     if (fp.blend_cont) {
       // the list now holds, from its start, the keys past the prefix whose
@@ -2881,11 +2934,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   float4(*const st)[64] = s_rec[wave];
 
   // software pipeline: records of batch `base`, index of batch `base + 64`
-  auto load_idx = [&](uint32_t k) -> uint32_t {
-    uint32_t g = 0xFFFFFFFFu;
-    if (k < L) g = list[k];
-    return g < (uint32_t)fp.n ? g : 0xFFFFFFFFu;  // defensive: never read past the records
-  };
+  auto load_idx = [&](uint32_t k) -> uint32_t { return blend_idx(fp, list, L, k); };
   // a record (32 B) and its colour + opacity (the scene's, or gs_set_sh's
   // view-dependent one), assembled as the staged 48-B layout
   const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
@@ -2898,9 +2947,9 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
     r2 = make_float4(c.z, c.w, t.z, t.w);
   };
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
-  uint32_t g_cur = load_idx(lane);
+  uint32_t g_cur = pre ? pre->g0 : load_idx(lane);
   if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
-  uint32_t g_next = load_idx(64 + lane);
+  uint32_t g_next = pre ? pre->g1 : load_idx(64 + lane);
 
   uint32_t staged = 0;  // records staged (profiled frames)
   for (uint32_t base = 0; base < L; base += 64) {
@@ -3066,13 +3115,26 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
   const int G = (int)gridDim.x, cpt = fp.chunks_per_tile;
   const int tiles_wg = fp.n_tiles > (int)blockIdx.x ? (fp.n_tiles - (int)blockIdx.x + G - 1) / G : 0;
   const uint32_t items_wg = (uint32_t)(tiles_wg * cpt);
-  for (;;) {
+  auto take = [&]() -> uint32_t {
     uint32_t j = 0u;
     if ((threadIdx.x & 63) == 0) j = atomicAdd(&s_next, 1u);
-    j = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl((int)j, 0, 64));
-    if (j >= items_wg) break;
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl((int)j, 0, 64));
+  };
+  auto wid_of = [&](uint32_t j) -> int {
     const int m = (int)j / cpt, chunk = (int)j - m * cpt;
-    blend_wave<BQW, HWEXP, kBlendPersistWaves>(fp, b, wave, ((int)blockIdx.x + G * m) * cpt + chunk);
+    return ((int)blockIdx.x + G * m) * cpt + chunk;
+  };
+  // the next item's list span and first list entries are loaded before the
+  // current item is blended: its three dependent round trips (tile bounds,
+  // list entries, records) shrink to the records'
+  uint32_t j = take();
+  BlendPre cur = blend_prefetch(fp, b, wid_of(j), j < items_wg);
+  while (j < items_wg) {
+    const uint32_t jn = take();
+    const BlendPre nxt = blend_prefetch(fp, b, wid_of(jn), jn < items_wg);
+    blend_wave<BQW, HWEXP, kBlendPersistWaves>(fp, b, wave, wid_of(j), &cur);
+    j = jn;
+    cur = nxt;
   }
 }
 
