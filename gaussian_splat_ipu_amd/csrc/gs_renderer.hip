@@ -229,7 +229,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
     fp.n_chunks = (int)((r->n + cs - 1) / cs);
   }
   fp.emit_wide = (size_t)r->n_tiles * 4 <= gsk::kBinLdsMax ? 1 : 0;
-  fp.bin_agg = (r->bin_agg && (r->bin_agg_mode == 1 || r->n_tiles <= kAggMaxTiles)) ? 1 : 0;
+  fp.bin_agg = (r->bin_agg && !r->lattice && (r->bin_agg_mode == 1 || r->n_tiles <= kAggMaxTiles)) ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && ((r->n_chunks > 0 && fp.emit_wide) || fp.bin_agg)) ? 1 : 0;
   fp.mean_w1 = (r->scene_w1 && r->env_mean_w1 != 0) ? 1 : 0;  // (A/B: GSPLAT_MEAN_W1=0)
   // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
