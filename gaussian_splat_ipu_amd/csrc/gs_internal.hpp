@@ -74,6 +74,7 @@ struct gs_renderer {
   void* d_out = nullptr;        // rgba f32 + bgr8
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
   void* d_lazy = nullptr;       // lazy big lists (16x16 tiles): per-tile tables + saved blend waves
+  void* d_agg = nullptr;        // aggregated binning: per projection block its tile box and offsets
   // GS_FLAG_LATTICE: the lattice-migration emulator's state (gs_lattice.hip)
   void* d_lat = nullptr;
   bool lattice = false;

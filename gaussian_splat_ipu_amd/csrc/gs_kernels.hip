@@ -502,7 +502,7 @@ __device__ __forceinline__ void wave_minmax_u16x2(uint32_t& lo, uint32_t& hi) {
 // places the pairs by LDS cursors.  The pairs land in a tile's segment in an
 // order set by the atomics; the depth sort puts every list in its total
 // (z, input index) order, so the lists and the frame are unchanged.
-constexpr int kAggCap = 1024;  // LDS histogram entries per workgroup
+constexpr uint32_t kAggSpread = 0xFFFFFFFFu;  // agg_box area marker: the per-pair fallback
 // a box of at most this many tiles is counted by ballots instead of LDS
 // atomics (a clustered scene's workgroup puts all its pairs in a few tiles,
 // where the LDS atomics of a wave serialise on the same addresses)
@@ -559,16 +559,31 @@ __device__ __forceinline__ bool rect_run(uint2 r, uint2 q, uint32_t& len) {
 
 // The projection workgroup's share of the per-tile counters: r = reference
 // rectangle, q = binned rectangle (q inside r) of this thread's Gaussian.
-__device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& b, uint2 r, uint2 q) {
+__device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& b, uint2 r, uint2 q, int blk) {
   __shared__ uint32_t cnt[kAggCap];
   __shared__ uint32_t s_lo[4], s_hi[4];
   const AggBox bx = agg_box(r, s_lo, s_hi);
+  // the box the emit uses (the reference rectangles' box, which holds the
+  // binned ones): origin, width, area (kAggSpread: the per-pair fallback)
+  if (threadIdx.x == 0)
+    b.agg_box[blk] = make_uint4((uint32_t)bx.x0, (uint32_t)bx.y0, (uint32_t)bx.w,
+                                bx.area > kAggCap ? kAggSpread : (uint32_t)bx.area);
   if (bx.area == 0) return;  // (uniform)
   uint32_t len;
   const bool start = rect_run(r, q, len);
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
   const bool mine = start && x0 <= x1;
+  uint32_t* const off = b.agg_off + (size_t)blk * kAggCap;
+  // one returning add per (workgroup, tile): binned | reference << 32 into
+  // the tile's counter; the binned half of the old value is this
+  // workgroup's offset within the tile's aggregated pairs (the emit's slots)
+  auto reserve = [&](int k, uint32_t v) {
+    const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
+    const unsigned long long old =
+        atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x], ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
+    off[k] = (uint32_t)old;
+  };
   if (bx.area <= kAggBallot) {  // (uniform) small box: per tile, ballots of the rectangles covering it
     __shared__ uint32_t s_wc[4][kAggBallot];
     const int wave = threadIdx.x >> 6;
@@ -583,20 +598,18 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
     if ((int)threadIdx.x < bx.area) {
       const int k = threadIdx.x;
       const uint32_t v = s_wc[0][k] + s_wc[1][k] + s_wc[2][k] + s_wc[3][k];
-      if (v) {
-        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
-        atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x], ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
-      }
+      if (v) reserve(k, v);
     }
     return;
   }
-  if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: per run, global adds
+  if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: per run, the fallback counters
     if (mine)
       for (uint32_t y = y0; y <= y1; ++y) {
         const bool yin = v0 <= y && y <= v1;
         for (uint32_t x = x0; x <= x1; ++x) {
-          const unsigned long long inc = ((unsigned long long)len << 32) | ((yin && u0 <= x && x <= u1) ? len : 0u);
-          atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x], inc);
+          const uint32_t t = y * fp.tiles_x + x;
+          if (yin && u0 <= x && x <= u1) atomicAdd(&b.tile_fb[t], len);
+          atomicAdd(&b.tile_cnt64[t], (unsigned long long)len << 32);
         }
       }
     return;
@@ -613,10 +626,7 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
   __syncthreads();
   for (int k = threadIdx.x; k < bx.area; k += 256) {
     const uint32_t v = cnt[k];
-    if (v) {
-      const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
-      atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x], ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
-    }
+    if (v) reserve(k, v);
   }
 }
 
@@ -650,7 +660,7 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
   } else if (i < fp.n) {
     rendered = project_one<P2>(fp, b, i, rect, crect);
   }
-  if (fp.bin_agg) agg_count(fp, b, rect, crect);
+  if (fp.bin_agg) agg_count(fp, b, rect, crect, blockIdx.x);
   // V per workgroup (summed by the scan kernel): no single-address atomics
   const int v = __syncthreads_count(rendered);
   if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
@@ -807,6 +817,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   __shared__ unsigned long long s_tot;
   __shared__ uint32_t s_qt[3];
   __shared__ uint32_t s_c[8192];  // a round's binned counts (striped in, blocked out)
+  __shared__ uint32_t s_a[8192];  // ... their aggregated parts
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // V = the projection workgroups' counts, reduced per wave at once (kept
@@ -838,19 +849,23 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     unsigned long long rsum = 0;
     {
       unsigned long long vs[8];
+      uint32_t fb[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = r0 + j * 1024 + tid;
         vs[j] = i < T ? b.tile_cnt64[i] : 0ull;
+        fb[j] = i < T ? b.tile_fb[i] : 0u;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = r0 + j * 1024 + tid;
         const uint32_t rf = (uint32_t)(vs[j] >> 32);
         rsum += rf;
-        s_c[j * 1024 + tid] = (uint32_t)vs[j];
+        s_c[j * 1024 + tid] = (uint32_t)vs[j] + fb[j];  // the tile's binned pairs
+        s_a[j * 1024 + tid] = (uint32_t)vs[j];          // ... of which the aggregated workgroups'
         if (i < T) {
           b.tile_cnt64[i] = 0ull;  // zero for the next frame's projection
+          b.tile_fb[i] = 0u;
           b.tile_ref[i] = rf;      // the histogram (reference list lengths; the host reads it at sync)
           if (b.footer) b.footer[16 + i] = rf;
         }
@@ -955,7 +970,8 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       if (i < T) {
         const uint32_t st = s_c[j * 1024 + tid];
         b.tile_start[i] = st;
-        b.tile_cursor[i] = st;  // gs_agg_emit_kernel's reservations
+        // the fallback workgroups' pairs follow the aggregated ones'
+        b.tile_cursor[i] = st + s_a[j * 1024 + tid];
       }
     }
     __syncthreads();  // the wave tables and s_c are rewritten by the next round
@@ -996,44 +1012,57 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
 }
 
 // Aggregated binning's emit: one workgroup per projection block of 256
-// Gaussians.  Its binned pairs are counted per tile of its box in LDS (runs
-// of equal rectangles add once), each non-zero tile reserves the
-// workgroup's range with one returning atomic on the tile's cursor, and every
-// pair then takes the next slot of its tile's range from an LDS cursor.
+// Gaussians.  The projection reserved the block's range of every tile it has
+// pairs in (agg_off: its offset among the tile's aggregated pairs) over the
+// box it recorded (agg_box); each pair takes the next slot of its tile's
+// range: by ballot ranks for a box of <= kAggBallot tiles, else from an LDS
+// cursor per tile (one atomic per run of equal rectangles).  A block whose
+// box was too wide for LDS places every pair with a global cursor past the
+// tile's aggregated pairs.
 __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffers b) {
   __shared__ uint32_t cnt[kAggCap];
-  __shared__ uint32_t s_lo[4], s_hi[4];
-  const int i = blockIdx.x * 256 + (int)threadIdx.x;
-  if (fp.band_cull && b.block_rendered[blockIdx.x] == 0u) return;  // (uniform) culled block: nothing binned
+  const int blk = blockIdx.x;
+  const int i = blk * 256 + (int)threadIdx.x;
+  if (fp.band_cull && b.block_rendered[blk] == 0u) return;  // (uniform) culled block: nothing binned
+  const uint4 box = b.agg_box[blk];
+  if (box.w == 0u) return;  // (uniform) nothing binned
   uint2 r = kEmptyRect;
   uint32_t dk = 0u;
   if (i < fp.n) {
     r = fp.rect8 ? rect8_unpack(reinterpret_cast<const uint32_t*>(b.crect)[i]) : (fp.pair_cull ? b.crect[i] : b.rect[i]);
     dk = b.depth_key[i];
   }
-  const AggBox bx = agg_box(r, s_lo, s_hi);
-  if (bx.area == 0) return;  // (uniform)
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   const unsigned long long key = ((unsigned long long)dk << 32) | (uint32_t)i;
+  if (box.w == kAggSpread || box.z == 0u) {  // (uniform) the per-pair fallback
+    if (x0 <= x1)
+      for (uint32_t y = y0; y <= y1; ++y)
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const uint32_t pos = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], 1u);
+          if (pos < fp.pair_cap) b.pairs[pos] = key;
+        }
+    return;
+  }
+  const int bx0 = (int)box.x, by0 = (int)box.y, bw = (int)box.z, area = (int)box.w;
+  const uint32_t* const off = b.agg_off + (size_t)blk * kAggCap;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (bx.area <= kAggBallot) {  // (uniform) small box: ranks from ballots, no LDS atomics
+  if (area <= kAggBallot) {  // (uniform) small box: ranks from ballots, no LDS atomics
     __shared__ uint32_t s_wc[4][kAggBallot];
     const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int k = 0; k < bx.area; ++k) {
-      const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
+    for (int k = 0; k < area; ++k) {
+      const uint32_t tx = (uint32_t)(bx0 + k % bw), ty = (uint32_t)(by0 + k / bw);
       const bool in = x0 <= tx && tx <= x1 && y0 <= ty && ty <= y1;
       const uint32_t c = (uint32_t)__popcll(ballot64(in));
       if (lane == 0) s_wc[wave][k] = c;
     }
     __syncthreads();
-    if ((int)threadIdx.x < bx.area) {  // the workgroup's range, split over its waves
+    if ((int)threadIdx.x < area) {  // the block's range, split over its waves
       const int k = threadIdx.x;
       const uint32_t c0 = s_wc[0][k], c1 = s_wc[1][k], c2 = s_wc[2][k], c3 = s_wc[3][k];
-      const uint32_t tot = c0 + c1 + c2 + c3;
       uint32_t base = 0u;
-      if (tot) {
-        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
-        base = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], tot);
+      if (c0 + c1 + c2 + c3) {
+        const int y = by0 + k / bw, x = bx0 + k % bw;
+        base = b.tile_start[y * fp.tiles_x + x] + off[k];
       }
       s_wc[0][k] = base;
       s_wc[1][k] = base + c0;
@@ -1041,8 +1070,8 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
       s_wc[3][k] = base + c0 + c1 + c2;
     }
     __syncthreads();
-    for (int k = 0; k < bx.area; ++k) {
-      const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
+    for (int k = 0; k < area; ++k) {
+      const uint32_t tx = (uint32_t)(bx0 + k % bw), ty = (uint32_t)(by0 + k / bw);
       const bool in = x0 <= tx && tx <= x1 && y0 <= ty && ty <= y1;
       const unsigned long long m = ballot64(in);
       if (in) {
@@ -1052,33 +1081,14 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
     }
     return;
   }
-  if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: a global cursor per pair
-    if (x0 <= x1)
-      for (uint32_t y = y0; y <= y1; ++y)
-        for (uint32_t x = x0; x <= x1; ++x) {
-          const uint32_t pos = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], 1u);
-          if (pos < fp.pair_cap) b.pairs[pos] = key;
-        }
-    return;
+  // LDS cursors seeded with the block's ranges (entries of tiles without its
+  // pairs hold stale offsets, never used)
+  for (int k = threadIdx.x; k < area; k += 256) {
+    const int y = by0 + k / bw, x = bx0 + k % bw;
+    cnt[k] = b.tile_start[y * fp.tiles_x + x] + off[k];
   }
-  for (int k = threadIdx.x; k < bx.area; k += 256) cnt[k] = 0u;
-  __syncthreads();
   uint32_t len;
   const bool start = rect_run(r, r, len);
-  if (start && x0 <= x1)
-    for (uint32_t y = y0; y <= y1; ++y) {
-      const int row = ((int)y - bx.y0) * bx.w - bx.x0;
-      for (uint32_t x = x0; x <= x1; ++x) atomicAdd(&cnt[row + (int)x], len);
-    }
-  __syncthreads();
-  // the workgroup's range of every tile it has pairs in
-  for (int k = threadIdx.x; k < bx.area; k += 256) {
-    const uint32_t c = cnt[k];
-    if (c) {
-      const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
-      cnt[k] = atomicAdd(&b.tile_cursor[y * fp.tiles_x + x], c);
-    }
-  }
   __syncthreads();
   // a run of equal rectangles takes its slots of each tile with one LDS
   // atomic by its first lane (clustered scenes: the lanes of a wave would
@@ -1089,7 +1099,7 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
   const uint32_t rank = (uint32_t)(lane - lead);
   if (x0 <= x1)
     for (uint32_t y = y0; y <= y1; ++y) {
-      const int row = ((int)y - bx.y0) * bx.w - bx.x0;
+      const int row = ((int)y - by0) * bw - bx0;
       for (uint32_t x = x0; x <= x1; ++x) {
         uint32_t base = 0u;
         if (start) base = atomicAdd(&cnt[row + (int)x], len);

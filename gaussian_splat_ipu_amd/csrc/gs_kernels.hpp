@@ -95,6 +95,12 @@ struct Buffers {
                                    //   tile (zero between frames: the scan resets it)
   uint32_t* tile_ref;       // [n_tiles] aggregated binning: the reference list lengths (the
                             //   histogram; copied to the host mirror at sync, not per frame)
+  uint32_t* tile_fb;        // [n_tiles] aggregated binning: binned pairs of the fallback
+                            //   (box too wide) workgroups, placed after the aggregated ones
+  uint4* agg_box;           // [ceil(n / 256)] per projection block: its box of tiles (x0, y0,
+                            //   width, area; area kAggSpread = the fallback)
+  uint32_t* agg_off;        // [ceil(n / 256) x kAggCap] the block's offset among each tile's
+                            //   aggregated pairs (returned by the projection's reservation)
   uint32_t* tile_start;     // [n_tiles + 1]
   uint32_t* tile_cursor;    // [n_tiles]
   unsigned long long* pairs;      // [pair_cap]  (depth_key << 32 | input index)
@@ -165,6 +171,7 @@ constexpr int GS_STAGE_EVENTS = 7;  // profile events: before project .. after b
 constexpr int kSortLdsCap = 2048;  // largest tile list sorted by one workgroup (registers + LDS)
 constexpr uint32_t kSortRegCap = 256;  // largest tile list sorted in the registers of one wave
 constexpr size_t kBinLdsMax = 160 * 1024;  // LDS of one CU: chunk histograms up to 81920 tiles
+constexpr int kAggCap = 512;  // aggregated binning: tiles of a projection block's LDS box
 
 size_t bin_lds_bytes(int n_tiles);
 bool bin_lds_fits(int n_tiles);

@@ -143,7 +143,7 @@ void release(gs_renderer* r) {
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
-  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount})
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg})
     if (p) (void)hipFree(p);
   if (r->d_sh && r->owns_sh) (void)hipFree(r->d_sh);
   free_pairs(r);
@@ -800,7 +800,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.counters = (uint32_t*)r->d_zero;
   r->buf.tile_count = (uint32_t*)r->d_zero + 16;
   const size_t n_agg = (T + 63) / 64;
-  const size_t tiles_bytes = (T + 1 + 4 * T) * 4 + n_agg * 32 + 16 + T * 8 + 8 + T * 4;
+  const size_t tiles_bytes = (T + 1 + 4 * T) * 4 + n_agg * 32 + 16 + T * 8 + 8 + T * 4 + T * 4;
   if ((e = hipMalloc(&r->d_tiles, tiles_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(tiles)"));
   poison(r->d_tiles, tiles_bytes, "tiles");
   r->buf.tile_start = (uint32_t*)r->d_tiles;
@@ -813,9 +813,11 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   // scan resets them)
   r->buf.tile_cnt64 = (unsigned long long*)(((uintptr_t)(r->buf.tile_agg + 2 * n_agg) + 7) & ~(uintptr_t)7);
   r->buf.tile_ref = (uint32_t*)(r->buf.tile_cnt64 + T);
+  r->buf.tile_fb = r->buf.tile_ref + T;
   if ((e = hipMemset(r->d_tiles, 0, (T + 1 + 4 * T) * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(tiles)"));
   if ((e = hipMemset(r->buf.tile_cnt64, 0, T * 8)) != hipSuccess) return fail(hip_fail(e, "hipMemset(tile counters)"));
+  if ((e = hipMemset(r->buf.tile_fb, 0, T * 4)) != hipSuccess) return fail(hip_fail(e, "hipMemset(tile counters)"));
 
   // binning mode: chunked LDS histograms unless the band's tile grid is too
   // large for one CU's LDS (or the caller asks for the global-atomic path)
@@ -853,6 +855,14 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       const char* agg_env = std::getenv("GSPLAT_BIN_AGG");
       r->bin_agg_mode = agg_env ? (std::strcmp(agg_env, "0") == 0 ? 0 : 1) : -1;
       r->bin_agg = r->bin_agg_mode != 0 && fixed_cs == nullptr;
+      if (r->bin_agg) {  // per projection block: its tile box and its offsets in each tile
+        const size_t nb = (nn + 255) / 256;
+        const size_t agg_bytes = nb * 16 + nb * (size_t)gsk::kAggCap * 4;
+        if ((e = hipMalloc(&r->d_agg, agg_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(agg boxes)"));
+        poison(r->d_agg, agg_bytes, "agg");
+        r->buf.agg_box = (uint4*)r->d_agg;
+        r->buf.agg_off = (uint32_t*)((char*)r->d_agg + nb * 16);
+      }
       if ((e = hipMalloc(&r->d_chunk, r->chunk_entries * 4)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
       poison(r->d_chunk, r->chunk_entries * 4, "chunk");
