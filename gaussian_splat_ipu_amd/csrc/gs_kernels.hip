@@ -809,11 +809,18 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
 // workgroup of 1024 threads, rounds of 8192 tiles (8 per thread in
 // registers); the histogram (reference lengths) and the counters go straight
 // to the mapped host mirror and, in a row-band group, to the frame's footer.
+// the aggregated scan's queues: 0 small (<= 256 keys), 1..3 medium with
+// >= 1024, >= 512, > 256 keys, 4 big (> 2048)
+constexpr int kAggQueues = 5;
+__device__ __forceinline__ int agg_queue(uint32_t L) {
+  return L <= kSortRegCap ? 0 : (L > (uint32_t)kSortLdsCap ? 4 : (L >= 1024u ? 1 : (L >= 512u ? 2 : 3)));
+}
+
 __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffers b) {
   // per wave of a round: pair sum, reference sum, queue counts; per wave the
   // exclusive bases (computed by lanes 0..15 of wave 0), and the round totals
-  __shared__ unsigned long long wsum[16], wref[16], wbase[16];
-  __shared__ uint32_t wq[16], wqb[3][16], wvis[16], wmax[16];
+  __shared__ unsigned long long wsum[16], wref[16], wbase[16], wq[16];
+  __shared__ uint32_t wqb[kAggQueues][16], wvis[16], wmax[16];
   __shared__ unsigned long long s_tot;
   __shared__ uint32_t s_qt[3];
   __shared__ uint32_t s_c[8192];  // a round's binned counts (striped in, blocked out)
@@ -837,7 +844,8 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     for (int d = 32; d > 0; d >>= 1) vsum += __shfl_xor(vsum, d, 64);
     if (lane == 0) wvis[wave] = vsum;
   }
-  // (lanes 0..15 of wave 0) the running bases over the rounds
+  // (lanes 0..15 of wave 0) the running bases over the rounds: pairs,
+  // reference pairs, small / medium / big queue lengths
   unsigned long long carry = 0, rcarry = 0;
   uint32_t qcarry[3] = {0u, 0u, 0u};
   uint32_t mx = 0;
@@ -876,22 +884,19 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     uint32_t v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = s_c[tid * 8 + j];
-    unsigned long long sum = 0;
-    uint32_t q = 0;
+    unsigned long long sum = 0, q = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t c = v[j];
       sum += c;
       mx = max(mx, c);
-      const int cl = sort_class(c);
-      if (i0 + j < T) q += cl == 0 ? 1u : (cl == 1 ? (1u << 10) : (1u << 20));
+      if (i0 + j < T) q += 1ull << (10 * agg_queue(c));
     }
-    unsigned long long inc = sum;
-    uint32_t qinc = q;
+    unsigned long long inc = sum, qinc = q;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const unsigned long long o = __shfl_up(inc, d, 64);
-      const uint32_t oq = __shfl_up(qinc, d, 64);
+      const unsigned long long oq = __shfl_up(qinc, d, 64);
       if (lane >= d) {
         inc += o;
         qinc += oq;
@@ -906,35 +911,47 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     if (lane == 0) wref[wave] = rsum;
     __syncthreads();
     if (tid < 16) {  // exclusive scan over the 16 waves
-      const unsigned long long ws = wsum[tid];
-      const uint32_t wqv = wq[tid];
-      uint32_t qk[3] = {wqv & 1023u, (wqv >> 10) & 1023u, (wqv >> 20) & 1023u};
-      unsigned long long si = ws, ri = wref[tid];
-      uint32_t qi[3] = {qk[0], qk[1], qk[2]};
+      const unsigned long long ws = wsum[tid], wqv = wq[tid];
+      unsigned long long si = ws, ri = wref[tid], qi = wqv;  // (queue counts: 5 fields of 10 bits, <= 512 each per wave)
+      uint32_t qk[kAggQueues];
+#pragma unroll
+      for (int k = 0; k < kAggQueues; ++k) qk[k] = (uint32_t)(wqv >> (10 * k)) & 1023u;
+      uint32_t qs[kAggQueues];  // (inclusive scans of the 16 waves' counts; a field can pass 1023 here)
+#pragma unroll
+      for (int k = 0; k < kAggQueues; ++k) qs[k] = qk[k];
 #pragma unroll
       for (int d = 1; d < 16; d <<= 1) {
         const unsigned long long o = __shfl_up(si, d, 64), orr = __shfl_up(ri, d, 64);
-        uint32_t oq[3];
+        uint32_t oq[kAggQueues];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) oq[k] = __shfl_up(qi[k], d, 64);
+        for (int k = 0; k < kAggQueues; ++k) oq[k] = __shfl_up(qs[k], d, 64);
         if (tid >= d) {
           si += o;
           ri += orr;
 #pragma unroll
-          for (int k = 0; k < 3; ++k) qi[k] += oq[k];
+          for (int k = 0; k < kAggQueues; ++k) qs[k] += oq[k];
         }
       }
+      (void)qi;
       wbase[tid] = carry + si - ws;
+      uint32_t qt[kAggQueues];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) wqb[k][tid] = qcarry[k] + qi[k] - qk[k];
+      for (int k = 0; k < kAggQueues; ++k) qt[k] = __shfl(qs[k], 15, 64);
+      // queue bases of this round: small, big, then the medium lists longest
+      // first (>= 1024, >= 512, > 256 keys: the sort, and a band's
+      // longest-first blend, start the heaviest lists first)
+      const uint32_t mb0 = qcarry[1], mb1 = mb0 + qt[1], mb2 = mb1 + qt[2];
+      wqb[0][tid] = qcarry[0] + qs[0] - qk[0];
+      wqb[1][tid] = mb0 + qs[1] - qk[1];
+      wqb[2][tid] = mb1 + qs[2] - qk[2];
+      wqb[3][tid] = mb2 + qs[3] - qk[3];
+      wqb[4][tid] = qcarry[2] + qs[4] - qk[4];
       const unsigned long long tot = __shfl(si, 15, 64), rtot = __shfl(ri, 15, 64);
-      uint32_t qt[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) qt[k] = __shfl(qi[k], 15, 64);
       carry += tot;
       rcarry += rtot;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) qcarry[k] += qt[k];
+      qcarry[0] += qt[0];
+      qcarry[1] += qt[1] + qt[2] + qt[3];
+      qcarry[2] += qt[4];
       if (tid == 0) {
         s_tot = carry;
 #pragma unroll
@@ -943,10 +960,10 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     }
     __syncthreads();
     unsigned long long run = wbase[wave] + inc - sum;
-    const uint32_t qx = qinc - q;  // this lane's exclusive counts in the wave
-    uint32_t sml = wqb[0][wave] + (qx & 1023u);
-    uint32_t med = wqb[1][wave] + ((qx >> 10) & 1023u);
-    uint32_t big = wqb[2][wave] + ((qx >> 20) & 1023u);
+    const unsigned long long qx = qinc - q;  // this lane's exclusive counts in the wave
+    uint32_t qpos[kAggQueues];
+#pragma unroll
+    for (int k = 0; k < kAggQueues; ++k) qpos[k] = wqb[k][wave] + ((uint32_t)(qx >> (10 * k)) & 1023u);
     __syncthreads();  // (every thread has read its counts from s_c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -954,11 +971,12 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       const uint32_t c = v[j];
       s_c[tid * 8 + j] = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);  // the tile start
       if (i < T) {
-        const int cl = sort_class(c);
-        if (cl == 0) b.small_tiles[sml++] = (uint32_t)i;
-        if (cl == 1) b.medium_tiles[med++] = (uint32_t)i;
-        if (b.tile_big) b.tile_big[i] = cl == 2 ? big : 0xFFFFFFFFu;
-        if (cl == 2) b.big_tiles[big++] = (uint32_t)i;
+        const int qq = agg_queue(c);
+        const uint32_t pos = qpos[qq]++;
+        if (qq == 0) b.small_tiles[pos] = (uint32_t)i;
+        if (qq >= 1 && qq <= 3) b.medium_tiles[pos] = (uint32_t)i;
+        if (b.tile_big) b.tile_big[i] = qq == 4 ? pos : 0xFFFFFFFFu;
+        if (qq == 4) b.big_tiles[pos] = (uint32_t)i;
       }
       run += c;
     }
