@@ -3280,9 +3280,12 @@ void launch_sort_tiles(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
   if (waves == 0) return;
-  if (fp.blend_persist > 0 && fp.blend_bqw == 4 && !fp.fast_exp) {
+  if (fp.blend_persist > 0 && fp.blend_bqw == 4) {
     const unsigned g = (unsigned)std::min<long>(fp.blend_persist, fp.n_tiles);
-    gs_blend_persist_kernel<4, false><<<g, 64 * kBlendPersistWaves, 0, s>>>(fp, b);
+    if (fp.fast_exp)
+      gs_blend_persist_kernel<4, true><<<g, 64 * kBlendPersistWaves, 0, s>>>(fp, b);
+    else
+      gs_blend_persist_kernel<4, false><<<g, 64 * kBlendPersistWaves, 0, s>>>(fp, b);
     return;
   }
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
