@@ -2635,6 +2635,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // -------------------------------------------------------------------- blend
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+#ifndef GS_BLEND_PACKED
+#define GS_BLEND_PACKED 1
+#endif
 
 // v_writelane_b32 x2: lanes L and L + 1 of v take the wave-uniform words lo,
 // hi -- a ballot's two halves.  The s_nop gives the two wait states a VALU
@@ -2721,9 +2724,19 @@ enum BlendExp { kExpExact = 0, kExpInRange = 1, kExpHw = 2 };
 template <int EXP>
 __device__ __forceinline__ float blend_power_exp(const Px& q, const float4& r0, const float4& r1,
                                                  float& power) {
+#if GS_BLEND_PACKED
+  // the two axes' terms as packed fp32 pairs (v_pk_add / v_pk_mul: one
+  // instruction per pair, each half rounded as the scalar op): the same
+  // operations in the same order, (h0 dx) dx + (h2 dy) dy - (k1 dx) dy
+  const f32x2 d = f32x2{r0.x, r0.y} - q.p;
+  const f32x2 t = f32x2{r0.z, r0.w} * d;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
+  const f32x2 u = t * d;
+  power = (u.x + u.y) - r1.x * d.x * d.y;
+#else
   const float dx = r0.x - q.p.x, dy = r0.y - q.p.y;
   const float h0 = r0.z, h2 = r0.w, k1 = r1.x;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
   power = (h0 * dx * dx + h2 * dy * dy) - k1 * dx * dy;
+#endif
   return EXP == kExpHw ? gs_expf_hw(power) : (EXP == kExpInRange ? gs_expf_inrange(power) : gs_expf(power));
 }
 
@@ -2739,10 +2752,16 @@ __device__ __forceinline__ void blend_composite(Px& q, float power, float e, con
   const bool brk = hit && test_T < 0.0001f;  // break (codelets.cpp:406-408)
   const bool upd = hit && !brk;
   if (__builtin_expect(upd, 0)) {
+#if GS_BLEND_PACKED
+    // colour += gCont * alpha * T, two channels per packed op
+    q.c01 = q.c01 + (f32x2{r1.z, r1.w} * alpha) * q.T;
+    q.c23 = q.c23 + (f32x2{r2.x, op} * alpha) * q.T;
+#else
     q.c01.x = q.c01.x + (r1.z * alpha) * q.T;  // colour += gCont * alpha * T
     q.c01.y = q.c01.y + (r1.w * alpha) * q.T;
     q.c23.x = q.c23.x + (r2.x * alpha) * q.T;
     q.c23.y = q.c23.y + (op * alpha) * q.T;
+#endif
     q.T = test_T;
   }
   q.done = q.done || brk;

@@ -20,3 +20,4 @@ for f in 3 4 6; do
   bands $O/q8f$f.jsonl
 done
 echo "== done $(date +%T)"
+bash tools/gpu_r4_packed.sh
