@@ -827,6 +827,20 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   __shared__ uint32_t s_a[8192];  // ... their aggregated parts
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // a round's counters, read striped (coalesced: lane-consecutive tiles);
+  // the first round's are issued before the V loads (one memory round trip
+  // for both)
+  unsigned long long vs[8];
+  uint32_t fb[8];
+  auto load_round = [&](int r0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = r0 + j * 1024 + tid;
+      vs[j] = i < T ? b.tile_cnt64[i] : 0ull;
+      fb[j] = i < T ? b.tile_fb[i] : 0u;
+    }
+  };
+  load_round(0);
   // V = the projection workgroups' counts, reduced per wave at once (kept
   // live across the rounds they were spilled)
   {
@@ -856,14 +870,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     // transposed through LDS so each thread scans 8 consecutive tiles
     unsigned long long rsum = 0;
     {
-      unsigned long long vs[8];
-      uint32_t fb[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = r0 + j * 1024 + tid;
-        vs[j] = i < T ? b.tile_cnt64[i] : 0ull;
-        fb[j] = i < T ? b.tile_fb[i] : 0u;
-      }
+      if (r0 > 0) load_round(r0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = r0 + j * 1024 + tid;
@@ -1005,27 +1012,37 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       m = max(m, wmax[w]);
     }
     const unsigned long long total = T > 0 ? s_tot : 0ull;
-    b.counters[0] = T > 0 ? s_qt[2] : 0u;
-    b.counters[1] = 0;
-    b.counters[2] = vis;
-    b.counters[3] = total > fp.pair_cap ? 1u : 0u;
+    // the frame counters from registers (no read-back of what was just
+    // stored), 16-B stores
+    const uint4 c0 = make_uint4(T > 0 ? s_qt[2] : 0u, 0u, vis, total > fp.pair_cap ? 1u : 0u);
+    const uint4 c1 = make_uint4(m, (uint32_t)total, (uint32_t)(total >> 32), T > 0 ? s_qt[1] : 0u);
+    // (tid 0 ran the wave scans: its rcarry is the frame's)
+    const uint4 c2 = make_uint4(0u, T > 0 ? s_qt[0] : 0u, (uint32_t)rcarry, (uint32_t)(rcarry >> 32));
+    const uint4 c3 = make_uint4(0u, 0u, 0u, 0u);
     if (total > fp.pair_cap) {  // sticky until the host's sync
       *b.host_sticky = 1u;
       if (b.group_sticky) *b.group_sticky = 1u;
     }
-    b.counters[4] = m;
-    b.counters[5] = (uint32_t)total;
-    b.counters[6] = (uint32_t)(total >> 32);
-    b.counters[7] = T > 0 ? s_qt[1] : 0u;
-    b.counters[8] = 0;
-    b.counters[9] = T > 0 ? s_qt[0] : 0u;
-    b.counters[10] = (uint32_t)rcarry;  // (tid 0 ran the wave scans: its rcarry is the frame's)
-    b.counters[11] = (uint32_t)(rcarry >> 32);
-    for (int k = 12; k < 16; ++k) b.counters[k] = 0;
+    uint4* const cv = reinterpret_cast<uint4*>(b.counters);
+    cv[0] = c0;
+    cv[1] = c1;
+    cv[2] = c2;
+    cv[3] = c3;
     b.tile_start[T] = (uint32_t)(total < 0xFFFFFFFFull ? total : 0xFFFFFFFFull);
-    for (int k = 0; k < 16; ++k) b.host_counters[k] = b.counters[k];
-    if (b.footer)
-      for (int k = 0; k < 16; ++k) b.footer[k] = b.counters[k];
+    if (b.footer) {
+      uint4* const fv = reinterpret_cast<uint4*>(b.footer);
+      fv[0] = c0;
+      fv[1] = c1;
+      fv[2] = c2;
+      fv[3] = c3;
+    }
+    // the host mirror: written here only when no emit follows (the emit's
+    // first workgroup copies it, off this single-workgroup kernel's path)
+    if (fp.n == 0) {
+      const uint32_t cc[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                               c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+      for (int k = 0; k < 16; ++k) b.host_counters[k] = cc[k];
+    }
   }
 }
 
@@ -1041,6 +1058,9 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
   __shared__ uint32_t cnt[kAggCap];
   const int blk = blockIdx.x;
   const int i = blk * 256 + (int)threadIdx.x;
+  // the scan's frame counters to the mapped host mirror (the next frames'
+  // big-list hint, the host's counters at sync)
+  if (blk == 0 && threadIdx.x < 16) b.host_counters[threadIdx.x] = b.counters[threadIdx.x];
   if (fp.band_cull && b.block_rendered[blk] == 0u) return;  // (uniform) culled block: nothing binned
   const uint4 box = b.agg_box[blk];
   if (box.w == 0u) return;  // (uniform) nothing binned
