@@ -2843,53 +2843,29 @@ __device__ __forceinline__ void blend_count_store(const FrameParams& fp, const B
   }
 }
 
-// The persistent blend's look-ahead: a (tile, block) item's list span and
-// the list entries of its first two batches, loaded while the wave still
-// blends the item before it (the prefix blend only, not the continuation).
-struct BlendPre {
-  int tile;           // -1: no item
-  uint32_t s, L;      // the walked span of the tile's list
-  uint32_t Lfull;     // the tile's whole list (lazy big lists: L is the sorted prefix)
-  uint32_t jb;        // the tile's big-list slot (~0: none)
-  uint32_t g0, g1;    // list entries of batches 0 and 1 (this lane's)
-};
-
+// A list entry.  With the sort in the blend (FrameParams::blend_sort) the
+// lists were written by this launch's own workgroups: agent-scope loads, so
+// a line of a neighbouring tile's list that another workgroup of the CU
+// pulled into the vector L1 before this tile's list was written is never
+// read from there.
 __device__ __forceinline__ uint32_t blend_idx(const FrameParams& fp, const uint32_t* list, uint32_t L, uint32_t k) {
   uint32_t g = 0xFFFFFFFFu;
-  if (k < L) g = list[k];
+  if (k < L) g = fp.blend_sort ? __hip_atomic_load(list + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : list[k];
   return g < (uint32_t)fp.n ? g : 0xFFFFFFFFu;  // defensive: never read past the records
 }
 
-__device__ __forceinline__ BlendPre blend_prefetch(const FrameParams& fp, const Buffers& b, int wid, bool ok) {
-  BlendPre it;
-  it.tile = -1;
-  it.s = it.L = it.Lfull = 0u;
-  it.jb = 0xFFFFFFFFu;
-  it.g0 = it.g1 = 0xFFFFFFFFu;
-  const int slot = wid / fp.chunks_per_tile;
-  if (!ok || slot >= fp.n_tiles) return it;
-  int tile = slot;
-  if (fp.blend_lpt) {
-    const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
-    tile = (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
-  }
-  it.tile = tile;
-  tile_segment(fp, b, tile, it.s, it.L);
-  it.Lfull = it.L;
-  if (fp.lazy) it.jb = b.tile_big[tile];
-  if (it.jb != 0xFFFFFFFFu) it.L = min(b.big_len[it.jb], it.L);
-  const int lane = threadIdx.x & 63;
-  it.g0 = blend_idx(fp, b.list + it.s, it.L, (uint32_t)lane);
-  it.g1 = blend_idx(fp, b.list + it.s, it.L, 64u + (uint32_t)lane);
-  return it;
+// the tile of blend slot `slot`: the tile order, or (blend_lpt) the sort
+// queues' order -- big, medium (longest first), then small and empty lists
+__device__ __forceinline__ int blend_tile_of(const FrameParams& fp, const Buffers& b, int slot) {
+  if (!fp.blend_lpt) return slot;
+  const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
+  return (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
 }
 
-// wid = the wave's (tile slot, 8x8 block) item; wave = its LDS staging slot
-// (of WPG: the waves of the workgroup); pre: the item's look-ahead (the
-// persistent blend), nullptr = load it here
-template <int BQW, bool HWEXP, int WPG = GS_BLEND_WPG>
-__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wave, int wid,
-                                           const BlendPre* pre = nullptr) {
+// wid = the wave's (tile slot, 8x8 block) item; st: the wave's LDS staging
+// of one batch (3 x 64 float4)
+template <int BQW, bool HWEXP>
+__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
   if (slot >= fp.n_tiles) return;
@@ -2911,15 +2887,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   // where the tile order puts them (8 bands: blend 35.7 -> 29.3 us).  The
   // full frame keeps the tile order (neighbouring tiles share records in L2:
   // 75.1 against 76.1 us in queue order).
-  int tile = slot;
-  if (pre) {
-    tile = pre->tile;
-  } else if (fp.blend_cont) {
-    tile = (int)b.big_tiles[jb];
-  } else if (fp.blend_lpt) {
-    const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
-    tile = (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
-  }
+  const int tile = fp.blend_cont ? (int)b.big_tiles[jb] : blend_tile_of(fp, b, slot);
   const int lane = threadIdx.x & 63;
   const int myq = lane >> 2;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
@@ -2965,19 +2933,12 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
 
   uint32_t s, L;
   uint32_t k0 = 0u, Lfull;
-  if (pre) {
-    s = pre->s;
-    L = pre->L;
-    Lfull = pre->Lfull;
-    jb = pre->jb;
-  } else {
-    tile_segment(fp, b, tile, s, L);
-    Lfull = L;
-    // lazy big list: this pass composites the sorted prefix [0, big_len), the
-    // continuation the rest [big_len, L) from the saved state
-    if (fp.lazy && !fp.blend_cont) jb = b.tile_big[tile];
-  }
-  if (!pre && jb != 0xFFFFFFFFu) {
+  tile_segment(fp, b, tile, s, L);
+  Lfull = L;
+  // lazy big list: this pass composites the sorted prefix [0, big_len), the
+  // continuation the rest [big_len, L) from the saved state
+  if (fp.lazy && !fp.blend_cont) jb = b.tile_big[tile];
+  if (jb != 0xFFFFFFFFu) {
     const uint32_t np = min(b.big_len[jb], L);
     if (fp.blend_cont) {
       // the list now holds, from its start, the keys past the prefix whose
@@ -2996,10 +2957,6 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   const uint32_t* __restrict__ list = b.list + s + k0;
   L -= k0;
 
-  // wave-private staging of one batch of 64 records (48 B each with the colour) in LDS
-  __shared__ float4 s_rec[WPG][3][64];
-  float4(*const st)[64] = s_rec[wave];
-
   // software pipeline: records of batch `base`, index of batch `base + 64`
   auto load_idx = [&](uint32_t k) -> uint32_t { return blend_idx(fp, list, L, k); };
   // a record (32 B) and its colour + opacity (the scene's, or gs_set_sh's
@@ -3014,9 +2971,9 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
     r2 = make_float4(c.z, c.w, t.z, t.w);
   };
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
-  uint32_t g_cur = pre ? pre->g0 : load_idx(lane);
+  uint32_t g_cur = load_idx(lane);
   if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
-  uint32_t g_next = pre ? pre->g1 : load_idx(64 + lane);
+  uint32_t g_next = load_idx(64 + lane);
 
   uint32_t staged = 0;  // records staged (profiled frames)
   for (uint32_t base = 0; base < L; base += 64) {
@@ -3153,56 +3110,60 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
 
+// The sort inside the blend (FrameParams::blend_sort; one workgroup = the
+// four 8x8 blocks of one 16x16 tile): the workgroup first sorts its tile's
+// list -- as gs_sort_tiles_kernel would: <= 64 keys in wave 0's registers,
+// <= kSortLdsCap by the four waves (64- or 128-key register runs, then
+// merge-path levels in LDS), equal depths re-sorted by input index, a list
+// > kSortLdsCap radix-sorted here unless the big-list launches took it --
+// then its four waves blend it.  No sort launch, and the list is read back
+// while it is still in L2.  The LDS of the sort is then reused as the
+// waves' record staging.
+constexpr int kBlendLdsWords = 2 * kSortLdsCap;  // u32 words (16 KB)
+static_assert(GS_BLEND_WPG == 4, "blend_sort: one workgroup per 16x16 tile (the renderer's chunks_per_tile == 4)");
+static_assert(kBlendLdsWords * 4 >= GS_BLEND_WPG * 3 * 64 * 16, "the staging fits the sort's LDS");
+static_assert(kBlendLdsWords >= 8 * 256 + 256 + 4 * 256, "the radix histograms fit the sort's LDS");
+
+__device__ __forceinline__ void blend_sort_tile(const FrameParams& fp, const Buffers& b, int tile,
+                                                unsigned long long* keys) {
+  uint32_t s, L;
+  tile_segment(fp, b, tile, s, L);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (L > (uint32_t)kSortLdsCap) {
+    // a big list: sorted by the big-list launches (big_separate), else here
+    if (!fp.big_separate) {
+      uint32_t* const hist = (uint32_t*)keys;
+      radix_sort_tile<256, 4>(fp, b, tile, hist, hist + 8 * 256, (uint32_t(*)[256])(hist + 9 * 256));
+    }
+    return;
+  }
+  if (L <= 64u) {
+    if (wave == 0) wave_sort_list(b, b.pairs + s, s, L, lane, keys);
+    return;
+  }
+  const bool ok = L <= kSortRegCap ? merge_sort_tile<256, 1, kOutDevice>(b, s, L, keys)
+                                   : merge_sort_tile<256, 2, kOutDevice>(b, s, L, keys);
+  if (!ok) {
+    __syncthreads();  // a long run of equal depths: again with input-index keys
+    merge_sort_tile<256, 2, kOutInput, kSrcRekey>(b, s, L, keys);
+  }
+}
+
 // HWEXP: GS_FLAG_FAST_EXP (its own kernel: the default path's code is unchanged)
 template <int BQW, bool HWEXP>
-__device__ __forceinline__ void blend_body(const FrameParams& fp, const Buffers& b, int blk) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_blend_kernel(FrameParams fp, Buffers b) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  blend_wave<BQW, HWEXP>(fp, b, wave, blk * GS_BLEND_WPG + wave);
-}
-
-template <int BQW, bool HWEXP>
-__global__ __launch_bounds__(256) void gs_blend_kernel(FrameParams fp, Buffers b) {
-  blend_body<BQW, HWEXP>(fp, b, blockIdx.x);
-}
-
-// GSPLAT_BLEND_PERSIST=G (A/B): G resident workgroups of 16 waves; workgroup
-// k owns the tiles k, k + G, k + 2G, ... (spread over the frame, so every
-// workgroup gets a similar load) and its waves take that range's (tile,
-// block) items one after another from an LDS counter -- no workgroup
-// dispatch per item, and no contended global counter (the round-3
-// persistent blend's single returning atomic serialised).
-constexpr int kBlendPersistWaves = 16;
-
-template <int BQW, bool HWEXP>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_blend_persist_kernel(FrameParams fp, Buffers b) {
-  __shared__ uint32_t s_next;
-  if (threadIdx.x == 0) s_next = 0u;
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int G = (int)gridDim.x, cpt = fp.chunks_per_tile;
-  const int tiles_wg = fp.n_tiles > (int)blockIdx.x ? (fp.n_tiles - (int)blockIdx.x + G - 1) / G : 0;
-  const uint32_t items_wg = (uint32_t)(tiles_wg * cpt);
-  auto take = [&]() -> uint32_t {
-    uint32_t j = 0u;
-    if ((threadIdx.x & 63) == 0) j = atomicAdd(&s_next, 1u);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl((int)j, 0, 64));
-  };
-  auto wid_of = [&](uint32_t j) -> int {
-    const int m = (int)j / cpt, chunk = (int)j - m * cpt;
-    return ((int)blockIdx.x + G * m) * cpt + chunk;
-  };
-  // the next item's list span and first list entries are loaded before the
-  // current item is blended: its three dependent round trips (tile bounds,
-  // list entries, records) shrink to the records'
-  uint32_t j = take();
-  BlendPre cur = blend_prefetch(fp, b, wid_of(j), j < items_wg);
-  while (j < items_wg) {
-    const uint32_t jn = take();
-    const BlendPre nxt = blend_prefetch(fp, b, wid_of(jn), jn < items_wg);
-    blend_wave<BQW, HWEXP, kBlendPersistWaves>(fp, b, wave, wid_of(j), &cur);
-    j = jn;
-    cur = nxt;
+  if (fp.blend_sort) {
+    const int slot = (int)blockIdx.x;  // (chunks_per_tile == GS_BLEND_WPG)
+    if (slot >= fp.n_tiles) return;
+    blend_sort_tile(fp, b, blend_tile_of(fp, b, slot), reinterpret_cast<unsigned long long*>(lds));
+    // the list's stores are done (s_waitcnt in the barrier) before any wave
+    // reads it, and the sort's LDS is free for the staging
+    __syncthreads();
   }
+  blend_wave<BQW, HWEXP>(fp, b, blockIdx.x * GS_BLEND_WPG + wave,
+                         reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
 }
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
@@ -3212,9 +3173,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 // counters load, 4 resident per CU).
 template <bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_cont_kernel(FrameParams fp, Buffers b) {
+  __shared__ float4 s_rec[GS_BLEND_WPG][3][64];
   if (fp.big_pass == 2 && b.counters[1] == 0u) return;  // no list outlived its window
+  const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nblk = (int)((b.counters[0] * (uint32_t)fp.chunks_per_tile + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
-  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) blend_body<4, HWEXP>(fp, b, blk);
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x)
+    blend_wave<4, HWEXP>(fp, b, blk * GS_BLEND_WPG + wave, s_rec[wave]);
 }
 
 
@@ -3311,7 +3275,7 @@ void launch_sort_big(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 }
 
 void launch_sort_tiles(const FrameParams& fp, const Buffers& b, hipStream_t s) {
-  if (fp.n_tiles == 0) return;
+  if (fp.n_tiles == 0 || fp.blend_sort) return;  // (blend_sort: each blend workgroup sorts its tile)
   // big + medium + ceil(small / waves) <= n_tiles + 1 workgroups do work
   gs_sort_tiles_kernel<<<fp.n_tiles + (fp.n_tiles + 3) / 4, 256, 0, s>>>(fp, b);
 }
@@ -3319,14 +3283,6 @@ void launch_sort_tiles(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const long waves = (long)fp.n_tiles * fp.chunks_per_tile;
   if (waves == 0) return;
-  if (fp.blend_persist > 0 && fp.blend_bqw == 4) {
-    const unsigned g = (unsigned)std::min<long>(fp.blend_persist, fp.n_tiles);
-    if (fp.fast_exp)
-      gs_blend_persist_kernel<4, true><<<g, 64 * kBlendPersistWaves, 0, s>>>(fp, b);
-    else
-      gs_blend_persist_kernel<4, false><<<g, 64 * kBlendPersistWaves, 0, s>>>(fp, b);
-    return;
-  }
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
   if (fp.fast_exp) {

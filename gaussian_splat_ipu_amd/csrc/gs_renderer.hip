@@ -211,7 +211,9 @@ gsk::FrameParams make_params(const gs_renderer* r) {
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
   if (r->env_blend_lpt >= 0) fp.blend_lpt = r->env_blend_lpt;  // (A/B)
-  fp.blend_persist = r->env_blend_persist > 0 ? r->env_blend_persist : 0;  // (A/B: GSPLAT_BLEND_PERSIST=G)
+  // the tile sort inside the blend's workgroups (16x16 tiles: one workgroup
+  // per tile; GSPLAT_BLEND_SORT=0 keeps the sort launch, A/B)
+  fp.blend_sort = (r->env_blend_sort != 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4) ? 1 : 0;
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
@@ -642,7 +644,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) r->env_blend_lpt = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) r->env_mean_w1 = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_BLEND_PERSIST")) r->env_blend_persist = std::max(0, std::min(4096, std::atoi(ev)));
+  if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
@@ -1082,6 +1084,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
     gsk::FrameParams fp = r->last_fp;
     fp.pair_cull = 0;
     fp.rect8 = 0;
+    fp.blend_sort = 0;  // (no blend here: the sort launch sorts the lists)
     gsk::Buffers bb = r->buf;
     bb.footer = nullptr;        // (a group's all-gather slot belongs to the frame)
     bb.group_sticky = nullptr;  // (this re-binning's overflow is handled here, not by the group)
