@@ -1,3 +1,3 @@
 #!/bin/bash
 # (superseded by gpu_r4_bsort.sh, which runs the same sweep after its A/B)
-exec bash "$(dirname "$0")/gpu_r4_bsort.sh"
+bash "$(dirname "$0")/gpu_r4_bsort.sh"
