@@ -135,7 +135,7 @@ def measured_copy_peak(torch, min_s: float = 0.06) -> float:
 
 
 def survey_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int, st: dict,
-                 share: float = 1.0, band: bool = False) -> float:
+                 share: float = 1.0, band: bool = False, sort_in_blend: bool = False) -> float:
     """Algorithmic HBM bytes per launch by SURVEY §8(d)'s terms -- the
     roofline's `achieved` (DESIGN.md §4): project N x (56 read + 52 write);
     scan N x 8 plus the tile ranges P x 8 + T x 8; emit N x 12 + P x 12; sort
@@ -144,20 +144,26 @@ def survey_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_con
     gs_frame_stats.blend_records: a wave stops when its pixels have saturated;
     lazy big lists stage their sorted prefixes only).  P = the binned pairs;
     share / band = a row band's share of the frame (band cull: every
-    Gaussian's 16-B cull record, the band's Gaussians in full)."""
+    Gaussian's 16-B cull record, the band's Gaussians in full).
+    sort_in_blend (gs_frame_stats.paths GS_PATH_BLEND_SORT): the blend
+    kernel's workgroups sort the lists of <= 2048 keys themselves, so that
+    sort pass's P x 24 is the blend launch's and the sort stage keeps the big
+    lists' (st["big_pairs"])."""
     rendered = st["n_rendered"] * share
+    in_blend = P - st["big_pairs"] if sort_in_blend else 0
     return {
         "project": n * 16 + rendered * 108 if band else n * 108,
         "scan": n * 8 + P * 8 + T * 8,
         "emit": n * 12 + P * 12,
-        "sort": P * 24,
-        "blend": T * 8 + rec * (4 + 36) + px * (16 + 3),
+        "sort": (P - in_blend) * 24,
+        "blend": T * 8 + rec * (4 + 36) + px * (16 + 3) + in_blend * 24,
         "blend_cont": rec_cont * (4 + 36) + st["cont_keys"] * 24,
     }[kernel]
 
 
 def layout_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_cont: int, st: dict,
-                 n_chunks: int, rect_b: int, share: float = 1.0, band: bool = False) -> float:
+                 n_chunks: int, rect_b: int, share: float = 1.0, band: bool = False,
+                 sort_in_blend: bool = False) -> float:
     """HBM bytes per launch of the layouts the kernels actually move (DESIGN
     §3): the figure to hold against the PMC bytes of the same launch (reported
     beside survey_bytes, labelled).
@@ -167,9 +173,11 @@ def layout_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_con
     continuation staged; st = the frame stats (big-list pairs, prefix / window
     keys); rect_b = the bytes of a Gaussian's two rectangles (8 with 8-bit
     bounds, else 16); share / band = a row band's share of the frame's pairs
-    (the group)."""
+    (the group); sort_in_blend: the small / medium lists' sort runs in the
+    blend's workgroups (its bytes move from the sort stage to the blend)."""
     rendered = st["n_rendered"] * share
     big = st["big_pairs"]
+    in_blend = (P - big) * 12 if sort_in_blend else 0
     pre, win = st["big_prefix_keys"], st["big_window_keys"]
     if band:  # band cull: every Gaussian's 16-B cull record, the band's Gaussians in full
         project = n * 16 + rendered * (48 + 4 + 32) + n * rect_b
@@ -189,10 +197,10 @@ def layout_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_con
         # emit: the binned rectangle and depth key, its chunk row, the pairs
         "emit": n * (rect_b // 2 + 4) + chunk_matrix + P * 8,
         # small / medium lists: read the 8-B keys, write the 4-B list
-        "sort": (P - big) * 12 + big_sort,
+        "sort": (P - big) * 12 + big_sort - in_blend,
         # the tile's list bounds; per staged record its 4-B list entry, the
         # 32-B record and the 16-B colour + opacity; RGBA f32 + BGR8 per pixel
-        "blend": T * 8 + rec * (4 + 32 + 16) + px * (16 + 3),
+        "blend": T * 8 + rec * (4 + 32 + 16) + px * (16 + 3) + in_blend,
         # the continued records, and the window keys the continuation sorted
         "blend_cont": rec_cont * (4 + 32 + 16) + st["cont_keys"] * 12,
     }[kernel]
@@ -441,6 +449,8 @@ def main():
     # columns and band rows (FrameParams::rect8)
     rect_b = 8 if (fb.tiles_across <= 256 and fb.tiles_down <= 256) else 16
     rec, rec_cont = st_view["blend_records"], st_view["blend_cont_records"]
+    # the tile sort ran inside the blend's workgroups (gs_frame_stats.paths)
+    sib = bool(st_view.get("paths", 0) & 2)
     kern = {}
     for name, (avg_ms, cnt) in kt.items():
         if name == "gather":
@@ -451,9 +461,11 @@ def main():
             continue
         if name == "blend_cont" and (not cnt or not rec_cont):
             continue  # (no lazy continuation ran: its stage is two back-to-back events)
-        b = survey_bytes(name, T_b, P_b, a.n, px, rec, rec_cont, st_view, share if group else 1.0, group)
+        b = survey_bytes(name, T_b, P_b, a.n, px, rec, rec_cont, st_view, share if group else 1.0, group,
+                         sort_in_blend=sib)
         lb = layout_bytes(name, T_b, P_b, a.n, px, rec, rec_cont, st_view,
-                          0 if group else bench_chunks(a.n), rect_b, share if group else 1.0, group)
+                          0 if group else bench_chunks(a.n), rect_b, share if group else 1.0, group,
+                          sort_in_blend=sib)
         kern[name] = {
             "avg_ms": round(avg_ms, 5),
             "launches": int(cnt),
@@ -464,6 +476,8 @@ def main():
     if "blend" in kern:
         kern["blend"]["records_staged"] = int(rec)
         kern["blend"]["pairs_binned"] = int(P_b)
+        # pairs the blend's workgroups sorted (sort inside the blend), in its alg_bytes at 24 B
+        kern["blend"]["pairs_sorted"] = int(P_b - st_view["big_pairs"]) if sib else 0
     if "blend_cont" in kern:
         kern["blend_cont"]["records_staged"] = int(rec_cont)
         kern["blend_cont"]["lists"] = int(st_view["cont_lists"])

@@ -112,7 +112,7 @@ class FrameStats(C.Structure):
         ("band_stride", C.c_uint32),
         ("n_pairs_binned", C.c_uint64),
         ("bin_global", C.c_uint32),
-        ("reserved0", C.c_uint32),
+        ("paths", C.c_uint32),
         ("blend_records", C.c_uint64),
         ("blend_cont_records", C.c_uint64),
         ("cont_keys", C.c_uint64),

@@ -354,6 +354,7 @@ int parse_footers(Group* g, const uint32_t* h, const std::vector<uint32_t>& boun
     g->stats.n_pairs_binned = st.n_pairs_binned;
     g->stats.max_list = st.max_list;
     g->stats.n_big_tiles = st.n_big_tiles;
+    g->stats.paths = st.paths;
   }
   return rc;
 }

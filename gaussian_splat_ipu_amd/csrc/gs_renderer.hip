@@ -495,6 +495,9 @@ int finish_frame(gs_renderer* r) {
   r->stats.max_list = mx;
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
+  r->stats.paths = r->have_fp ? ((r->last_fp.bin_agg ? GS_PATH_BIN_AGG : 0u) |
+                                 (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u))
+                              : 0u;
   r->stats.blend_records = r->stats.blend_cont_records = r->stats.cont_keys = 0;
   r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = r->stats.cont_full_sorts = 0;
   r->stats.big_pairs = r->stats.big_prefix_keys = r->stats.big_window_keys = 0;

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 10
+#define GSPLAT_ABI_VERSION 11
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -168,7 +168,10 @@ typedef struct gs_frame_stats {
                               GS_FLAG_NO_PAIR_CULL)                   */
   uint32_t bin_global;    /* ABI 5: 1 = the global-atomic binning path (tile
                              grids beyond one CU's LDS, or GS_FLAG_BIN_GLOBAL) */
-  uint32_t reserved0;
+  uint32_t paths;         /* ABI 11: the last frame's binning / sort paths:
+                             bit 0 (GS_PATH_BIN_AGG) the aggregated binning,
+                             bit 1 (GS_PATH_BLEND_SORT) the tile sort inside
+                             the blend's workgroups (no tile-sort launch) */
   uint64_t blend_records;      /* ABI 8, GS_FLAG_PROFILE renderers (frames with
                                   stage events; else 0): tile-list records the
                                   blend read in the last frame, per tile the
@@ -195,6 +198,9 @@ typedef struct gs_frame_stats {
   uint64_t big_window_keys; /* ABI 9, profiled lazy frames: keys kept for the
                              continuation's windows                        */
 } gs_frame_stats;
+
+/* gs_frame_stats.paths bits (ABI 11) */
+enum { GS_PATH_BIN_AGG = 1, GS_PATH_BLEND_SORT = 2 };
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */
 enum {

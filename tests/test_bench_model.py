@@ -79,6 +79,10 @@ def test_survey_bytes_are_section_8d_terms():
     assert abs(sb("blend") - 92.86e6) < 0.01e6
     assert sb("blend_cont") == 77 * 40 + 1000 * 24
     assert sb("project", share=0.25, band=True) == n * 16 + 0.25 * n * 108
+    # the sort inside the blend: the small / medium lists' pass moves to the blend
+    st["big_pairs"] = 1000
+    assert sb("blend", sort_in_blend=True) == T * 8 + rec * 40 + px * 19 + (P - 1000) * 24
+    assert sb("sort", sort_in_blend=True) == 1000 * 24
 
 
 def test_launch_modes():
@@ -140,7 +144,8 @@ def test_committed_lines_use_the_survey_terms():
         if d["config"].get("bands") is None:
             T = d["frame"]["n_tiles"]
             px = W * H
-            assert k["alg_bytes"] == T * 8 + k["records_staged"] * 40 + px * 19, p
+            # (+ the pairs the blend's workgroups sorted, when the sort ran inside it)
+            assert k["alg_bytes"] == T * 8 + k["records_staged"] * 40 + px * 19 + k.get("pairs_sorted", 0) * 24, p
         r = d["roofline"]
         dk = d["kernels"][r["kernel"]]
         assert r["alg_bytes_per_launch"] == dk["alg_bytes"], p
