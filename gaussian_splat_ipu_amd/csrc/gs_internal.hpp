@@ -75,6 +75,8 @@ struct gs_renderer {
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
   void* d_lazy = nullptr;       // lazy big lists (16x16 tiles): per-tile tables + saved blend waves
   void* d_agg = nullptr;        // aggregated binning: per projection block its tile box and offsets
+  void* d_probe = nullptr;      // (GS_PROBE builds, GSPLAT_PROBE_FILE) the kernels' per-frame start / end ring
+  int probe_n = 0;              // frames recorded in it
   // GS_FLAG_LATTICE: the lattice-migration emulator's state (gs_lattice.hip)
   void* d_lat = nullptr;
   bool lattice = false;
@@ -103,7 +105,7 @@ struct gs_renderer {
   // A/B hooks, read once at gs_create (GSPLAT_BLEND_LPT 0 | 1, GSPLAT_MEAN_W1,
   // GSPLAT_RECT8: 0 turns the layout off; GSPLAT_BLEND_PERSIST = G resident
   // blend workgroups); -1 = unset
-  int env_blend_lpt = -1, env_mean_w1 = -1, env_rect8 = -1, env_blend_sort = 1;
+  int env_blend_lpt = -1, env_mean_w1 = -1, env_rect8 = -1, env_blend_sort = -1;
   uint8_t* own_bgr = nullptr;     // the renderer's BGR8 band buffer
   uint8_t* bgr_target = nullptr;  // gs_set_bgr8_target: frames write their BGR8 here instead
   uint8_t* last_bgr = nullptr;    // where the last enqueued frame wrote its BGR8

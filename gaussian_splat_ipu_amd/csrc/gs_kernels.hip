@@ -486,6 +486,28 @@ __device__ __forceinline__ void wave_minmax_u16x2(uint32_t& lo, uint32_t& hi) {
   }
 }
 
+#if GS_PROBE
+// per wave: the kernel's earliest start and latest end for the frame
+// (vector atomics on the probe ring; probe builds only)
+struct ProbeScope {
+  unsigned long long* p = nullptr;
+  __device__ ProbeScope(const FrameParams& fp, const Buffers& b, int k) {
+    if (b.probe && (threadIdx.x & 63) == 0) {
+      p = b.probe + 2 * ((size_t)(fp.probe_frame % kProbeFrames) * kProbeKernels + (size_t)k);
+      atomicMin(p, (unsigned long long)wall_clock64());
+    }
+  }
+  __device__ ~ProbeScope() {
+    if (p) atomicMax(p + 1, (unsigned long long)wall_clock64());
+  }
+};
+#define GS_PROBE_SCOPE(k) ProbeScope gs_probe_scope_(fp, b, k)
+#else
+#define GS_PROBE_SCOPE(k) ((void)0)
+#endif
+enum { kPrProject = 0, kPrAggScan, kPrAggEmit, kPrCount, kPrColscan, kPrScanMulti, kPrEmitChunk, kPrSortTiles,
+       kPrBlend, kPrBlendCont, kPrScan, kPrEmit, kPrBig };
+
 // ----------------------------------------------------- aggregated binning
 // FrameParams::bin_agg: the per-tile list lengths are summed by the
 // projection's own workgroups and the pairs emitted with one returning
@@ -632,6 +654,7 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
 
 template <bool P2>
 __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrProject);
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool rendered = false;
   uint2 rect = kEmptyRect, crect = kEmptyRect;
@@ -676,6 +699,7 @@ __device__ __forceinline__ int sort_class(uint32_t L) {
 }
 
 __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrScan);
   __shared__ unsigned long long wsum[16];
   __shared__ uint32_t wq[16];  // per wave: small | medium << 10 | big << 20 (<= 512 each)
   __shared__ uint32_t wmax[16];
@@ -806,35 +830,37 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
 // Aggregated binning (FrameParams::bin_agg): tile starts, the sort queues and
 // the frame counters from the projection's per-tile counters (binned |
 // reference << 32), which it resets to zero for the next frame.  One
-// workgroup of 1024 threads, rounds of 8192 tiles (8 per thread in
-// registers); the histogram (reference lengths) and the counters go straight
+// workgroup of 1024 threads, rounds of 4096 tiles (4 per thread in
+// registers; 8 spilled); the histogram (reference lengths) and the counters go straight
 // to the mapped host mirror and, in a row-band group, to the frame's footer.
 // the aggregated scan's queues: 0 small (<= 256 keys), 1..3 medium with
 // >= 1024, >= 512, > 256 keys, 4 big (> 2048)
 constexpr int kAggQueues = 5;
+constexpr int kAggPer = 4, kAggRound = 1024 * kAggPer;
 __device__ __forceinline__ int agg_queue(uint32_t L) {
   return L <= kSortRegCap ? 0 : (L > (uint32_t)kSortLdsCap ? 4 : (L >= 1024u ? 1 : (L >= 512u ? 2 : 3)));
 }
 
 __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrAggScan);
   // per wave of a round: pair sum, reference sum, queue counts; per wave the
   // exclusive bases (computed by lanes 0..15 of wave 0), and the round totals
   __shared__ unsigned long long wsum[16], wref[16], wbase[16], wq[16];
   __shared__ uint32_t wqb[kAggQueues][16], wvis[16], wmax[16];
   __shared__ unsigned long long s_tot;
   __shared__ uint32_t s_qt[3];
-  __shared__ uint32_t s_c[8192];  // a round's binned counts (striped in, blocked out)
-  __shared__ uint32_t s_a[8192];  // ... their aggregated parts
+  __shared__ uint32_t s_c[kAggRound];  // a round's binned counts (striped in, blocked out)
+  __shared__ uint32_t s_a[kAggRound];  // ... their aggregated parts
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // a round's counters, read striped (coalesced: lane-consecutive tiles);
   // the first round's are issued before the V loads (one memory round trip
   // for both)
-  unsigned long long vs[8];
-  uint32_t fb[8];
+  unsigned long long vs[kAggPer];
+  uint32_t fb[kAggPer];
   auto load_round = [&](int r0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kAggPer; ++j) {
       const int i = r0 + j * 1024 + tid;
       vs[j] = i < T ? b.tile_cnt64[i] : 0ull;
       fb[j] = i < T ? b.tile_fb[i] : 0u;
@@ -863,7 +889,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   unsigned long long carry = 0, rcarry = 0;
   uint32_t qcarry[3] = {0u, 0u, 0u};
   uint32_t mx = 0;
-  for (int r0 = 0; r0 < T; r0 += 8192) {
+  for (int r0 = 0; r0 < T; r0 += kAggRound) {
     // the round's counters, read striped (coalesced: lane-consecutive tiles);
     // the histogram goes to tile_ref (and the group's footer) from here, the
     // counters are zeroed for the next frame, and the binned counts are
@@ -872,7 +898,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     {
       if (r0 > 0) load_round(r0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < kAggPer; ++j) {
         const int i = r0 + j * 1024 + tid;
         const uint32_t rf = (uint32_t)(vs[j] >> 32);
         rsum += rf;
@@ -887,13 +913,13 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       }
     }
     __syncthreads();
-    const int i0 = r0 + tid * 8;
-    uint32_t v[8];
+    const int i0 = r0 + tid * kAggPer;
+    uint32_t v[kAggPer];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = s_c[tid * 8 + j];
+    for (int j = 0; j < kAggPer; ++j) v[j] = s_c[tid * kAggPer + j];
     unsigned long long sum = 0, q = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kAggPer; ++j) {
       const uint32_t c = v[j];
       sum += c;
       mx = max(mx, c);
@@ -919,7 +945,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     __syncthreads();
     if (tid < 16) {  // exclusive scan over the 16 waves
       const unsigned long long ws = wsum[tid], wqv = wq[tid];
-      unsigned long long si = ws, ri = wref[tid], qi = wqv;  // (queue counts: 5 fields of 10 bits, <= 512 each per wave)
+      unsigned long long si = ws, ri = wref[tid], qi = wqv;  // (queue counts: 5 fields of 10 bits, <= 256 each per wave)
       uint32_t qk[kAggQueues];
 #pragma unroll
       for (int k = 0; k < kAggQueues; ++k) qk[k] = (uint32_t)(wqv >> (10 * k)) & 1023u;
@@ -973,10 +999,10 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     for (int k = 0; k < kAggQueues; ++k) qpos[k] = wqb[k][wave] + ((uint32_t)(qx >> (10 * k)) & 1023u);
     __syncthreads();  // (every thread has read its counts from s_c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kAggPer; ++j) {
       const int i = i0 + j;
       const uint32_t c = v[j];
-      s_c[tid * 8 + j] = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);  // the tile start
+      s_c[tid * kAggPer + j] = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);  // the tile start
       if (i < T) {
         const int qq = agg_queue(c);
         const uint32_t pos = qpos[qq]++;
@@ -990,7 +1016,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     __syncthreads();
     // the tile starts back striped (coalesced stores)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < kAggPer; ++j) {
       const int i = r0 + j * 1024 + tid;
       if (i < T) {
         const uint32_t st = s_c[j * 1024 + tid];
@@ -1055,6 +1081,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
 // box was too wide for LDS places every pair with a global cursor past the
 // tile's aggregated pairs.
 __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrAggEmit);
   __shared__ uint32_t cnt[kAggCap];
   const int blk = blockIdx.x;
   const int i = blk * 256 + (int)threadIdx.x;
@@ -1168,6 +1195,7 @@ __device__ __forceinline__ void lds_zero(uint32_t* cnt, int words) {
 }
 
 __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrCount);
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
   const int T = fp.n_tiles;
   const int c = blockIdx.x;
@@ -1256,6 +1284,7 @@ __global__ __launch_bounds__(1024) void gs_count_kernel(FrameParams fp, Buffers 
 // (n_chunks <= 256: at most 16 rows per wave, held in registers; a larger
 // scene's rows past a wave's 16th are read twice, summed then rewritten).
 __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrColscan);
   __shared__ uint32_t wsum[16][64], whsum[16][64];
   const int T = fp.n_tiles, NC = fp.n_chunks;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1341,6 +1370,7 @@ __global__ __launch_bounds__(1024) void gs_colscan_kernel(FrameParams fp, Buffer
 // Counters and list lengths also go straight to the mapped host mirror, so a
 // frame needs no device-to-host copy.
 __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrScanMulti);
   __shared__ unsigned long long s_sum[3][4];
   __shared__ uint32_t s_q[2][4][3], s_mx[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1461,6 +1491,7 @@ __global__ __launch_bounds__(256) void gs_scan_multi_kernel(FrameParams fp, Buff
 }
 
 __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrEmitChunk);
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
   const int T = fp.n_tiles;
   const int c = blockIdx.x;
@@ -1540,6 +1571,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
 // --------------------------------------------------------------------- emit
 // Fallback emit (tile grids too large for an LDS histogram): global cursors.
 __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrEmit);
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= fp.n) return;
   if (!block_live(fp, b, i)) return;
@@ -2132,6 +2164,7 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_sort_tiles_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrSortTiles);
   sort_tiles<256>(fp, b);
 }
 
@@ -2160,6 +2193,7 @@ __device__ __forceinline__ uint32_t big_buckets(uint32_t L) {
 
 // one workgroup: segment counts of the big lists -> exclusive prefix
 __global__ __launch_bounds__(1024) void gs_big_prefix_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   __shared__ uint32_t wsum[16], wsum_b[16];
   __shared__ uint32_t s_maxl;
   const uint32_t n_big = b.counters[0];
@@ -2257,6 +2291,7 @@ __device__ __forceinline__ void big_item(const Buffers& b, uint32_t n_big, uint3
 // one workgroup per big list (grid-stride): sample, sort it, pick splitters;
 // zero the list's bucket counters
 __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   __shared__ unsigned long long keys[kSortLdsCap];
   const uint32_t n_big = b.counters[0];
   const uint32_t tid = threadIdx.x;
@@ -2324,6 +2359,7 @@ __global__ __launch_bounds__(256) void gs_big_split_kernel(FrameParams fp, Buffe
 // list's pairs_alt region (from s + L - 1 down): the prefix takes at most the
 // keys below the bound from the front, so the two never meet.
 __global__ __launch_bounds__(256) void gs_big_select_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   __shared__ uint32_t s_par[6];
   __shared__ uint32_t s_n, s_base, s_n2, s_base2;
   const uint32_t n_big = b.counters[0], total = n_big ? b.counters[12] : 0u;
@@ -2379,6 +2415,7 @@ __global__ __launch_bounds__(256) void gs_big_select_kernel(FrameParams fp, Buff
 
 // one workgroup per big list (grid-stride): sort its prefix into list[s, s + n)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_psort_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   __shared__ unsigned long long keys[kSortLdsCap];
   const uint32_t n_big = b.counters[0];
   for (uint32_t j = blockIdx.x; j < n_big; j += gridDim.x) {
@@ -2417,6 +2454,7 @@ __device__ __forceinline__ void cont_live_box(const Buffers& b, uint32_t j, int&
 // depth >= cont_thr.  A window whose filtered keys overflow one workgroup's
 // sort is skipped (cont_len 0): pass 2 then takes every key past the prefix.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_cont_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   __shared__ unsigned long long keys[kSortLdsCap];
   __shared__ uint32_t s_m;
   const uint32_t n_big = b.counters[0];
@@ -2584,16 +2622,19 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
 }
 
 __global__ __launch_bounds__(256) void gs_big_count_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   big_bucket_pass<false>(fp, b);
 }
 
 __global__ __launch_bounds__(256) void gs_big_scatter_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   big_bucket_pass<true>(fp, b);
 }
 
 // one wave per big list: bucket counts -> bucket starts (exclusive, within the
 // list); the counters are reset for the scatter's reservations
 __global__ __launch_bounds__(256) void gs_big_bscan_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   const uint32_t n_big = b.counters[0];
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * 4u;
@@ -2624,6 +2665,7 @@ __global__ __launch_bounds__(256) void gs_big_bscan_kernel(FrameParams fp, Buffe
 
 // one workgroup per bucket (grid-stride): sort it into its place in the list
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_big_bsort_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBig);
   constexpr int NT = 256, NW = NT / 64;
   constexpr int kRadixWords = 8 * 256 + 256 + NW * 256;
   constexpr int kWords = 2 * kSortLdsCap > kRadixWords ? 2 * kSortLdsCap : kRadixWords;
@@ -2655,9 +2697,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // -------------------------------------------------------------------- blend
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-#ifndef GS_BLEND_PACKED
-#define GS_BLEND_PACKED 1
-#endif
 
 // v_writelane_b32 x2: lanes L and L + 1 of v take the wave-uniform words lo,
 // hi -- a ballot's two halves.  The s_nop gives the two wait states a VALU
@@ -2744,19 +2783,9 @@ enum BlendExp { kExpExact = 0, kExpInRange = 1, kExpHw = 2 };
 template <int EXP>
 __device__ __forceinline__ float blend_power_exp(const Px& q, const float4& r0, const float4& r1,
                                                  float& power) {
-#if GS_BLEND_PACKED
-  // the two axes' terms as packed fp32 pairs (v_pk_add / v_pk_mul: one
-  // instruction per pair, each half rounded as the scalar op): the same
-  // operations in the same order, (h0 dx) dx + (h2 dy) dy - (k1 dx) dy
-  const f32x2 d = f32x2{r0.x, r0.y} - q.p;
-  const f32x2 t = f32x2{r0.z, r0.w} * d;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
-  const f32x2 u = t * d;
-  power = (u.x + u.y) - r1.x * d.x * d.y;
-#else
   const float dx = r0.x - q.p.x, dy = r0.y - q.p.y;
   const float h0 = r0.z, h2 = r0.w, k1 = r1.x;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
   power = (h0 * dx * dx + h2 * dy * dy) - k1 * dx * dy;
-#endif
   return EXP == kExpHw ? gs_expf_hw(power) : (EXP == kExpInRange ? gs_expf_inrange(power) : gs_expf(power));
 }
 
@@ -2772,16 +2801,10 @@ __device__ __forceinline__ void blend_composite(Px& q, float power, float e, con
   const bool brk = hit && test_T < 0.0001f;  // break (codelets.cpp:406-408)
   const bool upd = hit && !brk;
   if (__builtin_expect(upd, 0)) {
-#if GS_BLEND_PACKED
-    // colour += gCont * alpha * T, two channels per packed op
-    q.c01 = q.c01 + (f32x2{r1.z, r1.w} * alpha) * q.T;
-    q.c23 = q.c23 + (f32x2{r2.x, op} * alpha) * q.T;
-#else
     q.c01.x = q.c01.x + (r1.z * alpha) * q.T;  // colour += gCont * alpha * T
     q.c01.y = q.c01.y + (r1.w * alpha) * q.T;
     q.c23.x = q.c23.x + (r2.x * alpha) * q.T;
     q.c23.y = q.c23.y + (op * alpha) * q.T;
-#endif
     q.T = test_T;
   }
   q.done = q.done || brk;
@@ -3152,6 +3175,7 @@ __device__ __forceinline__ void blend_sort_tile(const FrameParams& fp, const Buf
 // HWEXP: GS_FLAG_FAST_EXP (its own kernel: the default path's code is unchanged)
 template <int BQW, bool HWEXP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_blend_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBlend);
   __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (fp.blend_sort) {
@@ -3173,6 +3197,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // counters load, 4 resident per CU).
 template <bool HWEXP>
 __global__ __launch_bounds__(256) void gs_blend_cont_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBlendCont);
   __shared__ float4 s_rec[GS_BLEND_WPG][3][64];
   if (fp.big_pass == 2 && b.counters[1] == 0u) return;  // no list outlived its window
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

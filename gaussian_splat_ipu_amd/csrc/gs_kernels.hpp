@@ -8,6 +8,14 @@
 namespace gsk {
 
 // Per-frame constants, passed by value as kernel arguments.
+// Timeline probe builds (-DGS_PROBE=1, tools/build_variant.sh; never the
+// default library): every kernel records, per frame, its first wave's start
+// and its last wave's end (wall_clock64, 100 MHz), for tools/probe_timeline.py
+#ifndef GS_PROBE
+#define GS_PROBE 0
+#endif
+constexpr int kProbeFrames = 4096, kProbeKernels = 16;
+
 struct FrameParams {
   float mvp[16];      // proj * view, glm column-major (codelets.cpp:443)
   float tanfov;       // (float)tan(0.5 * fxy[0])   (codelets.cpp:444)
@@ -56,6 +64,7 @@ struct FrameParams {
                       //   flagged by the blend (window), 2 = those flagged again (full sort)
   int blend_cont;     // blend: 1 = the continuation of the flagged big-list blocks
   int count_records;  // blend: each wave writes the records it composited to blend_count
+  int probe_frame;    // (GS_PROBE builds) the frame's slot in the probe ring
   int fast_exp;       // blend: hardware exp2 (GS_FLAG_FAST_EXP, within a stated tolerance)
   int sh_degree;      // > 0: view-dependent colour from spherical harmonics (gs_set_sh)
   float campos[3];    // camera position in the scene's (prepared) frame, for the SH direction
@@ -67,6 +76,7 @@ struct FrameParams {
 
 // Device workspace of one renderer.
 struct Buffers {
+  unsigned long long* probe;      // (GS_PROBE builds, GSPLAT_PROBE_FILE) [kProbeFrames][kProbeKernels][2] or null
   // scene (SoA of the 64-B Gaussian3D record, ipu_geometry.hpp:305-311)
   const float4* mean;       // x y z w
   const float4* colour;     // r g b opacity

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -138,12 +139,32 @@ int alloc_pairs(gs_renderer* r, uint64_t cap) {
   return GS_OK;
 }
 
+// probe builds: the ring of this renderer's frames appended to
+// GSPLAT_PROBE_FILE (tools/probe_timeline.py): "GSPR", the device, the
+// frames recorded, then [frames][kProbeKernels][start, end] u64 (100 MHz
+// wall clock; start ~0 / end 0 = the kernel did not run)
+void dump_probe(gs_renderer* r) {
+  const char* path = std::getenv("GSPLAT_PROBE_FILE");
+  const int nf = std::min(r->probe_n, gsk::kProbeFrames);
+  if (!path || nf <= 0) return;
+  std::vector<unsigned long long> h((size_t)nf * gsk::kProbeKernels * 2);
+  if (hipMemcpy(h.data(), r->d_probe, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  if (FILE* f = std::fopen(path, "ab")) {
+    const int32_t hdr[4] = {0x52505347, r->device, nf, gsk::kProbeKernels};
+    std::fwrite(hdr, 4, 4, f);
+    std::fwrite(h.data(), 8, h.size(), f);
+    std::fclose(f);
+  }
+}
+
 void release(gs_renderer* r) {
   if (!r) return;
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
-  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg})
+  if (r->d_probe) dump_probe(r);
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg,
+                  r->d_probe})
     if (p) (void)hipFree(p);
   if (r->d_sh && r->owns_sh) (void)hipFree(r->d_sh);
   free_pairs(r);
@@ -212,8 +233,13 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
   if (r->env_blend_lpt >= 0) fp.blend_lpt = r->env_blend_lpt;  // (A/B)
   // the tile sort inside the blend's workgroups (16x16 tiles: one workgroup
-  // per tile; GSPLAT_BLEND_SORT=0 keeps the sort launch, A/B)
-  fp.blend_sort = (r->env_blend_sort != 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4) ? 1 : 0;
+  // per tile) for row bands: 8 bands of config 4, 38.2 -> 37.2 us per frame;
+  // whole frames keep the sort launch (config 3: 7 980 against 7 800
+  // frames/s, the sort launch overlapping the other frames' blends better;
+  // config 5 1 440 against 1 453).  GSPLAT_BLEND_SORT=0 / 1 forces it off /
+  // on (A/B).
+  fp.blend_sort = (fp.blend_bqw == 4 && fp.chunks_per_tile == 4 &&
+                   (r->env_blend_sort == 1 || (r->env_blend_sort < 0 && r->band_nrows < r->tiles_y))) ? 1 : 0;
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
@@ -413,7 +439,8 @@ int enqueue_lattice(gs_renderer* r, const gsk::FrameParams& fp, ProfileSlot* slo
 int enqueue_frame(gs_renderer* r) {
   // several frames may be in flight on the stream; the host mirrors always
   // hold the last one's counters after gs_sync
-  const gsk::FrameParams fp = make_params(r);
+  gsk::FrameParams fp = make_params(r);
+  if (r->d_probe) fp.probe_frame = r->probe_n++;
   r->last_fp = fp;
   r->have_fp = true;
   r->band_moved = false;
@@ -647,7 +674,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) r->env_blend_lpt = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) r->env_mean_w1 = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;
+  if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;  // else -1: auto
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
@@ -958,6 +985,15 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     for (auto& s : r->ring)
       for (auto& ev : s.ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return fail(hip_fail(e, "hipEventCreate"));
+  }
+  if (GS_PROBE && std::getenv("GSPLAT_PROBE_FILE") && !lattice) {
+    // the probe ring: starts at ~0 (atomicMin), ends at 0 (atomicMax)
+    std::vector<unsigned long long> init((size_t)gsk::kProbeFrames * gsk::kProbeKernels * 2);
+    for (size_t k = 0; k < init.size(); k += 2) init[k] = ~0ull;
+    if ((e = hipMalloc(&r->d_probe, init.size() * 8)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(probe)"));
+    if ((e = hipMemcpy(r->d_probe, init.data(), init.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(hip_fail(e, "hipMemcpy(probe)"));
+    r->buf.probe = (unsigned long long*)r->d_probe;
   }
   *out = r;
   return GS_OK;

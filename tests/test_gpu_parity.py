@@ -130,11 +130,15 @@ def test_synthetic_1080p_16x16(built):
     _assert_parity(s, f, g)
 
 
-def test_large_tile_lists_take_the_radix_path(built):
+@pytest.mark.parametrize("bsort", ["0", "1"])
+def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort):
     """A clustered scene (config 5's construction) puts > 2048 Gaussians on
     some tiles: those go through the block-wide LSD radix sort, first inside
-    the tile-sort launch, then (second frame) in the separate big-list launch."""
+    the tile-sort launch (bsort 1: inside the blend's workgroups), then
+    (second frame) in the separate big-list launch."""
     from gaussian_splat_ipu_amd import camera, scene
+
+    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
 
     src = scene.load_ply(PC12)
     cl = np.stack([src["x"], src["y"], src["z"]], 1)[:200]
@@ -507,9 +511,10 @@ def test_render_server_cli(built, tmp_path):
     assert out2.read_bytes() == data
 
 
+@pytest.mark.parametrize("bsort", ["0", "1"])
 @pytest.mark.parametrize("half_width,log_scale,planes", [
     (1.5, -3.8, 4), (0.3, -4.0, 4), (1.5, -3.8, 64), (0.3, -4.0, 400), (0.3, -4.0, 1)])
-def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
+def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale, planes, bsort):
     """Gaussians on planes of constant clip z (a view that only translates
     along z), in shuffled input order: the tile lists hold runs of equal
     depth, whose order must be the input index's (the oracle's stable order),
@@ -518,9 +523,12 @@ def test_equal_depths_keep_input_order(built, half_width, log_scale, planes):
     first frame, the big-list sample sort on the second).  4 planes make long
     runs (the list is re-sorted), 64 / 400 planes mostly short ones (put in
     order in place); one plane gives big lists of a single depth (one
-    sample-sort bucket > 2048 keys: its radix path)."""
+    sample-sort bucket > 2048 keys: its radix path).  bsort 1: the tile
+    sort inside the blend's workgroups."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
+
+    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
 
     g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=5, sh_degree=0)))
     a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
@@ -652,3 +660,24 @@ def test_aggregated_binning_4k_clustered(built, monkeypatch):
         s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0)
         _assert_parity(s, f, g, check_proj=False)
         s.close()
+
+
+@pytest.mark.parametrize("bsort", ["0", "1"])
+def test_blend_sort_paths_bit_exact(pc12, monkeypatch, bsort):
+    """The tile sort inside the blend's workgroups (GSPLAT_BLEND_SORT=1:
+    every 16x16 tile's workgroup sorts its list, then blends it) and the
+    separate sort launch give the oracle's lists, histogram and frame bit for
+    bit -- on a whole frame and on a row band (the default picks the in-blend
+    sort for bands only); the paths the frame took are in stats()["paths"]."""
+    from gaussian_splat_ipu_amd import camera
+
+    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    for band_count, band_index in [(1, 0), (8, 3)]:
+        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
+        assert bool(s.stats()["paths"] & 2) == (bsort == "1")
+        _assert_parity(s, f, g, check_proj=False)
+        s.close()
+
