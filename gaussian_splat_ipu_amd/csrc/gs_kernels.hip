@@ -1080,14 +1080,9 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
 // cursor per tile (one atomic per run of equal rectangles).  A block whose
 // box was too wide for LDS places every pair with a global cursor past the
 // tile's aggregated pairs.
-__global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffers b) {
-  GS_PROBE_SCOPE(kPrAggEmit);
-  __shared__ uint32_t cnt[kAggCap];
-  const int blk = blockIdx.x;
+__device__ __forceinline__ void agg_emit_block(const FrameParams& fp, const Buffers& b, int blk, uint32_t* cnt,
+                                               uint32_t (*s_wc)[kAggBallot]) {
   const int i = blk * 256 + (int)threadIdx.x;
-  // the scan's frame counters to the mapped host mirror (the next frames'
-  // big-list hint, the host's counters at sync)
-  if (blk == 0 && threadIdx.x < 16) b.host_counters[threadIdx.x] = b.counters[threadIdx.x];
   if (fp.band_cull && b.block_rendered[blk] == 0u) return;  // (uniform) culled block: nothing binned
   const uint4 box = b.agg_box[blk];
   if (box.w == 0u) return;  // (uniform) nothing binned
@@ -1112,7 +1107,6 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
   const uint32_t* const off = b.agg_off + (size_t)blk * kAggCap;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (area <= kAggBallot) {  // (uniform) small box: ranks from ballots, no LDS atomics
-    __shared__ uint32_t s_wc[4][kAggBallot];
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (int k = 0; k < area; ++k) {
       const uint32_t tx = (uint32_t)(bx0 + k % bw), ty = (uint32_t)(by0 + k / bw);
@@ -1172,6 +1166,22 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
         if (pos < fp.pair_cap) b.pairs[pos] = key;
       }
     }
+}
+
+// one workgroup per projection block, or (FrameParams::emit_grid) a grid
+// of that many workgroups walking the blocks
+__global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrAggEmit);
+  __shared__ uint32_t cnt[kAggCap];
+  __shared__ uint32_t s_wc[4][kAggBallot];
+  // the scan's frame counters to the mapped host mirror (the next frames'
+  // big-list hint, the host's counters at sync)
+  if (blockIdx.x == 0 && threadIdx.x < 16) b.host_counters[threadIdx.x] = b.counters[threadIdx.x];
+  const int nb = (fp.n + 255) / 256;
+  for (int blk = blockIdx.x; blk < nb; blk += gridDim.x) {
+    agg_emit_block(fp, b, blk, cnt, s_wc);
+    if ((int)gridDim.x < nb) __syncthreads();  // (uniform) the next block rewrites the LDS
+  }
 }
 
 // ------------------------------------------------------------ chunked binning
@@ -3256,7 +3266,8 @@ void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
   if (fp.bin_agg) {
-    gs_agg_emit_kernel<<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+    const int nb = (fp.n + 255) / 256;
+    gs_agg_emit_kernel<<<fp.emit_grid > 0 ? std::min(nb, fp.emit_grid) : nb, 256, 0, s>>>(fp, b);
     return;
   }
   if (!fp.bin_global) {

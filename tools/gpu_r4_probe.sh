@@ -33,4 +33,15 @@ rm -f $O/probe_full_f3.bin
 GSPLAT_LIB=$PL GSPLAT_PROBE_FILE=$O/probe_full_f3.bin timeout -k 10 300 python tools/band_emulate.py --inflight 3 --bands 1 --steps 400 > $O/probe_full_f3.jsonl 2> $O/probe_full_f3.err || exit $?
 bands $O/probe_full_f3.jsonl
 python3 tools/probe_timeline.py $O/probe_full_f3.bin --json $O/probe_full_f3.json
+for g in 256 1024; do
+  echo "== band 3 of 8, emit grid $g, inflight 3 / 6 $(date +%T)"
+  for f in 3 6; do
+    GSPLAT_EMIT_GRID=$g timeout -k 10 300 python tools/band_emulate.py --balanced --inflight $f --bands 8 --only-band 3 --steps 400 > $O/eg${g}_f$f.jsonl 2> $O/eg${g}_f$f.err || exit $?
+    bands $O/eg${g}_f$f.jsonl
+  done
+done
+echo "== probe: band 3 of 8, emit grid 256, inflight 6 $(date +%T)"
+rm -f $O/probe_eg256_f6.bin
+GSPLAT_EMIT_GRID=256 GSPLAT_LIB=$PL GSPLAT_PROBE_FILE=$O/probe_eg256_f6.bin timeout -k 10 300 python tools/band_emulate.py --balanced --inflight 6 --bands 8 --only-band 3 --steps 400 > $O/probe_eg256_f6.jsonl 2> $O/probe_eg256_f6.err || exit $?
+python3 tools/probe_timeline.py $O/probe_eg256_f6.bin --json $O/probe_eg256_f6.json
 echo "== done $(date +%T)"
