@@ -681,3 +681,23 @@ def test_blend_sort_paths_bit_exact(pc12, monkeypatch, bsort):
         _assert_parity(s, f, g, check_proj=False)
         s.close()
 
+
+
+@pytest.mark.parametrize("grid", ["7", "256"])
+def test_agg_emit_grid_walks_every_block(pc12, monkeypatch, grid):
+    """GSPLAT_EMIT_GRID=G: the aggregated emit as G workgroups walking the
+    projection blocks (LDS reused block after block) places every pair as
+    the one-workgroup-per-block launch does: a row band and a whole frame
+    with the aggregated binning forced, bit for bit against the oracle."""
+    from gaussian_splat_ipu_amd import camera
+
+    monkeypatch.setenv("GSPLAT_EMIT_GRID", grid)
+    monkeypatch.setenv("GSPLAT_BIN_AGG", "1")
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    for band_count, band_index in [(1, 0), (8, 3)]:
+        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
+        assert s.stats()["paths"] & 1
+        _assert_parity(s, f, g, check_proj=False)
+        s.close()
