@@ -652,10 +652,10 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
   }
 }
 
+// one block of 256 Gaussians (every thread of the workgroup calls it)
 template <bool P2>
-__global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
-  GS_PROBE_SCOPE(kPrProject);
-  const int i = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void project_block(const FrameParams& fp, const Buffers& b, int blk) {
+  const int i = blk * 256 + threadIdx.x;
   bool rendered = false;
   uint2 rect = kEmptyRect, crect = kEmptyRect;
   if (fp.band_cull) {
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
       culled = !__builtin_isnan(cr.w) && band_culled_fast<P2>(fp, cr);
     }
     if (__syncthreads_count(i < fp.n && !culled) == 0) {
-      if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = 0u;
+      if (threadIdx.x == 0) b.block_rendered[blk] = 0u;
       return;
     }
     if (culled) {  // no tile row in this band: empty rectangle, no record
@@ -683,10 +683,22 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
   } else if (i < fp.n) {
     rendered = project_one<P2>(fp, b, i, rect, crect);
   }
-  if (fp.bin_agg) agg_count(fp, b, rect, crect, blockIdx.x);
+  if (fp.bin_agg) agg_count(fp, b, rect, crect, blk);
   // V per workgroup (summed by the scan kernel): no single-address atomics
   const int v = __syncthreads_count(rendered);
-  if (threadIdx.x == 0) b.block_rendered[blockIdx.x] = (uint32_t)v;
+  if (threadIdx.x == 0) b.block_rendered[blk] = (uint32_t)v;
+}
+
+// one workgroup per block, or (FrameParams::project_grid) a grid of that
+// many workgroups walking the blocks
+template <bool P2>
+__global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrProject);
+  const int nb = (fp.n + 255) / 256;
+  for (int blk = blockIdx.x; blk < nb; blk += gridDim.x) {
+    project_block<P2>(fp, b, blk);
+    if ((int)gridDim.x < nb) __syncthreads();  // (uniform) the next block rewrites the LDS
+  }
 }
 
 // --------------------------------------------------------------------- scan
@@ -3230,10 +3242,12 @@ void launch_copy_word(hipStream_t s, uint32_t* dst, const uint32_t* src) {
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
+  const int nb = (fp.n + 255) / 256;
+  const int grid = fp.project_grid > 0 ? std::min(nb, fp.project_grid) : nb;
   if (fp.pow2)
-    gs_project_kernel<true><<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+    gs_project_kernel<true><<<grid, 256, 0, s>>>(fp, b);
   else
-    gs_project_kernel<false><<<(fp.n + 255) / 256, 256, 0, s>>>(fp, b);
+    gs_project_kernel<false><<<grid, 256, 0, s>>>(fp, b);
 }
 
 size_t bin_lds_bytes(int n_tiles) { return (size_t)((n_tiles + 1) / 2) * 4; }

@@ -684,13 +684,15 @@ def test_blend_sort_paths_bit_exact(pc12, monkeypatch, bsort):
 
 
 @pytest.mark.parametrize("grid", ["7", "256"])
-def test_agg_emit_grid_walks_every_block(pc12, monkeypatch, grid):
-    """GSPLAT_EMIT_GRID=G: the aggregated emit as G workgroups walking the
-    projection blocks (LDS reused block after block) places every pair as
-    the one-workgroup-per-block launch does: a row band and a whole frame
-    with the aggregated binning forced, bit for bit against the oracle."""
+def test_walking_grids_cover_every_block(pc12, monkeypatch, grid):
+    """GSPLAT_PROJECT_GRID=G / GSPLAT_EMIT_GRID=G: the projection and the
+    aggregated emit as G workgroups walking the 256-Gaussian blocks (LDS
+    reused block after block) bin every pair as the one-workgroup-per-block
+    launches do: a row band (band cull) and a whole frame with the aggregated
+    binning forced, bit for bit against the oracle."""
     from gaussian_splat_ipu_amd import camera
 
+    monkeypatch.setenv("GSPLAT_PROJECT_GRID", grid)
     monkeypatch.setenv("GSPLAT_EMIT_GRID", grid)
     monkeypatch.setenv("GSPLAT_BIN_AGG", "1")
     g, bb = pc12

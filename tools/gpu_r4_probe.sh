@@ -40,6 +40,13 @@ for g in 256 1024; do
     bands $O/eg${g}_f$f.jsonl
   done
 done
+for g in 1024 2048; do
+  echo "== band 3 of 8, project + emit grid $g, inflight 3 / 6 $(date +%T)"
+  for f in 3 6; do
+    GSPLAT_PROJECT_GRID=$g GSPLAT_EMIT_GRID=$g timeout -k 10 300 python tools/band_emulate.py --balanced --inflight $f --bands 8 --only-band 3 --steps 400 > $O/pg${g}_f$f.jsonl 2> $O/pg${g}_f$f.err || exit $?
+    bands $O/pg${g}_f$f.jsonl
+  done
+done
 echo "== probe: band 3 of 8, emit grid 256, inflight 6 $(date +%T)"
 rm -f $O/probe_eg256_f6.bin
 GSPLAT_EMIT_GRID=256 GSPLAT_LIB=$PL GSPLAT_PROBE_FILE=$O/probe_eg256_f6.bin timeout -k 10 300 python tools/band_emulate.py --balanced --inflight 6 --bands 8 --only-band 3 --steps 400 > $O/probe_eg256_f6.jsonl 2> $O/probe_eg256_f6.err || exit $?
