@@ -487,14 +487,16 @@ __device__ __forceinline__ void wave_minmax_u16x2(uint32_t& lo, uint32_t& hi) {
 }
 
 #if GS_PROBE
-// per wave: the kernel's earliest start and latest end for the frame
+// the kernel's earliest start (each workgroup's first wave) and latest end
+// (every wave) for the frame, spread over kProbeSlots (start, end) pairs
 // (vector atomics on the probe ring; probe builds only)
 struct ProbeScope {
   unsigned long long* p = nullptr;
   __device__ ProbeScope(const FrameParams& fp, const Buffers& b, int k) {
     if (b.probe && (threadIdx.x & 63) == 0) {
-      p = b.probe + 2 * ((size_t)(fp.probe_frame % kProbeFrames) * kProbeKernels + (size_t)k);
-      atomicMin(p, (unsigned long long)wall_clock64());
+      const size_t slot = (size_t)(blockIdx.x * 4u + (threadIdx.x >> 6)) % (size_t)kProbeSlots;
+      p = b.probe + 2 * (((size_t)(fp.probe_frame % kProbeFrames) * kProbeKernels + (size_t)k) * kProbeSlots + slot);
+      if (threadIdx.x == 0) atomicMin(p, (unsigned long long)wall_clock64());
     }
   }
   __device__ ~ProbeScope() {

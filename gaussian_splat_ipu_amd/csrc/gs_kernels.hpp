@@ -14,7 +14,10 @@ namespace gsk {
 #ifndef GS_PROBE
 #define GS_PROBE 0
 #endif
-constexpr int kProbeFrames = 4096, kProbeKernels = 16;
+// (per frame and kernel, kProbeSlots (start, end) pairs: the waves spread
+// their atomics over them -- one address per kernel serialised 15 k waves'
+// atomics and stretched the projection 15x)
+constexpr int kProbeFrames = 512, kProbeKernels = 16, kProbeSlots = 256;
 
 struct FrameParams {
   float mvp[16];      // proj * view, glm column-major (codelets.cpp:443)
@@ -78,7 +81,7 @@ struct FrameParams {
 
 // Device workspace of one renderer.
 struct Buffers {
-  unsigned long long* probe;      // (GS_PROBE builds, GSPLAT_PROBE_FILE) [kProbeFrames][kProbeKernels][2] or null
+  unsigned long long* probe;      // (GS_PROBE builds, GSPLAT_PROBE_FILE) [kProbeFrames][kProbeKernels][kProbeSlots][2] or null
   // scene (SoA of the 64-B Gaussian3D record, ipu_geometry.hpp:305-311)
   const float4* mean;       // x y z w
   const float4* colour;     // r g b opacity

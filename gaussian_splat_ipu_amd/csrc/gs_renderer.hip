@@ -141,18 +141,34 @@ int alloc_pairs(gs_renderer* r, uint64_t cap) {
 
 // probe builds: the ring of this renderer's frames appended to
 // GSPLAT_PROBE_FILE (tools/probe_timeline.py): "GSPR", the device, the
-// frames recorded, then [frames][kProbeKernels][start, end] u64 (100 MHz
-// wall clock; start ~0 / end 0 = the kernel did not run)
+// frames recorded (the last kProbeFrames, oldest first), the kernel count,
+// then [frames][kProbeKernels][start, end] u64 (100 MHz wall clock, reduced
+// over the slots; start ~0 / end 0 = the kernel did not run)
 void dump_probe(gs_renderer* r) {
   const char* path = std::getenv("GSPLAT_PROBE_FILE");
   const int nf = std::min(r->probe_n, gsk::kProbeFrames);
   if (!path || nf <= 0) return;
-  std::vector<unsigned long long> h((size_t)nf * gsk::kProbeKernels * 2);
+  const size_t per_frame = (size_t)gsk::kProbeKernels * gsk::kProbeSlots * 2;
+  std::vector<unsigned long long> h((size_t)gsk::kProbeFrames * per_frame);
   if (hipMemcpy(h.data(), r->d_probe, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  std::vector<unsigned long long> out((size_t)nf * gsk::kProbeKernels * 2);
+  for (int j = 0; j < nf; ++j) {
+    const int f = (r->probe_n - nf + j) % gsk::kProbeFrames;
+    for (int k = 0; k < gsk::kProbeKernels; ++k) {
+      unsigned long long s = ~0ull, e = 0ull;
+      const unsigned long long* p = h.data() + (size_t)f * per_frame + (size_t)k * gsk::kProbeSlots * 2;
+      for (int q = 0; q < gsk::kProbeSlots; ++q) {
+        s = std::min(s, p[2 * q]);
+        e = std::max(e, p[2 * q + 1]);
+      }
+      out[((size_t)j * gsk::kProbeKernels + k) * 2] = s;
+      out[((size_t)j * gsk::kProbeKernels + k) * 2 + 1] = e;
+    }
+  }
   if (FILE* f = std::fopen(path, "ab")) {
     const int32_t hdr[4] = {0x52505347, r->device, nf, gsk::kProbeKernels};
     std::fwrite(hdr, 4, 4, f);
-    std::fwrite(h.data(), 8, h.size(), f);
+    std::fwrite(out.data(), 8, out.size(), f);
     std::fclose(f);
   }
 }
@@ -992,7 +1008,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   }
   if (GS_PROBE && std::getenv("GSPLAT_PROBE_FILE") && !lattice) {
     // the probe ring: starts at ~0 (atomicMin), ends at 0 (atomicMax)
-    std::vector<unsigned long long> init((size_t)gsk::kProbeFrames * gsk::kProbeKernels * 2);
+    std::vector<unsigned long long> init((size_t)gsk::kProbeFrames * gsk::kProbeKernels * gsk::kProbeSlots * 2);
     for (size_t k = 0; k < init.size(); k += 2) init[k] = ~0ull;
     if ((e = hipMalloc(&r->d_probe, init.size() * 8)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(probe)"));
     if ((e = hipMemcpy(r->d_probe, init.data(), init.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
