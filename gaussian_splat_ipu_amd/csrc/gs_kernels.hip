@@ -59,9 +59,11 @@ __device__ __forceinline__ uint32_t depth_key_of(float z) {
 
 constexpr uint2 kEmptyRect = {1u, 1u};  // tx0 = 1 > tx1 = 0
 
-// the alpha box of record g (the z, w of its second float4)
-__device__ __forceinline__ uint2 rec_box(const Buffers& b, uint32_t g) {
-  return reinterpret_cast<const uint2*>(b.rec)[(2ull * g + 1ull) * 2ull + 1ull];
+// the alpha box of record g (the z, w of its last float4: the second of the
+// 32-B record, the third of the 48-B one)
+__device__ __forceinline__ uint2 rec_box(const FrameParams& fp, const Buffers& b, uint32_t g) {
+  const unsigned long long q = fp.rec48 ? 3ull * g + 2ull : 2ull * g + 1ull;
+  return reinterpret_cast<const uint2*>(b.rec)[q * 2ull + 1ull];
 }
 
 // FrameParams::rect8: a rectangle's four tile bounds, 8 bits each
@@ -311,11 +313,11 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   // without the band cull every live Gaussian needs its colour and rotation:
   // load them with the mean (one memory round trip instead of two)
   if (!fp.band_cull) {
-    if (!fp.mean_w1) col = b.colour[i];
+    if (!fp.mean_w1 || fp.rec48) col = b.colour[i];  // (its w is the opacity, as mean_op's)
     rot = b.rot[i];
   }
-  // the record: 32 B per Gaussian (48 B with the colour for the readback)
-  float4* rec = b.rec + (fp.full_record ? 3 : 2) * (size_t)i;
+  // the record: 32 B per Gaussian (48 B with the colour: rec48, and the readback)
+  float4* rec = b.rec + ((fp.full_record || fp.rec48) ? 3 : 2) * (size_t)i;
   uint2 rect = kEmptyRect, crect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
@@ -369,7 +371,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       return false;
     }
     if (fp.band_cull) {
-      if (!fp.mean_w1) col = b.colour[i];
+      if (!fp.mean_w1 || fp.rec48) col = b.colour[i];  // (its w is the opacity, as mean_op's)
       rot = b.rot[i];
     }
     if (fp.sh_degree >= 0 && b.sh) sh_colour(fp, b, i, mean, col);
@@ -458,8 +460,13 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       rec[2] = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
     } else if ((binned.x & 0xFFFFu) <= (binned.x >> 16)) {
       rec[0] = rec0;
-      rec[1] = make_float4(k1, pcut, __uint_as_float(b01), __uint_as_float(b23));
-      if (fp.sh_degree >= 0 && b.sh) b.col_out[i] = col;
+      if (fp.rec48) {  // the staged layout: colour and opacity beside the conic
+        rec[1] = make_float4(k1, pcut, col.x, col.y);
+        rec[2] = make_float4(col.z, col.w, __uint_as_float(b01), __uint_as_float(b23));
+      } else {
+        rec[1] = make_float4(k1, pcut, __uint_as_float(b01), __uint_as_float(b23));
+        if (fp.sh_degree >= 0 && b.sh) b.col_out[i] = col;
+      }
     }
   } else if (fp.full_record) {  // empty slot: never binned; a neutral record for the readback
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -2507,7 +2514,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        bx[u] = key[u] != ~0ull ? rec_box(b, (uint32_t)key[u])
+        bx[u] = key[u] != ~0ull ? rec_box(fp, b, (uint32_t)key[u])
                                 : make_uint2(kEmptyBox, kEmptyBox);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -2614,7 +2621,7 @@ __device__ __forceinline__ void big_bucket_pass(const FrameParams& fp, const Buf
 #pragma unroll
       for (int q = 0; q < Q; ++q)  // the record's alpha box (its 3rd float4's z, w)
         bx[q] = (use[q] && (uint32_t)(key[q] >> 32) >= thr)
-                    ? rec_box(b, (uint32_t)key[q])
+                    ? rec_box(fp, b, (uint32_t)key[q])
                     : make_uint2(kEmptyBox, kEmptyBox);
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
@@ -3010,6 +3017,13 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   // view-dependent one), assembled as the staged 48-B layout
   const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
   auto load_rec = [&](uint32_t g, float4& r0, float4& r1, float4& r2) {
+    if (fp.rec48) {  // one 48-B record (rec48)
+      const float4* q3 = b.rec + 3 * (size_t)g;
+      r0 = q3[0];
+      r1 = q3[1];
+      r2 = q3[2];
+      return;
+    }
     const float4* qq = b.rec + 2 * (size_t)g;
     r0 = qq[0];
     const float4 t = qq[1];    // k1 pcut boxx boxy

@@ -44,7 +44,8 @@ struct FrameParams {
   int blend_bqw;        // blend wave = 4x4 quads (8x8 px) | 8x2 quads (16x4 px) | 0: quad run
   int blend_lpt;        // blend tiles longest list first (row bands), else in tile order
   int project_grid;     // > 0: the projection as this many workgroups walking the blocks (A/B)
-  int emit_grid;        // > 0: the aggregated emit as this many workgroups walking the blocks (A/B)
+  int emit_grid;
+  int rec48;            // the 48-B record with the colour and opacity in it (the blend's staged layout): no colour gather        // > 0: the aggregated emit as this many workgroups walking the blocks (A/B)
   int blend_sort;       // each blend workgroup (one 16x16 tile) sorts its tile's list first: no tile-sort launch
   unsigned long long pair_cap;
   int write_rgba;

@@ -130,15 +130,17 @@ def test_synthetic_1080p_16x16(built):
     _assert_parity(s, f, g)
 
 
-@pytest.mark.parametrize("bsort", ["0", "1"])
-def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort):
+@pytest.mark.parametrize("bsort,rec48", [("0", "0"), ("1", "0"), ("0", "1")])
+def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort, rec48):
     """A clustered scene (config 5's construction) puts > 2048 Gaussians on
     some tiles: those go through the block-wide LSD radix sort, first inside
     the tile-sort launch (bsort 1: inside the blend's workgroups), then
-    (second frame) in the separate big-list launch."""
+    (second frame) in the separate big-list launch.  rec48: the 48-B record
+    with the colour in it (the lazy lists' alpha boxes read from it too)."""
     from gaussian_splat_ipu_amd import camera, scene
 
     monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
+    monkeypatch.setenv("GSPLAT_REC48", rec48)
 
     src = scene.load_ply(PC12)
     cl = np.stack([src["x"], src["y"], src["z"]], 1)[:200]
@@ -701,5 +703,23 @@ def test_walking_grids_cover_every_block(pc12, monkeypatch, grid):
     for band_count, band_index in [(1, 0), (8, 3)]:
         s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
         assert s.stats()["paths"] & 1
+        _assert_parity(s, f, g, check_proj=False)
+        s.close()
+
+
+
+def test_rec48_bit_exact(pc12, monkeypatch):
+    """GSPLAT_REC48=1: the projection writes the 48-B record with the colour
+    and opacity in it and the blend reads it in one piece instead of
+    gathering the colour: a whole frame and a row band, bit for bit against
+    the oracle (the SH colour through it: test_sh.py)."""
+    from gaussian_splat_ipu_amd import camera
+
+    monkeypatch.setenv("GSPLAT_REC48", "1")
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    for band_count, band_index in [(1, 0), (8, 3)]:
+        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
         _assert_parity(s, f, g, check_proj=False)
         s.close()
