@@ -30,6 +30,11 @@ for v in 0 1; do
   GSPLAT_REC48=$v timeout -k 10 400 python tools/band_emulate.py --balanced --inflight 3 --bands 8 > $O/bands_r$v.jsonl 2> $O/bands_r$v.err || exit $?
   bands $O/bands_r$v.jsonl
 done
+for g in 0 2048; do
+  echo "== c5 project grid $g $(date +%T)"
+  GSPLAT_PROJECT_GRID=$g timeout -k 10 400 python bench.py --config5 --steps 240 --warmup 120 --no-cpu-baseline > $O/c5_pg$g.json 2> $O/c5_pg$g.err || exit $?
+  line $O/c5_pg$g.json
+done
 for v in 0 1; do
   echo "== PMC c3 rec48=$v $(date +%T)"
   GSPLAT_REC48=$v NAME=c3_r48_$v BENCH_ARGS="--inflight 1" PASSES="fetch write" bash tools/profile.sh || exit $?
