@@ -685,7 +685,7 @@ def test_blend_sort_paths_bit_exact(pc12, monkeypatch, bsort):
 
 
 
-@pytest.mark.parametrize("grid", ["7", "256"])
+@pytest.mark.parametrize("grid", ["0", "7", "256"])
 def test_walking_grids_cover_every_block(pc12, monkeypatch, grid):
     """GSPLAT_PROJECT_GRID=G / GSPLAT_EMIT_GRID=G: the projection and the
     aggregated emit as G workgroups walking the 256-Gaussian blocks (LDS
