@@ -68,7 +68,8 @@ def main():
     win = fr[lo:lo + max(1, int(n * a.keep))]
     starts = [min(v[0] for v in ks.values()) for _, _, ks in win]
     ends = [max(v[1] for v in ks.values()) for _, _, ks in win]
-    period = stats.median(np.diff(starts)) * TICK_US if len(starts) > 1 else None
+    # (frames of F streams start in bursts: the mean spacing, not the median)
+    period = (starts[-1] - starts[0]) / (len(starts) - 1) * TICK_US if len(starts) > 1 else None
     latency = stats.median([e - s for s, e in zip(starts, ends)]) * TICK_US
     dur, gap = {}, {}
     for _, _, ks in win:
