@@ -2122,15 +2122,21 @@ __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buf
 
 // One wave sorts a list of L <= kSortRegCap keys src[0, L) in registers and
 // writes it at list[s, s + L) (equal depths: see write_tied_list).
+// (EMAX: the largest register network compiled in -- L <= 64 EMAX keys)
+template <int EMAX = 4>
 __device__ __forceinline__ void wave_sort_list(const Buffers& b, const unsigned long long* src, uint32_t s,
                                                uint32_t L, int lane, unsigned long long* slice) {
   bool done;
-  if (L <= 64u)
+  if constexpr (EMAX == 1) {
     done = wave_sort_tile<1>(b, src, s, L, lane, slice);
-  else if (L <= 128u)
-    done = wave_sort_tile<2>(b, src, s, L, lane, slice);
-  else
-    done = wave_sort_tile<4>(b, src, s, L, lane, slice);
+  } else {
+    if (L <= 64u)
+      done = wave_sort_tile<1>(b, src, s, L, lane, slice);
+    else if (L <= 128u)
+      done = wave_sort_tile<2>(b, src, s, L, lane, slice);
+    else
+      done = wave_sort_tile<4>(b, src, s, L, lane, slice);
+  }
   if (!done) {  // equal depths (wave-uniform)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -3174,7 +3180,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
 // The sort inside the blend (FrameParams::blend_sort; one workgroup = the
 // four 8x8 blocks of one 16x16 tile): the workgroup first sorts its tile's
 // list -- as gs_sort_tiles_kernel would: <= 64 keys in wave 0's registers,
-// <= kSortLdsCap by the four waves (64- or 128-key register runs, then
+// <= kSortLdsCap by the four waves (128-key register runs, then
 // merge-path levels in LDS), equal depths re-sorted by input index, a list
 // > kSortLdsCap radix-sorted here unless the big-list launches took it --
 // then its four waves blend it.  No sort launch, and the list is read back
@@ -3198,12 +3204,12 @@ __device__ __forceinline__ void blend_sort_tile(const FrameParams& fp, const Buf
     }
     return;
   }
+  // (two of the sort launch's networks only: the kernel's code stays small)
   if (L <= 64u) {
-    if (wave == 0) wave_sort_list(b, b.pairs + s, s, L, lane, keys);
+    if (wave == 0) wave_sort_list<1>(b, b.pairs + s, s, L, lane, keys);
     return;
   }
-  const bool ok = L <= kSortRegCap ? merge_sort_tile<256, 1, kOutDevice>(b, s, L, keys)
-                                   : merge_sort_tile<256, 2, kOutDevice>(b, s, L, keys);
+  const bool ok = merge_sort_tile<256, 2, kOutDevice>(b, s, L, keys);
   if (!ok) {
     __syncthreads();  // a long run of equal depths: again with input-index keys
     merge_sort_tile<256, 2, kOutInput, kSrcRekey>(b, s, L, keys);
@@ -3214,18 +3220,27 @@ __device__ __forceinline__ void blend_sort_tile(const FrameParams& fp, const Buf
 template <int BQW, bool HWEXP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_blend_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrBlend);
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
+  __shared__ float4 s_rec[GS_BLEND_WPG][3][64];
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (fp.blend_sort) {
-    const int slot = (int)blockIdx.x;  // (chunks_per_tile == GS_BLEND_WPG)
-    if (slot >= fp.n_tiles) return;
-    blend_sort_tile(fp, b, blend_tile_of(fp, b, slot), reinterpret_cast<unsigned long long*>(lds));
-    // the list's stores are done (s_waitcnt in the barrier) before any wave
-    // reads it, and the sort's LDS is free for the staging
-    __syncthreads();
-  }
-  blend_wave<BQW, HWEXP>(fp, b, blockIdx.x * GS_BLEND_WPG + wave,
-                         reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
+  blend_wave<BQW, HWEXP>(fp, b, blockIdx.x * GS_BLEND_WPG + wave, s_rec[wave]);
+}
+
+// The blend with the tile sort inside (FrameParams::blend_sort, 16x16 tiles):
+// its own symbol, so the whole-frame blend does not carry the sort's ~20 KB
+// of code (the CU pair's instruction cache is shared with the other frames'
+// kernels: config 3 7 703 -> 7 839 frames/s, blend 79.2 -> 76.7 us without it)
+template <bool HWEXP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gs_blend_sort_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBlend);
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int slot = (int)blockIdx.x;  // (chunks_per_tile == GS_BLEND_WPG)
+  if (slot >= fp.n_tiles) return;
+  blend_sort_tile(fp, b, blend_tile_of(fp, b, slot), reinterpret_cast<unsigned long long*>(lds));
+  // the list's stores are done (s_waitcnt in the barrier) before any wave
+  // reads it, and the sort's LDS is free for the staging
+  __syncthreads();
+  blend_wave<4, HWEXP>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
 }
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
@@ -3351,6 +3366,13 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (waves == 0) return;
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
+  if (fp.blend_sort) {  // (blend_bqw == 4, chunks_per_tile == GS_BLEND_WPG: one workgroup per tile)
+    if (fp.fast_exp)
+      gs_blend_sort_kernel<true><<<grid, block, 0, s>>>(fp, b);
+    else
+      gs_blend_sort_kernel<false><<<grid, block, 0, s>>>(fp, b);
+    return;
+  }
   if (fp.fast_exp) {
     if (fp.blend_bqw == 4)
       gs_blend_kernel<4, true><<<grid, block, 0, s>>>(fp, b);
