@@ -700,9 +700,20 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
 
 // one workgroup per block, or (FrameParams::project_grid) a grid of that
 // many workgroups walking the blocks
-template <bool P2>
+// LEAN: a whole frame's plain projection (no band cull, no aggregated
+// counting, no readback record, no SH, no global-atomic binning): those
+// paths are compiled out of its instantiation (a smaller kernel beside the
+// other frames' kernels in the instruction cache)
+template <bool P2, bool LEAN>
 __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrProject);
+  if constexpr (LEAN) {
+    fp.band_cull = 0;
+    fp.bin_agg = 0;
+    fp.full_record = 0;
+    fp.sh_degree = -1;
+    fp.bin_global = 0;
+  }
   const int nb = (fp.n + 255) / 256;
   for (int blk = blockIdx.x; blk < nb; blk += gridDim.x) {
     project_block<P2>(fp, b, blk);
@@ -3275,10 +3286,13 @@ void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
   const int nb = (fp.n + 255) / 256;
   const int grid = fp.project_grid > 0 ? std::min(nb, fp.project_grid) : nb;
-  if (fp.pow2)
-    gs_project_kernel<true><<<grid, 256, 0, s>>>(fp, b);
+  const bool lean = !fp.band_cull && !fp.bin_agg && !fp.full_record && !(fp.sh_degree >= 0 && b.sh) && !fp.bin_global;
+  if (fp.pow2 && lean)
+    gs_project_kernel<true, true><<<grid, 256, 0, s>>>(fp, b);
+  else if (fp.pow2)
+    gs_project_kernel<true, false><<<grid, 256, 0, s>>>(fp, b);
   else
-    gs_project_kernel<false><<<grid, 256, 0, s>>>(fp, b);
+    gs_project_kernel<false, false><<<grid, 256, 0, s>>>(fp, b);
 }
 
 size_t bin_lds_bytes(int n_tiles) { return (size_t)((n_tiles + 1) / 2) * 4; }
