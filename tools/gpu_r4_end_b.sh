@@ -2,7 +2,8 @@
 # Round-4 end set, part B: the default bench line (CPU baseline included,
 # reading the committed config-3 PMC summary), the driver-shaped line, the
 # SH-3 line, the in-process group line, and the band emulations of configs 4
-# (1/2/4/8) and 5 (8).  Outputs under gpurun_out/r4end/.
+# (1/2/4/8) and 5 (8), the kernel stats of one pipelined band and the
+# timeline probe (tools/probe_timeline.py).  Outputs under gpurun_out/r4end/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r4end
@@ -26,4 +27,17 @@ cut -c1-300 $O/bands_c4.jsonl
 echo "== bands c5 $(date +%T)"
 timeout -k 10 600 python tools/band_emulate.py --config5 --balanced --rebalance --inflight 3 --bands 1,8 > $O/bands_c5.jsonl 2> $O/bands_c5.err || exit $?
 cut -c1-300 $O/bands_c5.jsonl
+echo "== band 3 of 8 kernel stats $(date +%T)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_band3 -o band3 --output-format csv -- python3 tools/band_emulate.py --balanced --inflight 3 --bands 8 --only-band 3 --steps 200 > $O/trace_band3.log 2>&1 || exit $?
+PL=$PWD/tmp_ab/probe/libgsplat.so
+for f in 1 3; do
+  echo "== timeline probe: band 3 of 8, inflight $f $(date +%T)"
+  rm -f $O/probe_b3_f$f.bin
+  GSPLAT_LIB=$PL GSPLAT_PROBE_FILE=$O/probe_b3_f$f.bin timeout -k 10 300 python tools/band_emulate.py --balanced --inflight $f --bands 8 --only-band 3 --steps 400 > $O/probe_b3_f$f.jsonl 2> $O/probe_b3_f$f.err || exit $?
+  python3 tools/probe_timeline.py $O/probe_b3_f$f.bin --json $O/probe_b3_f$f.json
+done
+echo "== timeline probe: whole frame, inflight 3 $(date +%T)"
+rm -f $O/probe_full_f3.bin
+GSPLAT_LIB=$PL GSPLAT_PROBE_FILE=$O/probe_full_f3.bin timeout -k 10 300 python tools/band_emulate.py --inflight 3 --bands 1 --steps 400 > $O/probe_full_f3.jsonl 2> $O/probe_full_f3.err || exit $?
+python3 tools/probe_timeline.py $O/probe_full_f3.bin --json $O/probe_full_f3.json
 echo "== done $(date +%T)"
