@@ -706,14 +706,15 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
 // kProjLean: a whole frame's plain projection (no band cull, no aggregated
 // counting, no readback record, no SH, no global-atomic binning);
 // kProjBand: a row band's (band cull and aggregated counting, nothing else);
+// kProjAgg: a whole frame's with the aggregated counting (GSPLAT_BIN_AGG=1);
 // kProjAny: every path, chosen at run time.
-enum { kProjAny = 0, kProjLean = 1, kProjBand = 2 };
+enum { kProjAny = 0, kProjLean = 1, kProjBand = 2, kProjAgg = 3 };
 template <bool P2, int MODE>
 __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrProject);
   if constexpr (MODE != kProjAny) {
     fp.band_cull = MODE == kProjBand ? 1 : 0;
-    fp.bin_agg = MODE == kProjBand ? 1 : 0;
+    fp.bin_agg = (MODE == kProjBand || MODE == kProjAgg) ? 1 : 0;
     fp.full_record = 0;
     fp.sh_degree = -1;
     fp.bin_global = 0;
@@ -872,32 +873,34 @@ __global__ __launch_bounds__(1024) void gs_scan_kernel(FrameParams fp, Buffers b
 // the aggregated scan's queues: 0 small (<= 256 keys), 1..3 medium with
 // >= 1024, >= 512, > 256 keys, 4 big (> 2048)
 constexpr int kAggQueues = 5;
-constexpr int kAggPer = 4, kAggRound = 1024 * kAggPer;
 __device__ __forceinline__ int agg_queue(uint32_t L) {
   return L <= kSortRegCap ? 0 : (L > (uint32_t)kSortLdsCap ? 4 : (L >= 1024u ? 1 : (L >= 512u ? 2 : 3)));
 }
 
-__global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffers b) {
+template <int NT, int PER>
+__global__ __launch_bounds__(NT) void gs_agg_scan_kernel(FrameParams fp, Buffers b) {
+  constexpr int NW = NT / 64, ROUND = NT * PER;
+  static_assert(NW >= 2 && NW <= 16 && 64 * PER <= 1023, "wave scan by lanes < NW; 10-bit queue fields");
   GS_PROBE_SCOPE(kPrAggScan);
   // per wave of a round: pair sum, reference sum, queue counts; per wave the
-  // exclusive bases (computed by lanes 0..15 of wave 0), and the round totals
-  __shared__ unsigned long long wsum[16], wref[16], wbase[16], wq[16];
-  __shared__ uint32_t wqb[kAggQueues][16], wvis[16], wmax[16];
+  // exclusive bases (computed by lanes 0..NW-1 of wave 0), and the round totals
+  __shared__ unsigned long long wsum[NW], wref[NW], wbase[NW], wq[NW];
+  __shared__ uint32_t wqb[kAggQueues][NW], wvis[NW], wmax[NW];
   __shared__ unsigned long long s_tot;
   __shared__ uint32_t s_qt[3];
-  __shared__ uint32_t s_c[kAggRound];  // a round's binned counts (striped in, blocked out)
-  __shared__ uint32_t s_a[kAggRound];  // ... their aggregated parts
+  __shared__ uint32_t s_c[ROUND];  // a round's binned counts (striped in, blocked out)
+  __shared__ uint32_t s_a[ROUND];  // ... their aggregated parts
   const int T = fp.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // a round's counters, read striped (coalesced: lane-consecutive tiles);
   // the first round's are issued before the V loads (one memory round trip
   // for both)
-  unsigned long long vs[kAggPer];
-  uint32_t fb[kAggPer];
+  unsigned long long vs[PER];
+  uint32_t fb[PER];
   auto load_round = [&](int r0) {
 #pragma unroll
-    for (int j = 0; j < kAggPer; ++j) {
-      const int i = r0 + j * 1024 + tid;
+    for (int j = 0; j < PER; ++j) {
+      const int i = r0 + j * NT + tid;
       vs[j] = i < T ? b.tile_cnt64[i] : 0ull;
       fb[j] = i < T ? b.tile_fb[i] : 0u;
     }
@@ -910,10 +913,10 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     uint32_t vr[8], vsum = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int i = tid + k * 1024;
+      const int i = tid + k * NT;
       vr[k] = i < nb ? b.block_rendered[i] : 0u;
     }
-    for (int i = tid + 8 * 1024; i < nb; i += 1024) vsum += b.block_rendered[i];
+    for (int i = tid + 8 * NT; i < nb; i += NT) vsum += b.block_rendered[i];
 #pragma unroll
     for (int k = 0; k < 8; ++k) vsum += vr[k];
 #pragma unroll
@@ -925,7 +928,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   unsigned long long carry = 0, rcarry = 0;
   uint32_t qcarry[3] = {0u, 0u, 0u};
   uint32_t mx = 0;
-  for (int r0 = 0; r0 < T; r0 += kAggRound) {
+  for (int r0 = 0; r0 < T; r0 += ROUND) {
     // the round's counters, read striped (coalesced: lane-consecutive tiles);
     // the histogram goes to tile_ref (and the group's footer) from here, the
     // counters are zeroed for the next frame, and the binned counts are
@@ -934,12 +937,12 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     {
       if (r0 > 0) load_round(r0);
 #pragma unroll
-      for (int j = 0; j < kAggPer; ++j) {
-        const int i = r0 + j * 1024 + tid;
+      for (int j = 0; j < PER; ++j) {
+        const int i = r0 + j * NT + tid;
         const uint32_t rf = (uint32_t)(vs[j] >> 32);
         rsum += rf;
-        s_c[j * 1024 + tid] = (uint32_t)vs[j] + fb[j];  // the tile's binned pairs
-        s_a[j * 1024 + tid] = (uint32_t)vs[j];          // ... of which the aggregated workgroups'
+        s_c[j * NT + tid] = (uint32_t)vs[j] + fb[j];  // the tile's binned pairs
+        s_a[j * NT + tid] = (uint32_t)vs[j];          // ... of which the aggregated workgroups'
         if (i < T) {
           b.tile_cnt64[i] = 0ull;  // zero for the next frame's projection
           b.tile_fb[i] = 0u;
@@ -949,13 +952,13 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       }
     }
     __syncthreads();
-    const int i0 = r0 + tid * kAggPer;
-    uint32_t v[kAggPer];
+    const int i0 = r0 + tid * PER;
+    uint32_t v[PER];
 #pragma unroll
-    for (int j = 0; j < kAggPer; ++j) v[j] = s_c[tid * kAggPer + j];
+    for (int j = 0; j < PER; ++j) v[j] = s_c[tid * PER + j];
     unsigned long long sum = 0, q = 0;
 #pragma unroll
-    for (int j = 0; j < kAggPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
       const uint32_t c = v[j];
       sum += c;
       mx = max(mx, c);
@@ -979,17 +982,17 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     }
     if (lane == 0) wref[wave] = rsum;
     __syncthreads();
-    if (tid < 16) {  // exclusive scan over the 16 waves
+    if (tid < NW) {  // exclusive scan over the NW waves
       const unsigned long long ws = wsum[tid], wqv = wq[tid];
-      unsigned long long si = ws, ri = wref[tid], qi = wqv;  // (queue counts: 5 fields of 10 bits, <= 256 each per wave)
+      unsigned long long si = ws, ri = wref[tid], qi = wqv;  // (queue counts: 5 fields of 10 bits, <= 64 PER each per wave)
       uint32_t qk[kAggQueues];
 #pragma unroll
       for (int k = 0; k < kAggQueues; ++k) qk[k] = (uint32_t)(wqv >> (10 * k)) & 1023u;
-      uint32_t qs[kAggQueues];  // (inclusive scans of the 16 waves' counts; a field can pass 1023 here)
+      uint32_t qs[kAggQueues];  // (inclusive scans of the NW waves' counts; a field can pass 1023 here)
 #pragma unroll
       for (int k = 0; k < kAggQueues; ++k) qs[k] = qk[k];
 #pragma unroll
-      for (int d = 1; d < 16; d <<= 1) {
+      for (int d = 1; d < NW; d <<= 1) {
         const unsigned long long o = __shfl_up(si, d, 64), orr = __shfl_up(ri, d, 64);
         uint32_t oq[kAggQueues];
 #pragma unroll
@@ -1005,7 +1008,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       wbase[tid] = carry + si - ws;
       uint32_t qt[kAggQueues];
 #pragma unroll
-      for (int k = 0; k < kAggQueues; ++k) qt[k] = __shfl(qs[k], 15, 64);
+      for (int k = 0; k < kAggQueues; ++k) qt[k] = __shfl(qs[k], NW - 1, 64);
       // queue bases of this round: small, big, then the medium lists longest
       // first (>= 1024, >= 512, > 256 keys: the sort, and a band's
       // longest-first blend, start the heaviest lists first)
@@ -1015,7 +1018,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
       wqb[2][tid] = mb1 + qs[2] - qk[2];
       wqb[3][tid] = mb2 + qs[3] - qk[3];
       wqb[4][tid] = qcarry[2] + qs[4] - qk[4];
-      const unsigned long long tot = __shfl(si, 15, 64), rtot = __shfl(ri, 15, 64);
+      const unsigned long long tot = __shfl(si, NW - 1, 64), rtot = __shfl(ri, NW - 1, 64);
       carry += tot;
       rcarry += rtot;
       qcarry[0] += qt[0];
@@ -1035,10 +1038,10 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     for (int k = 0; k < kAggQueues; ++k) qpos[k] = wqb[k][wave] + ((uint32_t)(qx >> (10 * k)) & 1023u);
     __syncthreads();  // (every thread has read its counts from s_c)
 #pragma unroll
-    for (int j = 0; j < kAggPer; ++j) {
+    for (int j = 0; j < PER; ++j) {
       const int i = i0 + j;
       const uint32_t c = v[j];
-      s_c[tid * kAggPer + j] = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);  // the tile start
+      s_c[tid * PER + j] = (uint32_t)(run < 0xFFFFFFFFull ? run : 0xFFFFFFFFull);  // the tile start
       if (i < T) {
         const int qq = agg_queue(c);
         const uint32_t pos = qpos[qq]++;
@@ -1052,13 +1055,13 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
     __syncthreads();
     // the tile starts back striped (coalesced stores)
 #pragma unroll
-    for (int j = 0; j < kAggPer; ++j) {
-      const int i = r0 + j * 1024 + tid;
+    for (int j = 0; j < PER; ++j) {
+      const int i = r0 + j * NT + tid;
       if (i < T) {
-        const uint32_t st = s_c[j * 1024 + tid];
+        const uint32_t st = s_c[j * NT + tid];
         b.tile_start[i] = st;
         // the fallback workgroups' pairs follow the aggregated ones'
-        b.tile_cursor[i] = st + s_a[j * 1024 + tid];
+        b.tile_cursor[i] = st + s_a[j * NT + tid];
       }
     }
     __syncthreads();  // the wave tables and s_c are rewritten by the next round
@@ -1069,7 +1072,7 @@ __global__ __launch_bounds__(1024) void gs_agg_scan_kernel(FrameParams fp, Buffe
   __syncthreads();
   if (tid == 0) {
     uint32_t vis = 0, m = 0;
-    for (int w = 0; w < 16; ++w) {
+    for (int w = 0; w < NW; ++w) {
       vis += wvis[w];
       m = max(m, wmax[w]);
     }
@@ -3295,6 +3298,8 @@ void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     gs_project_kernel<true, kProjLean><<<grid, 256, 0, s>>>(fp, b);
   else if (fp.pow2 && plain && fp.band_cull && fp.bin_agg)
     gs_project_kernel<true, kProjBand><<<grid, 256, 0, s>>>(fp, b);
+  else if (fp.pow2 && plain && !fp.band_cull && fp.bin_agg)
+    gs_project_kernel<true, kProjAgg><<<grid, 256, 0, s>>>(fp, b);
   else if (fp.pow2)
     gs_project_kernel<true, kProjAny><<<grid, 256, 0, s>>>(fp, b);
   else
@@ -3315,7 +3320,9 @@ hipError_t init_kernel_attributes() {
 
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.bin_agg) {
-    gs_agg_scan_kernel<<<1, 1024, 0, s>>>(fp, b);
+    // 256 threads (4 waves): a workgroup the dispatcher places as soon as
+    // one SIMD slot per SIMD of a CU is free, beside the other frames' waves
+    gs_agg_scan_kernel<256, 8><<<1, 256, 0, s>>>(fp, b);
     return;
   }
   if (!fp.bin_global && fp.n_chunks > 0 && fp.n_tiles > 0) {
