@@ -254,14 +254,15 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // frames/s, the sort launch overlapping the other frames' blends better;
   // config 5 1 440 against 1 453).  GSPLAT_BLEND_SORT=0 / 1 forces it off /
   // on (A/B).
-  // the projection and the aggregated emit as 2048 workgroups walking the
-  // 256-Gaussian blocks (one resident round: 8 per CU) rather than one per
-  // block: 8 bands of config 4, 40.2 -> 39.1 us per frame; of config 5,
-  // 308 -> 289 us; config 3 7 665 -> 7 738 frames/s (GSPLAT_PROJECT_GRID /
-  // GSPLAT_EMIT_GRID = G, 0: one workgroup per block)
+  // the aggregated emit as 2048 workgroups walking the 256-Gaussian blocks
+  // (one resident round: 8 per CU) rather than one per block: a band's culled
+  // blocks cost a loop iteration, not a workgroup (GSPLAT_EMIT_GRID = G, 0:
+  // one workgroup per block).  The projection keeps one workgroup per block
+  // by default (GSPLAT_PROJECT_GRID = G walks): inside the walking loop it
+  // needs 73-113 VGPRs instead of 51-57 (gs_kernels.hip)
   fp.emit_grid = r->env_emit_grid >= 0 ? r->env_emit_grid : 2048;
   fp.rec48 = r->env_rec48 > 0 ? 1 : 0;  // (A/B: GSPLAT_REC48=1)
-  fp.project_grid = r->env_project_grid >= 0 ? r->env_project_grid : 2048;
+  fp.project_grid = r->env_project_grid >= 0 ? r->env_project_grid : 0;
   fp.blend_sort = (fp.blend_bqw == 4 && fp.chunks_per_tile == 4 &&
                    (r->env_blend_sort == 1 || (r->env_blend_sort < 0 && r->band_nrows < r->tiles_y))) ? 1 : 0;
   fp.pair_cap = r->pair_cap;
