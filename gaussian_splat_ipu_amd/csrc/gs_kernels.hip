@@ -3458,9 +3458,10 @@ void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   f2.big_pass = 2;
   gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f2, b);
   // (the splitters of every big list were chosen by the frame's first split pass)
-  launch_big_buckets(f2, b, s, 256);
+  const unsigned g2 = fp.pass2_grid > 0 ? (unsigned)fp.pass2_grid : 256u;
+  launch_big_buckets(f2, b, s, g2);
   f2.blend_cont = 1;
-  const unsigned grid2 = std::min(grid, 256u);
+  const unsigned grid2 = std::min(grid, g2);
   if (fp.fast_exp)
     gs_blend_cont_kernel<true><<<grid2, block, 0, s>>>(f2, b);
   else

@@ -262,6 +262,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // needs 73-113 VGPRs instead of 51-57 (gs_kernels.hip)
   fp.emit_grid = r->env_emit_grid >= 0 ? r->env_emit_grid : 2048;
   fp.rec48 = r->env_rec48 > 0 ? 1 : 0;  // (A/B: GSPLAT_REC48=1)
+  fp.pass2_grid = r->env_pass2_grid;     // (A/B: GSPLAT_PASS2_GRID=G)
   fp.project_grid = r->env_project_grid >= 0 ? r->env_project_grid : 0;
   fp.blend_sort = (fp.blend_bqw == 4 && fp.chunks_per_tile == 4 &&
                    (r->env_blend_sort == 1 || (r->env_blend_sort < 0 && r->band_nrows < r->tiles_y))) ? 1 : 0;
@@ -701,6 +702,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_EMIT_GRID")) r->env_emit_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_REC48")) r->env_rec48 = std::atoi(ev) > 0 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_PASS2_GRID")) r->env_pass2_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_PROJECT_GRID")) r->env_project_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;  // else -1: auto
   int dev = cfg->device;
