@@ -3203,6 +3203,148 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   if (valid) store_pixel(fp, b, px, tyb * fp.tile_h + ly, q);
 }
 
+// Two pixels per lane (FrameParams::blend_px2, 16x16 tiles, no lazy big
+// lists): a wave covers a 16x8 half of the tile, lane l the pixels
+// (2 (l & 7), l >> 3) and the one right of it, with one mask per lane: the
+// records whose alpha box meets either pixel (8 pixel-pair column ballots and
+// 8 row ballots).  Per record the lane runs two independent chains (power,
+// exponential, composite) -- the record's LDS reads, the mask walk and the
+// h2 dy dy term are shared, each pixel's arithmetic is renderTile's in its
+// order (codelets.cpp:385-411) -- and a tile takes two waves, not four, so
+// its records are staged twice instead of four times.  A record is also
+// evaluated for the lane's pixel whose column it does not meet: power <
+// pcut there, so it is skipped exactly as the reference skips it.
+template <int EXP>
+__device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[64], uint32_t w, uint32_t h) {
+  unsigned long long m = ((unsigned long long)h << 32) | w;
+  while (m) {
+    const int ja = __builtin_ctzll(m);
+    m &= m - 1ull;
+    const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
+    asm volatile("" ::"v"(a1.z), "v"(a1.w), "v"(a2.x), "v"(a2.y));  // all loads issued up front
+    const float h0 = a0.z, h2 = a0.w, k1 = a1.x;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
+    const float dy = a0.y - qa.p.y;               // (one row: the same dy for both pixels)
+    const float h2dd = h2 * dy * dy;
+    const float dxa = a0.x - qa.p.x, dxb = a0.x - qb.p.x;
+    const float pa = (h0 * dxa * dxa + h2dd) - k1 * dxa * dy;
+    const float pb = (h0 * dxb * dxb + h2dd) - k1 * dxb * dy;
+    const float ea = EXP == kExpHw ? gs_expf_hw(pa) : (EXP == kExpInRange ? gs_expf_inrange(pa) : gs_expf(pa));
+    const float eb = EXP == kExpHw ? gs_expf_hw(pb) : (EXP == kExpInRange ? gs_expf_inrange(pb) : gs_expf(pb));
+    blend_composite(qa, pa, ea, a1, a2, true);
+    blend_composite(qb, pb, eb, a1, a2, true);
+    m = (qa.done && qb.done) ? 0ull : m;
+  }
+}
+
+// wid = (tile slot) * 2 + half; st: the wave's LDS staging of one batch
+template <bool HWEXP>
+__device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
+  const int slot = wid >> 1, half = wid & 1;
+  if (slot >= fp.n_tiles) return;
+  const int tile = blend_tile_of(fp, b, slot);
+  const int lane = threadIdx.x & 63;
+  const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
+  const int tile_x0 = tx * fp.tile_w;
+  const int tile_y0 = (fp.band_ty0 + tyb * fp.band_stride) * fp.tile_h;
+  const int pc = lane & 7, row = lane >> 3;  // pixel-pair column, row of the 16x8 half
+  const int lx = 2 * pc, ly = 8 * half + row;
+  const int px = tile_x0 + lx, py = tile_y0 + ly;
+  Px qa, qb;
+  qa.p = f32x2{(float)px, (float)py};
+  qb.p = f32x2{(float)(px + 1), (float)py};
+  qa.T = qb.T = 1.0f;
+  qa.c01 = qa.c23 = qb.c01 = qb.c23 = f32x2{0.0f, 0.0f};
+  const bool va = py < fp.height && px < fp.width, vb = py < fp.height && px + 1 < fp.width;
+  qa.done = !va;
+  qb.done = !vb;
+
+  uint32_t s, L;
+  tile_segment(fp, b, tile, s, L);
+  const uint32_t* __restrict__ list = b.list + s;
+  auto load_idx = [&](uint32_t k) -> uint32_t { return blend_idx(fp, list, L, k); };
+  const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
+  auto load_rec = [&](uint32_t g, float4& r0, float4& r1, float4& r2) {
+    if (fp.rec48) {
+      const float4* q3 = b.rec + 3 * (size_t)g;
+      r0 = q3[0];
+      r1 = q3[1];
+      r2 = q3[2];
+      return;
+    }
+    const float4* qq = b.rec + 2 * (size_t)g;
+    r0 = qq[0];
+    const float4 t = qq[1];    // k1 pcut boxx boxy
+    const float4 c = ccol[g];  // r g b opacity
+    r1 = make_float4(t.x, t.y, c.x, c.y);
+    r2 = make_float4(c.z, c.w, t.z, t.w);
+  };
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
+  uint32_t g_cur = load_idx(lane);
+  if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
+  uint32_t g_next = load_idx(64 + lane);
+
+  uint32_t staged = 0;
+  for (uint32_t base = 0; base < L; base += 64) {
+    if (ballot64(!(qa.done && qb.done)) == 0ull) break;
+    staged += min(64u, L - base);
+    const bool have = g_cur != 0xFFFFFFFFu;
+    st[0][lane] = make_float4(a0.x, a0.y, -0.5f * a0.z, -0.5f * a0.w);
+    st[1][lane] = a1;
+    st[2][lane] = a2;
+    const uint32_t boxx = __float_as_uint(a2.z), boxy = __float_as_uint(a2.w);
+    const int rx0 = (int)(boxx << 16) >> 16, rx1 = (int)boxx >> 16;
+    const int ry0 = (int)(boxy << 16) >> 16, ry1 = (int)boxy >> 16;
+    const bool rok = have && !(a2.y == 0.0f) && rx0 <= rx1 && ry0 <= ry1;
+    const bool fast = ballot64(rok && !(a1.y >= -80.0f)) == 0ull;
+    g_cur = g_next;
+    a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
+    g_next = load_idx(base + 128 + lane);
+    // pixel-pair column c meets the box iff floor((rx0 - bx) / 2) <= c <=
+    // floor((rx1 - bx) / 2); rows per pixel
+    const int bx = tile_x0, by = tile_y0 + 8 * half;
+    const int xlo = rok ? (rx0 - bx) >> 1 : 0x40000000, xsp = rok ? ((rx1 - bx) >> 1) - xlo : 0;
+    const int ylo = rok ? ry0 - by : 0x40000000, ysp = rok ? (ry1 - by) - ylo : 0;
+    uint32_t tab = 0u;
+    BallotTab<0, 0, 8>::run(tab, xlo, xsp);
+    BallotTab<8, 0, 8>::run(tab, ylo, ysp);
+    const int ac = 8 * pc, ar = 8 * (8 + row);
+    const uint32_t mcl = (uint32_t)__builtin_amdgcn_ds_bpermute(ac, (int)tab);
+    const uint32_t mch = (uint32_t)__builtin_amdgcn_ds_bpermute(ac + 4, (int)tab);
+    const uint32_t mrl = (uint32_t)__builtin_amdgcn_ds_bpermute(ar, (int)tab);
+    const uint32_t mrh = (uint32_t)__builtin_amdgcn_ds_bpermute(ar + 4, (int)tab);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool both = qa.done && qb.done;
+    const uint32_t m_lo = both ? 0u : (mcl & mrl), m_hi = both ? 0u : (mch & mrh);
+    if (HWEXP) {
+      blend_records_px2<kExpHw>(qa, qb, st, m_lo, m_hi);
+    } else if (fast) {
+      blend_records_px2<kExpInRange>(qa, qb, st, m_lo, m_hi);
+    } else {
+      blend_records_px2<kExpExact>(qa, qb, st, m_lo, m_hi);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // profiled frames: the staged records at this tile's wave slots 0 / 1 (2 / 3
+  // unused: zeroed, the host takes the tile's largest)
+  if (fp.count_records && lane == 0) {
+    b.blend_count[4 * slot + half] = staged;
+    b.blend_count[4 * slot + 2 + half] = 0u;
+  }
+  if (va) store_pixel(fp, b, px, tyb * fp.tile_h + ly, qa);
+  if (vb) store_pixel(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
+}
+
+template <bool HWEXP>
+__global__ __launch_bounds__(256) void gs_blend_px2_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBlend);
+  __shared__ float4 s_rec[4][3][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  blend_wave_px2<HWEXP>(fp, b, blockIdx.x * 4 + wave, s_rec[wave]);
+}
+
 // The sort inside the blend (FrameParams::blend_sort; one workgroup = the
 // four 8x8 blocks of one 16x16 tile): the workgroup first sorts its tile's
 // list -- as gs_sort_tiles_kernel would: <= 64 keys in wave 0's registers,
@@ -3408,6 +3550,14 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (waves == 0) return;
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
+  if (fp.blend_px2) {  // (16x16 tiles, no lazy lists, no in-blend sort: two waves per tile)
+    const unsigned g2 = (unsigned)((2L * fp.n_tiles + 3) / 4);
+    if (fp.fast_exp)
+      gs_blend_px2_kernel<true><<<g2, 256, 0, s>>>(fp, b);
+    else
+      gs_blend_px2_kernel<false><<<g2, 256, 0, s>>>(fp, b);
+    return;
+  }
   if (fp.blend_sort) {  // (blend_bqw == 4, chunks_per_tile == GS_BLEND_WPG: one workgroup per tile)
     if (fp.fast_exp)
       gs_blend_sort_kernel<true><<<grid, block, 0, s>>>(fp, b);

@@ -130,8 +130,8 @@ def test_synthetic_1080p_16x16(built):
     _assert_parity(s, f, g)
 
 
-@pytest.mark.parametrize("bsort,rec48", [("0", "0"), ("1", "0"), ("0", "1")])
-def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort, rec48):
+@pytest.mark.parametrize("bsort,rec48,px2", [("0", "0", "0"), ("1", "0", "0"), ("0", "1", "0"), ("0", "0", "1")])
+def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort, rec48, px2):
     """A clustered scene (config 5's construction) puts > 2048 Gaussians on
     some tiles: those go through the block-wide LSD radix sort, first inside
     the tile-sort launch (bsort 1: inside the blend's workgroups), then
@@ -141,6 +141,7 @@ def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort, rec48):
 
     monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
     monkeypatch.setenv("GSPLAT_REC48", rec48)
+    monkeypatch.setenv("GSPLAT_BLEND_PX2", px2)  # (the first frame; the lazy lists' frames keep one pixel per lane)
 
     src = scene.load_ply(PC12)
     cl = np.stack([src["x"], src["y"], src["z"]], 1)[:200]
@@ -513,7 +514,7 @@ def test_render_server_cli(built, tmp_path):
     assert out2.read_bytes() == data
 
 
-@pytest.mark.parametrize("bsort", ["0", "1"])
+@pytest.mark.parametrize("bsort", ["0", "1", "px2"])
 @pytest.mark.parametrize("half_width,log_scale,planes", [
     (1.5, -3.8, 4), (0.3, -4.0, 4), (1.5, -3.8, 64), (0.3, -4.0, 400), (0.3, -4.0, 1)])
 def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale, planes, bsort):
@@ -530,7 +531,8 @@ def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
 
-    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
+    monkeypatch.setenv("GSPLAT_BLEND_SORT", "0" if bsort == "px2" else bsort)
+    monkeypatch.setenv("GSPLAT_BLEND_PX2", "1" if bsort == "px2" else "0")
 
     g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=5, sh_degree=0)))
     a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
@@ -718,6 +720,25 @@ def test_rec48_bit_exact(pc12, monkeypatch):
     monkeypatch.setenv("GSPLAT_REC48", "1")
     g, bb = pc12
     W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    for band_count, band_index in [(1, 0), (8, 3)]:
+        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
+        _assert_parity(s, f, g, check_proj=False)
+        s.close()
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (1000, 700)])
+def test_blend_px2_bit_exact(pc12, monkeypatch, W, H):
+    """GSPLAT_BLEND_PX2=1: two pixels per blend lane (a 16x8 half of the tile
+    per wave, one mask per pixel pair, two independent chains per record)
+    gives the oracle's frame bit for bit: a whole frame (partial tiles at the
+    right and bottom edges for 1000x700) and a row band with the sort launch
+    (the in-blend sort keeps the one-pixel lanes)."""
+    from gaussian_splat_ipu_amd import camera
+
+    monkeypatch.setenv("GSPLAT_BLEND_PX2", "1")
+    monkeypatch.setenv("GSPLAT_BLEND_SORT", "0")
+    g, bb = pc12
     view, proj = camera.headless(bb, W, H)
     for band_count, band_index in [(1, 0), (8, 3)]:
         s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
