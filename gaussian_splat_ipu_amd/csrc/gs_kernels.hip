@@ -3600,15 +3600,16 @@ void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     gs_blend_cont_kernel<true><<<grid, block, 0, s>>>(f1, b);
   else
     gs_blend_cont_kernel<false><<<grid, block, 0, s>>>(f1, b);
-  // Pass 2 runs for a few lists per frame at most (config 5: ~3 of ~110
-  // continued lists) and is a no-op on most frames: its grid-stride kernels
-  // get small grids, so the no-op dispatches are short (the kernels return at
-  // once when counters[1] says no list outlived its window)
+  // Pass 2 runs for a few lists per frame (config 5: ~3 of ~110 continued
+  // lists); its kernels return at once when counters[1] says no list
+  // outlived its window.  Full grids: 256-workgroup grid-stride grids made
+  // the frames that do have pass-2 lists slower (config 5: continuation
+  // 204 -> 246 us, 1 535 -> 1 492 frames/s; GSPLAT_PASS2_GRID, A/B)
   FrameParams f2 = fp;
   f2.big_pass = 2;
   gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f2, b);
   // (the splitters of every big list were chosen by the frame's first split pass)
-  const unsigned g2 = fp.pass2_grid > 0 ? (unsigned)fp.pass2_grid : 256u;
+  const unsigned g2 = fp.pass2_grid > 0 ? (unsigned)fp.pass2_grid : 4096u;
   launch_big_buckets(f2, b, s, g2);
   f2.blend_cont = 1;
   const unsigned grid2 = std::min(grid, g2);

@@ -45,7 +45,7 @@ struct FrameParams {
   int blend_lpt;        // blend tiles longest list first (row bands), else in tile order
   int project_grid;     // > 0: the projection as this many workgroups walking the blocks (A/B)
   int emit_grid;
-  int pass2_grid;       // > 0: the lazy continuation's pass-2 grid-stride grids (A/B; default 256)
+  int pass2_grid;       // > 0: the lazy continuation's pass-2 grid-stride grids (A/B; default 4096)
   int rec48;            // the 48-B record with the colour and opacity in it (the blend's staged layout): no colour gather        // > 0: the aggregated emit as this many workgroups walking the blocks (A/B)
   int blend_sort;
   int blend_px2;        // two pixels per blend lane (16x16 tiles, no lazy lists, no in-blend sort): two waves per tile       // each blend workgroup (one 16x16 tile) sorts its tile's list first: no tile-sort launch
