@@ -2951,7 +2951,8 @@ __device__ __forceinline__ int blend_tile_of(const FrameParams& fp, const Buffer
 // wid = the wave's (tile slot, 8x8 block) item; st: the wave's LDS staging
 // of one batch (3 x 64 float4)
 template <int BQW, bool HWEXP>
-__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
+__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64],
+                                           int tile_in = -1) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
   if (slot >= fp.n_tiles) return;
@@ -2973,7 +2974,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   // where the tile order puts them (8 bands: blend 35.7 -> 29.3 us).  The
   // full frame keeps the tile order (neighbouring tiles share records in L2:
   // 75.1 against 76.1 us in queue order).
-  const int tile = fp.blend_cont ? (int)b.big_tiles[jb] : blend_tile_of(fp, b, slot);
+  const int tile = tile_in >= 0 ? tile_in : (fp.blend_cont ? (int)b.big_tiles[jb] : blend_tile_of(fp, b, slot));
   const int lane = threadIdx.x & 63;
   const int myq = lane >> 2;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
@@ -3238,10 +3239,13 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
 
 // wid = (tile slot) * 2 + half; st: the wave's LDS staging of one batch
 template <bool HWEXP>
-__device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
+// (tile_in >= 0: the tile, and count_slot its group of four words in
+// blend_count, given by the caller)
+__device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64],
+                                               int tile_in = -1, int count_slot = -1) {
   const int slot = wid >> 1, half = wid & 1;
   if (slot >= fp.n_tiles) return;
-  const int tile = blend_tile_of(fp, b, slot);
+  const int tile = tile_in >= 0 ? tile_in : blend_tile_of(fp, b, slot);
   const int lane = threadIdx.x & 63;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
   const int tile_x0 = tx * fp.tile_w;
@@ -3330,8 +3334,9 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
   // profiled frames: the staged records at this tile's wave slots 0 / 1 (2 / 3
   // unused: zeroed, the host takes the tile's largest)
   if (fp.count_records && lane == 0) {
-    b.blend_count[4 * slot + half] = staged;
-    b.blend_count[4 * slot + 2 + half] = 0u;
+    const int cs = count_slot >= 0 ? count_slot : slot;
+    b.blend_count[4 * cs + half] = staged;
+    b.blend_count[4 * cs + 2 + half] = 0u;
   }
   if (va) store_pixel(fp, b, px, tyb * fp.tile_h + ly, qa);
   if (vb) store_pixel(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
@@ -3343,6 +3348,28 @@ __global__ __launch_bounds__(256) void gs_blend_px2_kernel(FrameParams fp, Buffe
   __shared__ float4 s_rec[4][3][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   blend_wave_px2<HWEXP>(fp, b, blockIdx.x * 4 + wave, s_rec[wave]);
+}
+
+template <bool HWEXP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void gs_blend_px2h_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBlend);
+  __shared__ float4 s_rec[4][3][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // blend_px2 == 2: the lists longer than one wave's register sort (the big
+  // and medium queues, longest first) keep one pixel per lane and four waves
+  // per tile -- their waves' serial walks set the kernel's tail -- and the
+  // short lists (the small queue, tile order) take two pixels per lane, two
+  // tiles per workgroup.  Grid: n_tiles workgroups, the surplus exits.
+  const uint32_t nh = b.counters[0] + b.counters[7], ns = b.counters[9];
+  const uint32_t w = blockIdx.x;
+  if (w < nh) {
+    const int tile = (int)(w < b.counters[0] ? b.big_tiles[w] : b.medium_tiles[w - b.counters[0]]);
+    blend_wave<4, HWEXP>(fp, b, (int)w * 4 + wave, s_rec[wave], tile);
+    return;
+  }
+  const uint32_t k = 2u * (w - nh) + (uint32_t)(wave >> 1);
+  if (k >= ns) return;
+  blend_wave_px2<HWEXP>(fp, b, (int)k * 2 + (wave & 1), s_rec[wave], (int)b.small_tiles[k], (int)(nh + k));
 }
 
 // The sort inside the blend (FrameParams::blend_sort; one workgroup = the
@@ -3551,6 +3578,13 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
   if (fp.blend_px2) {  // (16x16 tiles, no lazy lists, no in-blend sort: two waves per tile)
+    if (fp.blend_px2 == 2) {
+      if (fp.fast_exp)
+        gs_blend_px2h_kernel<true><<<(unsigned)fp.n_tiles, 256, 0, s>>>(fp, b);
+      else
+        gs_blend_px2h_kernel<false><<<(unsigned)fp.n_tiles, 256, 0, s>>>(fp, b);
+      return;
+    }
     const unsigned g2 = (unsigned)((2L * fp.n_tiles + 3) / 4);
     if (fp.fast_exp)
       gs_blend_px2_kernel<true><<<g2, 256, 0, s>>>(fp, b);

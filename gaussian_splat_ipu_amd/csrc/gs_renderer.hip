@@ -307,9 +307,9 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   }
   fp.big_pass = 0;
   fp.blend_cont = 0;
-  // two pixels per blend lane (GSPLAT_BLEND_PX2=1, A/B)
+  // two pixels per blend lane (GSPLAT_BLEND_PX2=1; 2: only the short lists)
   fp.blend_px2 = (r->env_blend_px2 > 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !fp.lazy &&
-                  !fp.blend_sort) ? 1 : 0;
+                  !fp.blend_sort) ? r->env_blend_px2 : 0;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
@@ -705,7 +705,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_EMIT_GRID")) r->env_emit_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_REC48")) r->env_rec48 = std::atoi(ev) > 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_BLEND_PX2")) r->env_blend_px2 = std::atoi(ev) > 0 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_BLEND_PX2")) r->env_blend_px2 = std::max(0, std::min(2, std::atoi(ev)));
   if (const char* ev = std::getenv("GSPLAT_PASS2_GRID")) r->env_pass2_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_PROJECT_GRID")) r->env_project_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;  // else -1: auto
