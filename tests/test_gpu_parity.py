@@ -130,7 +130,8 @@ def test_synthetic_1080p_16x16(built):
     _assert_parity(s, f, g)
 
 
-@pytest.mark.parametrize("bsort,rec48,px2", [("0", "0", "0"), ("1", "0", "0"), ("0", "1", "0"), ("0", "0", "1")])
+@pytest.mark.parametrize("bsort,rec48,px2", [("0", "0", "0"), ("1", "0", "0"), ("0", "1", "0"), ("0", "0", "1"),
+                                              ("0", "0", "2")])
 def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort, rec48, px2):
     """A clustered scene (config 5's construction) puts > 2048 Gaussians on
     some tiles: those go through the block-wide LSD radix sort, first inside
@@ -514,7 +515,7 @@ def test_render_server_cli(built, tmp_path):
     assert out2.read_bytes() == data
 
 
-@pytest.mark.parametrize("bsort", ["0", "1", "px2"])
+@pytest.mark.parametrize("bsort", ["0", "1", "px2", "px2h"])
 @pytest.mark.parametrize("half_width,log_scale,planes", [
     (1.5, -3.8, 4), (0.3, -4.0, 4), (1.5, -3.8, 64), (0.3, -4.0, 400), (0.3, -4.0, 1)])
 def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale, planes, bsort):
@@ -531,8 +532,8 @@ def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
 
-    monkeypatch.setenv("GSPLAT_BLEND_SORT", "0" if bsort == "px2" else bsort)
-    monkeypatch.setenv("GSPLAT_BLEND_PX2", "1" if bsort == "px2" else "0")
+    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort if bsort in ("0", "1") else "0")
+    monkeypatch.setenv("GSPLAT_BLEND_PX2", {"px2": "1", "px2h": "2"}.get(bsort, "0"))
 
     g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=5, sh_degree=0)))
     a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
@@ -727,16 +728,18 @@ def test_rec48_bit_exact(pc12, monkeypatch):
         s.close()
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("W,H", [(1920, 1080), (1000, 700)])
-def test_blend_px2_bit_exact(pc12, monkeypatch, W, H):
+def test_blend_px2_bit_exact(pc12, monkeypatch, W, H, mode):
     """GSPLAT_BLEND_PX2=1: two pixels per blend lane (a 16x8 half of the tile
     per wave, one mask per pixel pair, two independent chains per record)
     gives the oracle's frame bit for bit: a whole frame (partial tiles at the
     right and bottom edges for 1000x700) and a row band with the sort launch
-    (the in-blend sort keeps the one-pixel lanes)."""
+    (the in-blend sort keeps the one-pixel lanes).  Mode 2: only the small
+    queue's tiles take two pixels per lane, the longer lists one."""
     from gaussian_splat_ipu_amd import camera
 
-    monkeypatch.setenv("GSPLAT_BLEND_PX2", "1")
+    monkeypatch.setenv("GSPLAT_BLEND_PX2", mode)
     monkeypatch.setenv("GSPLAT_BLEND_SORT", "0")
     g, bb = pc12
     view, proj = camera.headless(bb, W, H)
