@@ -307,9 +307,11 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   }
   fp.big_pass = 0;
   fp.blend_cont = 0;
-  // two pixels per blend lane (GSPLAT_BLEND_PX2=1; 2: only the short lists)
-  fp.blend_px2 = (r->env_blend_px2 > 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !fp.lazy &&
-                  !fp.blend_sort) ? r->env_blend_px2 : 0;
+  // two pixels per blend lane (GSPLAT_BLEND_PX2=1; 2: only the short lists,
+  // which lazy frames allow: their big lists keep the one-pixel waves whose
+  // state the continuation resumes)
+  fp.blend_px2 = (r->env_blend_px2 > 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !fp.blend_sort &&
+                  (!fp.lazy || r->env_blend_px2 == 2)) ? r->env_blend_px2 : 0;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);

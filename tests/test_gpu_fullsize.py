@@ -334,8 +334,9 @@ def test_ref_tile_major_readback(built, tw, th):
 
 
 # ------------------------------------------------------------- lazy big lists
+@pytest.mark.parametrize("px2", ["0", "2"])
 @pytest.mark.parametrize("op_lo,op_hi", [(0.004, 0.02), (0.02, 0.3)])
-def test_lazy_big_lists_continuation(built, op_lo, op_hi):
+def test_lazy_big_lists_continuation(built, monkeypatch, op_lo, op_hi, px2):
     """Big lists (> 2048 keys) of faint Gaussians: pixels outlive the sorted
     prefix of ~1.5 k keys, so their blend waves save their state and continue
     over the sorted window of the next keys (pass 1); waves that outlive the
@@ -343,9 +344,12 @@ def test_lazy_big_lists_continuation(built, op_lo, op_hi):
     gs_kernels.hip, lazy big lists).  The second frame of the renderer takes
     that path; the frame must equal the oracle's bit for bit.  op 0.004-0.02:
     nearly every big tile continues, and some pixels never saturate (pass 2);
-    0.02-0.3: some do."""
+    0.02-0.3: some do.  px2 2: the short lists' tiles blend two pixels per
+    lane beside the big lists' one-pixel waves."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
+
+    monkeypatch.setenv("GSPLAT_BLEND_PX2", px2)
 
     src = scene.load_ply(PC12)
     centres = np.stack([src["x"], src["y"], src["z"]], 1)[::4]
