@@ -24,4 +24,15 @@ for rep in 1 2 3; do
     line $O/c3_${v}_$rep.json
   done
 done
+for rep in 1 2; do
+  for v in base px2h; do
+    echo "== c5 $v rep $rep $(date +%T)"
+    case $v in
+      base) E="" ;;
+      px2h) E="GSPLAT_BLEND_PX2=2" ;;
+    esac
+    env $E timeout -k 10 400 python bench.py --config5 --steps 240 --warmup 120 --no-cpu-baseline > $O/c5_${v}_$rep.json 2> $O/c5_${v}_$rep.err || exit $?
+    line $O/c5_${v}_$rep.json
+  done
+done
 echo "== done $(date +%T)"
