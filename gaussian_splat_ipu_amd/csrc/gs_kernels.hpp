@@ -48,7 +48,7 @@ struct FrameParams {
   int pass2_grid;       // > 0: the lazy continuation's pass-2 grid-stride grids (A/B; default 4096)
   int rec48;            // the 48-B record with the colour and opacity in it (the blend's staged layout): no colour gather        // > 0: the aggregated emit as this many workgroups walking the blocks (A/B)
   int blend_sort;
-  int blend_px2;        // two pixels per blend lane (16x16 tiles, no lazy lists, no in-blend sort): two waves per tile       // each blend workgroup (one 16x16 tile) sorts its tile's list first: no tile-sort launch
+  int blend_px2;        // two pixels per blend lane (16x16 tiles, no in-blend sort): 1 every tile (no lazy lists), 2 the short lists       // each blend workgroup (one 16x16 tile) sorts its tile's list first: no tile-sort launch
   unsigned long long pair_cap;
   int write_rgba;
   int bgr_pitch;      // bytes per row of the BGR8 output

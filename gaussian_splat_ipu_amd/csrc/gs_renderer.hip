@@ -307,11 +307,18 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   }
   fp.big_pass = 0;
   fp.blend_cont = 0;
-  // two pixels per blend lane (GSPLAT_BLEND_PX2=1; 2: only the short lists,
-  // which lazy frames allow: their big lists keep the one-pixel waves whose
-  // state the continuation resumes)
-  fp.blend_px2 = (r->env_blend_px2 > 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !fp.blend_sort &&
-                  (!fp.lazy || r->env_blend_px2 == 2)) ? r->env_blend_px2 : 0;
+  // two pixels per blend lane on whole frames without lazy big lists
+  // (config 3: 8 235 -> 8 454 frames/s, three interleaved repeats, although
+  // the blend alone, one frame in flight, takes 87 instead of 77 us: half
+  // the waves, each with two pixel chains, leave CUs to the other frames and
+  // stage each tile's records twice instead of four times).
+  // GSPLAT_BLEND_PX2=0 keeps one pixel per lane; =2 takes two pixels only on
+  // the short lists' tiles, which lazy frames allow (their big lists keep the
+  // one-pixel waves whose state the continuation resumes): config 3 8 196,
+  // config 5 1 520 -> 1 482, so not the default.
+  const int px2 = r->env_blend_px2 >= 0 ? r->env_blend_px2 : 1;
+  fp.blend_px2 = (px2 > 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !fp.blend_sort &&
+                  (!fp.lazy || px2 == 2)) ? px2 : 0;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
