@@ -102,7 +102,7 @@ STAGE_KERNELS = {
     "scan": ["gs_count", "gs_colscan", "gs_scan_multi", "gs_scan", "gs_agg_scan"],
     "emit": ["gs_emit_chunk", "gs_emit", "gs_agg_emit"],
     "sort": ["gs_sort_tiles", "gs_big_prefix", "gs_big_split", "gs_big_select", "gs_big_psort"],
-    "blend": ["gs_blend", "gs_blend_sort", "gs_blend_px2", "gs_blend_px2h"],
+    "blend": ["gs_blend", "gs_blend_sort", "gs_blend_px2", "gs_blend_px2h", "gs_blend_sort_px2"],
     # lazy big lists (config 5): the windows of the flagged lists sorted, the
     # continued blend (PMC: its per-launch average over the frame's two launches)
     "blend_cont": ["gs_big_cont", "gs_blend_cont"],

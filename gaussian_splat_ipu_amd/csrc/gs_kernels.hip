@@ -3438,6 +3438,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   blend_wave<4, HWEXP>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
 }
 
+// The in-blend sort with two-pixel lanes (FrameParams::blend_px2 with
+// blend_sort): a workgroup = two tiles (LPT slots 2w, 2w + 1), sorted one
+// after the other by all four waves, then blended by two waves each.
+template <bool HWEXP>
+__global__ __launch_bounds__(256) void gs_blend_sort_px2_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBlend);
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int slot0 = 2 * (int)blockIdx.x;
+  if (slot0 >= fp.n_tiles) return;
+#pragma unroll 1
+  for (int k = 0; k < 2; ++k) {
+    if (slot0 + k >= fp.n_tiles) break;  // (uniform)
+    blend_sort_tile(fp, b, blend_tile_of(fp, b, slot0 + k), reinterpret_cast<unsigned long long*>(lds));
+    __syncthreads();  // the list's stores done; the LDS free again
+  }
+  blend_wave_px2<HWEXP>(fp, b, (int)blockIdx.x * 4 + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
+}
+
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
 // the prefix blend).  A grid-stride loop over the waves of the big lists
 // only: a grid of every tile's waves, nearly all of which exit at once, cost
@@ -3577,7 +3596,7 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (waves == 0) return;
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
-  if (fp.blend_px2) {  // (16x16 tiles, no lazy lists, no in-blend sort: two waves per tile)
+  if (fp.blend_px2 && !fp.blend_sort) {  // (16x16 tiles, no lazy lists: two waves per tile)
     if (fp.blend_px2 == 2) {
       if (fp.fast_exp)
         gs_blend_px2h_kernel<true><<<(unsigned)fp.n_tiles, 256, 0, s>>>(fp, b);
@@ -3590,6 +3609,14 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
       gs_blend_px2_kernel<true><<<g2, 256, 0, s>>>(fp, b);
     else
       gs_blend_px2_kernel<false><<<g2, 256, 0, s>>>(fp, b);
+    return;
+  }
+  if (fp.blend_sort && fp.blend_px2) {  // (two tiles per workgroup)
+    const unsigned g2 = (unsigned)((fp.n_tiles + 1) / 2);
+    if (fp.fast_exp)
+      gs_blend_sort_px2_kernel<true><<<g2, 256, 0, s>>>(fp, b);
+    else
+      gs_blend_sort_px2_kernel<false><<<g2, 256, 0, s>>>(fp, b);
     return;
   }
   if (fp.blend_sort) {  // (blend_bqw == 4, chunks_per_tile == GS_BLEND_WPG: one workgroup per tile)

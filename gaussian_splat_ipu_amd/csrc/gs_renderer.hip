@@ -319,6 +319,9 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   const int px2 = r->env_blend_px2 >= 0 ? r->env_blend_px2 : 1;
   fp.blend_px2 = (px2 > 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !fp.blend_sort &&
                   (!fp.lazy || px2 == 2)) ? px2 : 0;
+  // row bands (the in-blend sort): two-pixel lanes, two tiles per workgroup
+  // (GSPLAT_BAND_PX2=1, A/B)
+  if (fp.blend_sort && !fp.lazy && r->env_band_px2 > 0) fp.blend_px2 = 1;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
@@ -715,6 +718,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_EMIT_GRID")) r->env_emit_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_REC48")) r->env_rec48 = std::atoi(ev) > 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_BLEND_PX2")) r->env_blend_px2 = std::max(0, std::min(2, std::atoi(ev)));
+  if (const char* ev = std::getenv("GSPLAT_BAND_PX2")) r->env_band_px2 = std::atoi(ev) > 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_PASS2_GRID")) r->env_pass2_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_PROJECT_GRID")) r->env_project_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;  // else -1: auto

@@ -747,3 +747,20 @@ def test_blend_px2_bit_exact(pc12, monkeypatch, W, H, mode):
         s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
         _assert_parity(s, f, g, check_proj=False)
         s.close()
+
+
+def test_band_px2_bit_exact(pc12, monkeypatch):
+    """GSPLAT_BAND_PX2=1: row bands with the in-blend sort and two-pixel
+    lanes (two tiles per workgroup, sorted one after the other), bit for
+    bit against the oracle on three bands of an 8-way split."""
+    from gaussian_splat_ipu_amd import camera
+
+    monkeypatch.setenv("GSPLAT_BAND_PX2", "1")
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    for band_index in (0, 3, 7):
+        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=8, band_index=band_index)
+        assert s.stats()["paths"] & 2
+        _assert_parity(s, f, g, check_proj=False)
+        s.close()
