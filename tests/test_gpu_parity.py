@@ -728,19 +728,24 @@ def test_rec48_bit_exact(pc12, monkeypatch):
         s.close()
 
 
+@pytest.mark.parametrize("lpt", ["auto", "0"])
 @pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("W,H", [(1920, 1080), (1000, 700)])
-def test_blend_px2_bit_exact(pc12, monkeypatch, W, H, mode):
+def test_blend_px2_bit_exact(pc12, monkeypatch, W, H, mode, lpt):
     """GSPLAT_BLEND_PX2=1: two pixels per blend lane (a 16x8 half of the tile
     per wave, one mask per pixel pair, two independent chains per record)
     gives the oracle's frame bit for bit: a whole frame (partial tiles at the
     right and bottom edges for 1000x700) and a row band with the sort launch
     (the in-blend sort keeps the one-pixel lanes).  Mode 2: only the small
-    queue's tiles take two pixels per lane, the longer lists one."""
+    queue's tiles take two pixels per lane, the longer lists one.  Whole
+    frames with two-pixel lanes take the tiles longest list first by default
+    (lpt "auto"); "0" keeps the tile order."""
     from gaussian_splat_ipu_amd import camera
 
     monkeypatch.setenv("GSPLAT_BLEND_PX2", mode)
     monkeypatch.setenv("GSPLAT_BLEND_SORT", "0")
+    if lpt != "auto":
+        monkeypatch.setenv("GSPLAT_BLEND_LPT", lpt)
     g, bb = pc12
     view, proj = camera.headless(bb, W, H)
     for band_count, band_index in [(1, 0), (8, 3)]:
