@@ -52,15 +52,6 @@
 #ifndef GS_PX2_INTERLEAVE
 #define GS_PX2_INTERLEAVE 1
 #endif
-// (A/B) the interleaved two-pixel step's colour updates without branches
-#ifndef GS_PX2_BRANCHFREE
-#define GS_PX2_BRANCHFREE 0
-#endif
-// (A/B) one-pixel blend: the next record's reads and exponential issued
-// before this record's composite
-#ifndef GS_BLEND_PIPE
-#define GS_BLEND_PIPE 0
-#endif
 // the one-pixel blend kernels' fewest waves per SIMD (8: at most 64 VGPRs)
 #ifndef GS_BLEND_WPE
 #define GS_BLEND_WPE 8
@@ -2912,34 +2903,6 @@ __device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers
 template <int EXP>
 __device__ __forceinline__ void blend_records(Px& q, float4 (*st)[64], uint32_t w, uint32_t h) {
   unsigned long long m = ((unsigned long long)h << 32) | w;
-#if GS_BLEND_PIPE
-  // (A/B) software-pipelined: the next record's LDS reads, power and
-  // exponential (independent of the pixel's state) are issued before this
-  // record's composite, so the LDS round trip and the exponential overlap
-  // the T / colour update instead of following it.  Same records, same
-  // order, same operations.
-  if (!m) return;
-  int ja = __builtin_ctzll(m);
-  m &= m - 1ull;
-  float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
-  float pa;
-  float ea = blend_power_exp<EXP>(q, a0, a1, pa);
-  for (;;) {
-    const bool more = m != 0ull;
-    const int jn = more ? __builtin_ctzll(m) : 0;
-    m &= m - 1ull;
-    const float4 n0 = st[0][jn], n1 = st[1][jn], n2 = st[2][jn];
-    blend_composite(q, pa, ea, a1, a2, true);
-    if (!more || q.done) break;
-    float pn;
-    const float en = blend_power_exp<EXP>(q, n0, n1, pn);
-    a1 = n1;
-    a2 = n2;
-    pa = pn;
-    ea = en;
-  }
-  return;
-#endif
   while (m) {
     const int ja = __builtin_ctzll(m);
     m &= m - 1ull;
@@ -3291,23 +3254,6 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
     const bool hitb = !qb.done && !(pb > 0.0f) && !(pb < pcut) && !(alb < 1.0f / 255.0f);
     const bool brka = hita && tta < 0.0001f, brkb = hitb && ttb < 0.0001f;
     const bool upda = hita && !brka, updb = hitb && !brkb;
-#if GS_PX2_BRANCHFREE
-    // (A/B) no update branches: a pixel that does not take the record adds
-    // (c * 0) * T = +-0 to each channel (the same sums) and keeps its T
-    {
-      const float wa = upda ? ala : 0.0f, wb = updb ? alb : 0.0f;
-      qa.c01.x = qa.c01.x + (a1.z * wa) * qa.T;
-      qa.c01.y = qa.c01.y + (a1.w * wa) * qa.T;
-      qa.c23.x = qa.c23.x + (a2.x * wa) * qa.T;
-      qa.c23.y = qa.c23.y + (op * wa) * qa.T;
-      qb.c01.x = qb.c01.x + (a1.z * wb) * qb.T;
-      qb.c01.y = qb.c01.y + (a1.w * wb) * qb.T;
-      qb.c23.x = qb.c23.x + (a2.x * wb) * qb.T;
-      qb.c23.y = qb.c23.y + (op * wb) * qb.T;
-      qa.T = upda ? tta : qa.T;
-      qb.T = updb ? ttb : qb.T;
-    }
-#else
     if (__builtin_expect(upda, 0)) {
       qa.c01.x = qa.c01.x + (a1.z * ala) * qa.T;
       qa.c01.y = qa.c01.y + (a1.w * ala) * qa.T;
@@ -3322,7 +3268,6 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
       qb.c23.y = qb.c23.y + (op * alb) * qb.T;
       qb.T = ttb;
     }
-#endif
     qa.done = qa.done || brka;
     qb.done = qb.done || brkb;
 #else
