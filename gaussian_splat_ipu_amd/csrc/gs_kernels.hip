@@ -2207,15 +2207,28 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   // big lists: radix-sorted here (4 keys per lane and round) unless the
   // segmented merge sort has taken them this frame (FrameParams::big_separate)
   const uint32_t n_big = fp.big_separate ? 0u : b.counters[0];
+  // FrameParams::blend_seg: each list's (tile, start, length) at its blend
+  // slot (the queues' order: big, medium, small)
+  auto put_seg = [&](uint32_t slot, uint32_t t, uint32_t s, uint32_t L) {
+    if (fp.blend_seg && (threadIdx.x & 63) == 0) b.blend_seg[slot] = make_uint4(t, s, L, 0u);
+  };
   if (blockIdx.x < n_big) {  // the longest lists first
-    radix_sort_tile<NT, 4>(fp, b, (int)b.big_tiles[blockIdx.x], r_hist, r_base, r_wcnt);
+    const uint32_t t = b.big_tiles[blockIdx.x];
+    if (fp.blend_seg && threadIdx.x == 0) {
+      uint32_t s, L;
+      tile_segment(fp, b, (int)t, s, L);
+      put_seg(blockIdx.x, t, s, L);
+    }
+    radix_sort_tile<NT, 4>(fp, b, (int)t, r_hist, r_base, r_wcnt);
     return;
   }
   const uint32_t n_med = b.counters[7], n_small = b.counters[9];
   const uint32_t item = blockIdx.x - n_big;
   if (item < n_med) {
     uint32_t s, L;
-    tile_segment(fp, b, (int)b.medium_tiles[item], s, L);
+    const uint32_t t = b.medium_tiles[item];
+    tile_segment(fp, b, (int)t, s, L);
+    if (threadIdx.x == 0) put_seg(n_big + item, t, s, L);
     if (!merge_sort_tile<NT, 2, kOutDevice>(b, s, L, keys)) {
       __syncthreads();  // a long run of equal depths: again with input-index keys
       merge_sort_tile<NT, 2, kOutInput, kSrcRekey>(b, s, L, keys);
@@ -2227,7 +2240,9 @@ __device__ __forceinline__ void sort_tiles(const FrameParams& fp, const Buffers&
   if (k >= n_small) return;
   const int lane = threadIdx.x & 63;
   uint32_t s, L;
-  tile_segment(fp, b, (int)b.small_tiles[k], s, L);
+  const uint32_t t = b.small_tiles[k];
+  tile_segment(fp, b, (int)t, s, L);
+  put_seg(n_big + n_med + k, t, s, L);
   // this wave's slice of the (here unused) merge buffer, for a list with
   // equal depths
   static_assert(NW * kSortRegCap <= kWords / 2, "small-list slices fit the merge buffer");
@@ -3286,7 +3301,19 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
                                                int tile_in = -1, int count_slot = -1) {
   const int slot = wid >> 1, half = wid & 1;
   if (slot >= fp.n_tiles) return;
-  const int tile = tile_in >= 0 ? tile_in : blend_tile_of(fp, b, slot);
+  int tile;
+  uint32_t s, L;
+  if (fp.blend_seg && !fp.blend_sort && tile_in < 0) {
+    // the slot's tile and list segment in one load (the sort launch's);
+    // otherwise the queue entry, then the tile's start and end
+    const uint4 sg = b.blend_seg[slot];
+    tile = (int)sg.x;
+    s = sg.y;
+    L = sg.z;
+  } else {
+    tile = tile_in >= 0 ? tile_in : blend_tile_of(fp, b, slot);
+    tile_segment(fp, b, tile, s, L);
+  }
   const int lane = threadIdx.x & 63;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
   const int tile_x0 = tx * fp.tile_w;
@@ -3303,8 +3330,6 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
   qa.done = !va;
   qb.done = !vb;
 
-  uint32_t s, L;
-  tile_segment(fp, b, tile, s, L);
   const uint32_t* __restrict__ list = b.list + s;
   auto load_idx = [&](uint32_t k) -> uint32_t { return blend_idx(fp, list, L, k); };
   const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;

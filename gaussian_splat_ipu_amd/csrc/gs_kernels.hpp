@@ -43,6 +43,9 @@ struct FrameParams {
   int chunks_per_tile;  // blend waves per tile (16 pixel quads each)
   int blend_bqw;        // blend wave = 4x4 quads (8x8 px) | 8x2 quads (16x4 px) | 0: quad run
   int blend_lpt;        // blend tiles longest list first (row bands), else in tile order
+  int blend_seg;        // (blend_lpt, two-pixel lanes, the sort launch sorts every list) the
+                        //   sort launch writes each slot's (tile, start, length), the blend
+                        //   reads it in one load
   int project_grid;     // > 0: the projection as this many workgroups walking the blocks (A/B)
   int emit_grid;
   int pass2_grid;       // > 0: the lazy continuation's pass-2 grid-stride grids (A/B; default 4096)
@@ -133,7 +136,10 @@ struct Buffers {
   uint32_t* bk_list;        // bucket -> big-list slot
   uint32_t* bk_off;         // [n_tiles + 1]  big-list slot -> first bucket
   uint32_t* medium_tiles;   // [n_tiles]  lists in (kSortRegCap, kSortLdsCap] (block sort queue)
-  uint32_t* small_tiles;    // [n_tiles]  lists in [1, kSortRegCap] (one-wave sort queue)
+  uint32_t* small_tiles;    // [n_tiles]  lists in [0, kSortRegCap] (one-wave sort queue)
+  uint4* blend_seg;         // [n_tiles]  (tile, list start, list length, 0) in the blend's
+                            //   longest-first slot order, written by the sort launch
+                            //   (FrameParams::blend_seg)
   uint32_t* chunk_off;      // [n_chunks][n_tiles] chunk histograms -> offsets
   uint4* tile_agg;          // [2 * ceil(n_tiles / 64)] per 64 tiles: list-length sum (lo, hi),
                             //   small | medium << 8 | big << 16 counts, max length;

@@ -327,6 +327,10 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // longest lists first) -- config 3 blend 86.4 -> 79.4 us alone, 8 451 ->
   // 8 524 frames/s, three interleaved repeats (GSPLAT_BLEND_LPT=0: tile order)
   if (fp.blend_px2 == 1 && r->env_blend_lpt < 0) fp.blend_lpt = 1;
+  // ... and read their slot's tile and list segment in one load, written by
+  // the sort launch (which sorts every list when big_separate is off)
+  fp.blend_seg = (fp.blend_px2 == 1 && fp.blend_lpt && !fp.blend_sort && !fp.big_separate && !fp.lazy &&
+                  r->env_blend_seg != 0) ? 1 : 0;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
@@ -724,6 +728,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if (const char* ev = std::getenv("GSPLAT_REC48")) r->env_rec48 = std::atoi(ev) > 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_BLEND_PX2")) r->env_blend_px2 = std::max(0, std::min(2, std::atoi(ev)));
   if (const char* ev = std::getenv("GSPLAT_BAND_PX2")) r->env_band_px2 = std::atoi(ev) > 0 ? 1 : 0;
+  if (const char* ev = std::getenv("GSPLAT_BLEND_SEG")) r->env_blend_seg = std::atoi(ev) != 0 ? 1 : 0;
   if (const char* ev = std::getenv("GSPLAT_PASS2_GRID")) r->env_pass2_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_PROJECT_GRID")) r->env_project_grid = std::max(0, std::atoi(ev));
   if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;  // else -1: auto
@@ -890,7 +895,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.counters = (uint32_t*)r->d_zero;
   r->buf.tile_count = (uint32_t*)r->d_zero + 16;
   const size_t n_agg = (T + 63) / 64;
-  const size_t tiles_bytes = (T + 1 + 4 * T) * 4 + n_agg * 32 + 16 + T * 8 + 8 + T * 4 + T * 4;
+  const size_t tiles_bytes = (T + 1 + 4 * T) * 4 + n_agg * 32 + 16 + T * 8 + 8 + T * 4 + T * 4 + 16 + T * 16;
   if ((e = hipMalloc(&r->d_tiles, tiles_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(tiles)"));
   poison(r->d_tiles, tiles_bytes, "tiles");
   r->buf.tile_start = (uint32_t*)r->d_tiles;
@@ -904,6 +909,7 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.tile_cnt64 = (unsigned long long*)(((uintptr_t)(r->buf.tile_agg + 2 * n_agg) + 7) & ~(uintptr_t)7);
   r->buf.tile_ref = (uint32_t*)(r->buf.tile_cnt64 + T);
   r->buf.tile_fb = r->buf.tile_ref + T;
+  r->buf.blend_seg = (uint4*)(((uintptr_t)(r->buf.tile_fb + T) + 15) & ~(uintptr_t)15);
   if ((e = hipMemset(r->d_tiles, 0, (T + 1 + 4 * T) * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMemset(tiles)"));
   if ((e = hipMemset(r->buf.tile_cnt64, 0, T * 8)) != hipSuccess) return fail(hip_fail(e, "hipMemset(tile counters)"));

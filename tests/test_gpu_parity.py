@@ -728,7 +728,7 @@ def test_rec48_bit_exact(pc12, monkeypatch):
         s.close()
 
 
-@pytest.mark.parametrize("lpt", ["auto", "0"])
+@pytest.mark.parametrize("lpt", ["auto", "0", "noseg"])
 @pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("W,H", [(1920, 1080), (1000, 700)])
 def test_blend_px2_bit_exact(pc12, monkeypatch, W, H, mode, lpt):
@@ -739,12 +739,16 @@ def test_blend_px2_bit_exact(pc12, monkeypatch, W, H, mode, lpt):
     (the in-blend sort keeps the one-pixel lanes).  Mode 2: only the small
     queue's tiles take two pixels per lane, the longer lists one.  Whole
     frames with two-pixel lanes take the tiles longest list first by default
-    (lpt "auto"); "0" keeps the tile order."""
+    (lpt "auto"), reading each slot's tile and list segment from the sort
+    launch's table; "noseg" reads the queues and tile starts instead
+    (GSPLAT_BLEND_SEG=0); "0" keeps the tile order."""
     from gaussian_splat_ipu_amd import camera
 
     monkeypatch.setenv("GSPLAT_BLEND_PX2", mode)
     monkeypatch.setenv("GSPLAT_BLEND_SORT", "0")
-    if lpt != "auto":
+    if lpt == "noseg":
+        monkeypatch.setenv("GSPLAT_BLEND_SEG", "0")
+    elif lpt != "auto":
         monkeypatch.setenv("GSPLAT_BLEND_LPT", lpt)
     g, bb = pc12
     view, proj = camera.headless(bb, W, H)
