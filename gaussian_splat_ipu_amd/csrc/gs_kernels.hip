@@ -52,11 +52,6 @@
 #ifndef GS_PX2_INTERLEAVE
 #define GS_PX2_INTERLEAVE 1
 #endif
-// two-pixel blend: the record loop as a wave-uniform loop (1) or a per-lane
-// loop (0)
-#ifndef GS_PX2_UNIFORM
-#define GS_PX2_UNIFORM 0
-#endif
 // the one-pixel blend kernels' fewest waves per SIMD (8: at most 64 VGPRs)
 #ifndef GS_BLEND_WPE
 #define GS_BLEND_WPE 8
@@ -3247,20 +3242,8 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
 template <int EXP>
 __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[64], uint32_t w, uint32_t h) {
   unsigned long long m = ((unsigned long long)h << 32) | w;
-#if GS_PX2_UNIFORM
-  // The wave steps while any lane has a record left (one ballot, a scalar
-  // branch); a lane whose mask is empty runs the step on record 0 with its
-  // decisions forced off.  Its lanes were masked off before, which costs the
-  // wave the same issue cycles, but the per-lane loop exit needed exec-mask
-  // bookkeeping every step.
-  while (ballot64(m != 0ull) != 0ull) {
-    const bool live = m != 0ull;
-    const int ja = live ? __builtin_ctzll(m) : 0;
-#else
   while (m) {
-    constexpr bool live = true;
     const int ja = __builtin_ctzll(m);
-#endif
     m &= m - 1ull;
     const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
     asm volatile("" ::"v"(a1.z), "v"(a1.w), "v"(a2.x), "v"(a2.y));  // all loads issued up front
@@ -3282,8 +3265,8 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
     const float ala = (va < 0.99f) ? va : 0.99f, alb = (vb < 0.99f) ? vb : 0.99f;
     const float tta = qa.T * (1.0f - ala), ttb = qb.T * (1.0f - alb);
     asm volatile("" ::"v"(ala), "v"(alb), "v"(tta), "v"(ttb));
-    const bool hita = live && !qa.done && !(pa > 0.0f) && !(pa < pcut) && !(ala < 1.0f / 255.0f);
-    const bool hitb = live && !qb.done && !(pb > 0.0f) && !(pb < pcut) && !(alb < 1.0f / 255.0f);
+    const bool hita = !qa.done && !(pa > 0.0f) && !(pa < pcut) && !(ala < 1.0f / 255.0f);
+    const bool hitb = !qb.done && !(pb > 0.0f) && !(pb < pcut) && !(alb < 1.0f / 255.0f);
     const bool brka = hita && tta < 0.0001f, brkb = hitb && ttb < 0.0001f;
     const bool upda = hita && !brka, updb = hitb && !brkb;
     if (__builtin_expect(upda, 0)) {
@@ -3303,8 +3286,8 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
     qa.done = qa.done || brka;
     qb.done = qb.done || brkb;
 #else
-    blend_composite(qa, pa, ea, a1, a2, live);
-    blend_composite(qb, pb, eb, a1, a2, live);
+    blend_composite(qa, pa, ea, a1, a2, true);
+    blend_composite(qb, pb, eb, a1, a2, true);
 #endif
     m = (qa.done && qb.done) ? 0ull : m;
   }
