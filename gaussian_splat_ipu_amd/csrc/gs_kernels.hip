@@ -52,6 +52,10 @@
 #ifndef GS_PX2_INTERLEAVE
 #define GS_PX2_INTERLEAVE 1
 #endif
+// two-pixel blend: waves per workgroup (2 = one tile, 4 = two tiles)
+#ifndef GS_PX2_WPG
+#define GS_PX2_WPG 4
+#endif
 // the one-pixel blend kernels' fewest waves per SIMD (8: at most 64 VGPRs)
 #ifndef GS_BLEND_WPE
 #define GS_BLEND_WPE 8
@@ -3409,11 +3413,11 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
 }
 
 template <bool HWEXP>
-__global__ __launch_bounds__(256) void gs_blend_px2_kernel(FrameParams fp, Buffers b) {
+__global__ __launch_bounds__(64 * GS_PX2_WPG) void gs_blend_px2_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrBlend);
-  __shared__ float4 s_rec[4][3][64];
+  __shared__ float4 s_rec[GS_PX2_WPG][3][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  blend_wave_px2<HWEXP>(fp, b, blockIdx.x * 4 + wave, s_rec[wave]);
+  blend_wave_px2<HWEXP>(fp, b, blockIdx.x * GS_PX2_WPG + wave, s_rec[wave]);
 }
 
 template <bool HWEXP>
@@ -3670,11 +3674,11 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
         gs_blend_px2h_kernel<false><<<(unsigned)fp.n_tiles, 256, 0, s>>>(fp, b);
       return;
     }
-    const unsigned g2 = (unsigned)((2L * fp.n_tiles + 3) / 4);
+    const unsigned g2 = (unsigned)((2L * fp.n_tiles + GS_PX2_WPG - 1) / GS_PX2_WPG);
     if (fp.fast_exp)
-      gs_blend_px2_kernel<true><<<g2, 256, 0, s>>>(fp, b);
+      gs_blend_px2_kernel<true><<<g2, 64 * GS_PX2_WPG, 0, s>>>(fp, b);
     else
-      gs_blend_px2_kernel<false><<<g2, 256, 0, s>>>(fp, b);
+      gs_blend_px2_kernel<false><<<g2, 64 * GS_PX2_WPG, 0, s>>>(fp, b);
     return;
   }
   if (fp.blend_sort && fp.blend_px2) {  // (two tiles per workgroup)
