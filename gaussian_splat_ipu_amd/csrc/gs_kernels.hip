@@ -56,11 +56,6 @@
 #ifndef GS_PX2_WPG
 #define GS_PX2_WPG 4
 #endif
-// (A/B) two-pixel blend: waves of lists longer than this raise their issue
-// priority (0: off)
-#ifndef GS_PX2_PRIO
-#define GS_PX2_PRIO 0
-#endif
 // the one-pixel blend kernels' fewest waves per SIMD (8: at most 64 VGPRs)
 #ifndef GS_BLEND_WPE
 #define GS_BLEND_WPE 8
@@ -3340,11 +3335,6 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
   qb.done = !vb;
 
   const uint32_t* __restrict__ list = b.list + s;
-#if GS_PX2_PRIO > 0
-  // (A/B) a long list's waves issue ahead of the other waves of their SIMD
-  // (the other frames' kernels included), so the heaviest walks end sooner
-  if (L > (uint32_t)GS_PX2_PRIO) __builtin_amdgcn_s_setprio(2);
-#endif
   auto load_idx = [&](uint32_t k) -> uint32_t { return blend_idx(fp, list, L, k); };
   const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
   auto load_rec = [&](uint32_t g, float4& r0, float4& r1, float4& r2) {
