@@ -96,17 +96,50 @@ def parse():
     return ap.parse_args()
 
 
-# the kernels behind each timed stage (rocprof short names)
-STAGE_KERNELS = {
-    "project": ["gs_project"],
-    "scan": ["gs_count", "gs_colscan", "gs_scan_multi", "gs_scan", "gs_agg_scan"],
-    "emit": ["gs_emit_chunk", "gs_emit", "gs_agg_emit"],
-    "sort": ["gs_sort_tiles", "gs_big_prefix", "gs_big_split", "gs_big_select", "gs_big_psort"],
-    "blend": ["gs_blend", "gs_blend_sort", "gs_blend_px2", "gs_blend_px2h", "gs_blend_sort_px2"],
-    # lazy big lists (config 5): the windows of the flagged lists sorted, the
-    # continued blend (PMC: its per-launch average over the frame's two launches)
-    "blend_cont": ["gs_big_cont", "gs_blend_cont"],
-}
+# gs_frame_stats.paths bits (include/gsplat.h)
+PATH_BIN_AGG, PATH_BLEND_SORT, PATH_BLEND_PX2, PATH_LAZY, PATH_BIG_LISTS = 1, 2, 4, 8, 16
+
+
+def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
+    """[(rocprof short name, launches per frame)] of the kernels a timed stage
+    launched, from the frame's gs_frame_stats.paths (gs_kernels.hip launch_*):
+    the roofline's PMC bytes and VALU are those kernels' per-launch counters
+    weighted by their launches per frame -- never another path's kernel, never
+    a per-launch average of several kernels summed."""
+    agg, bsort, px2, lazy, big = (bool(paths & b) for b in (PATH_BIN_AGG, PATH_BLEND_SORT, PATH_BLEND_PX2,
+                                                            PATH_LAZY, PATH_BIG_LISTS))
+    buckets = [("gs_big_count", 1), ("gs_big_bscan", 1), ("gs_big_scatter", 1), ("gs_big_bsort", 1)]
+    if stage == "project":
+        return [("gs_project", 1)]
+    if stage == "scan":
+        if agg:
+            return [("gs_agg_scan", 1)]
+        return [("gs_scan", 1)] if bin_global else [("gs_count", 1), ("gs_colscan", 1), ("gs_scan_multi", 1)]
+    if stage == "emit":
+        return [("gs_agg_emit", 1)] if agg else ([("gs_emit", 1)] if bin_global else [("gs_emit_chunk", 1)])
+    if stage == "sort":
+        ks = [] if bsort else [("gs_sort_tiles", 1)]
+        if big:
+            ks += [("gs_big_prefix", 1), ("gs_big_split", 1)]
+            ks += [("gs_big_select", 1), ("gs_big_psort", 1)] if lazy else buckets
+        return ks
+    if stage == "blend":
+        return [("gs_blend_px2" if px2 else ("gs_blend_sort" if bsort else "gs_blend"), 1)]
+    if stage == "blend_cont":  # lazy big lists: window sort + continued blend, pass 2 (launch_blend_cont)
+        return [("gs_big_cont", 1), ("gs_blend_cont", 2), ("gs_big_prefix", 1)] + buckets
+    raise KeyError(stage)
+
+
+def stage_pmc(stage: str, paths: int, kernels: dict, bin_global: bool = False):
+    """(HBM bytes, wave64 VALU instructions, missing kernel names) per frame of
+    a stage, from a PMC summary's per-launch counters (tools/pmc_summary.py)."""
+    ks = stage_kernels(stage, paths, bin_global)
+    missing = [k for k, _ in ks if k not in kernels]
+    if missing or not ks:
+        return None, None, missing
+    hbm = sum(n * kernels[k]["hbm_bytes_per_launch"] for k, n in ks)
+    valu = sum(n * kernels[k].get("SQ_INSTS_VALU", 0.0) for k, n in ks)
+    return hbm, valu, []
 
 
 def measured_copy_peak(torch, min_s: float = 0.06) -> float:
@@ -510,22 +543,30 @@ def main():
         except Exception:
             pm = None
 
+    paths = int(st_view.get("paths", 0))
+    bin_global = bool(st_view.get("bin_global", 0))
+
     def roof(name):
         k = kern[name]
         pmc = valu = None
-        if pm is not None:
-            ks = pm.get("kernels", {})
-            names = [x for x in STAGE_KERNELS[name] if x in ks]
-            if names:
-                pmc = int(sum(ks[x]["hbm_bytes_per_launch"] for x in names))
+        launched = [x for x, _ in stage_kernels(name, paths, bin_global)]
+        if pm is None:
+            note = f"no PMC summary for {pmc_key} in {os.path.relpath(a.pmc_json, ROOT)}"
+        else:
+            hb, vi, missing = stage_pmc(name, paths, pm.get("kernels", {}), bin_global)
+            if missing:
+                note = f"the PMC summary lacks {', '.join(missing)}, which this stage launched"
+            else:
+                note = None
+                pmc = int(hb)
                 # VALU issue-slot fraction beside the HBM fraction (SURVEY §8 d):
                 # wave64 VALU instructions x 2 cycles over 1024 SIMDs x 2.4 GHz
-                vi = sum(ks[x].get("SQ_INSTS_VALU", 0.0) for x in names)
                 if vi:
                     valu = round(min(1.0, vi * 2.0 / (1024 * 2.4e9 * k["avg_ms"] * 1e-3)), 3)
         ach = k["alg_GBps"]
-        return {
+        out = {
             "kernel": name,
+            "launched": launched,
             "achieved": ach,
             "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
             "traffic": pmc,
@@ -537,6 +578,9 @@ def main():
             "avg_launch_ms": k["avg_ms"],
             "valu_issue_frac": valu,
         }
+        if note:
+            out["traffic_note"] = note
+        return out
 
     rd = roof(dom)
     roofline = {
@@ -548,6 +592,7 @@ def main():
         "frac": rd["frac"],
         "traffic": rd["traffic"],
         "traffic_key": pmc_key,
+        "traffic_kernels": rd["launched"],
         "traffic_over_alg": rd["traffic_over_alg"],
         "alg_bytes_per_launch": rd["alg_bytes_per_launch"],
         "alg_bytes_model": "SURVEY §8(d) terms (bench.survey_bytes); the blend's P = the records it staged, "
@@ -558,10 +603,15 @@ def main():
                               "record = list entry + 32-B record + 16-B colour)",
         "avg_launch_ms": rd["avg_launch_ms"],
         "valu_issue_frac": rd["valu_issue_frac"],
+        "traffic_model": "PMC HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) and VALU of the kernels this stage launched in "
+                         "the timed frames (gs_frame_stats.paths -> bench.stage_kernels), per launch x launches per "
+                         "frame; null with traffic_note when the summary lacks one of them",
         "selection": "longest stage of the one-in-flight kernel table (every stage, the lazy continuation included)",
         "latency_bound": dom == "blend_cont",
         "peak_measured": peak_measured,
     }
+    if rd.get("traffic_note"):
+        roofline["traffic_note"] = rd["traffic_note"]
     if dom == "blend_cont":
         roofline["note"] = ("the longest stage is the lazy continuation, a chain of short launches (latency-bound); "
                             "the blend's own roofline is in roofline.blend")
@@ -664,7 +714,7 @@ def main():
                 "pmc_key": pmc_key,
             },
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "n_pairs_binned", "max_list", "n_tiles",
-                                         "n_big_tiles")},
+                                         "n_big_tiles", "paths", "bin_global")},
             "frame_check": frame_check,
             "kernels": kern,
             "roofline": roofline,

@@ -215,7 +215,17 @@ struct Group {
   std::vector<std::thread> workers;
   FrameCmd cmd;                       // the posted frame
   std::atomic<uint64_t> post_seq{0};  // frames posted
-  std::atomic<uint32_t> done{0};      // workers finished with the posted frame
+  std::atomic<uint32_t> done{0};      // workers finished with the posted frame's band
+  // phase 2 of a threaded frame: once every member's band is enqueued, the
+  // caller posts the verdict (gather_seq = the frame's post_seq); the
+  // workers issue their all-gathers only if every band succeeded, so a
+  // failed member never leaves the others' collectives half-issued
+  std::atomic<uint64_t> gather_seq{0};
+  std::atomic<bool> gather_ok{false};
+  std::atomic<uint32_t> gathered{0};  // workers past phase 2 of the posted frame
+  // a frame failed in one member after others had issued device work for it:
+  // the group refuses further frames (gs_destroy still releases it)
+  bool failed = false;
   std::atomic<int> sleepers{0};
   std::atomic<bool> stop{false};
   std::mutex wmu;
@@ -450,15 +460,6 @@ int member_gathered(Group* g, Member& m, const FrameCmd& f) {
   return GS_OK;
 }
 
-// A worker's (or the caller's) whole part of the frame: its band and, over
-// RCCL, its own all-gather call (no group call: one thread per communicator).
-int member_frame(Group* g, Member& m, const FrameCmd& f) {
-  int rc = member_render(g, m, f);
-  if (rc != GS_OK || !g->rccl) return rc;
-  if ((rc = member_gather_rccl(g, m, f)) != GS_OK) return rc;
-  return member_gathered(g, m, f);
-}
-
 inline void cpu_relax() {
 #if !defined(__HIP_DEVICE_COMPILE__)
   __builtin_ia32_pause();
@@ -492,9 +493,22 @@ void worker_main(Group* g, int k) {
     if (s == seen) return;  // stop
     seen = s;
     const FrameCmd f = g->cmd;
-    m.rc = member_frame(g, m, f);
+    m.rc = member_render(g, m, f);
     if (m.rc != GS_OK) m.err = gsh::last_error();
     g->done.fetch_add(1, std::memory_order_acq_rel);
+    if (!g->rccl) continue;
+    // phase 2: the caller's verdict on every member's band (a short wait: the
+    // caller posts it as soon as the last band is enqueued)
+    while (g->gather_seq.load(std::memory_order_acquire) != s) cpu_relax();
+    if (g->gather_ok.load(std::memory_order_acquire)) {
+      int rc = member_gather_rccl(g, m, f);
+      if (rc == GS_OK) rc = member_gathered(g, m, f);
+      if (rc != GS_OK) {
+        m.rc = rc;
+        m.err = gsh::last_error();
+      }
+    }
+    g->gathered.fetch_add(1, std::memory_order_acq_rel);
   }
 }
 
@@ -510,6 +524,10 @@ void stop_workers(Group* g) {
 }
 
 int enqueue(Group* g) {
+  if (g->failed) {
+    set_error("row-band group: an earlier frame failed on one member; destroy the group");
+    return GS_EDEVICE;
+  }
   const int i = (int)(g->frame % (uint64_t)g->F);
   SlotInfo& si = g->sinfo[i];
   int rc = set_dev(g->mem[0].device);
@@ -532,20 +550,39 @@ int enqueue(Group* g) {
   if (g->threaded) {
     // members 1.. on their worker threads, member 0 here; over RCCL each
     // member's all-gather is its own thread's call
+    // (two phases: every band first, then -- only if all succeeded -- every
+    // member's all-gather, each on its own thread)
     g->cmd = f;
     g->done.store(0, std::memory_order_relaxed);
-    g->post_seq.fetch_add(1);
+    g->gathered.store(0, std::memory_order_relaxed);
+    const uint64_t seq = g->post_seq.fetch_add(1) + 1;
     if (g->sleepers.load() > 0) {
       std::lock_guard<std::mutex> lk(g->wmu);
       g->wcv.notify_all();
     }
     Member& m0 = g->mem[0];
-    m0.rc = member_frame(g, m0, f);
+    m0.rc = member_render(g, m0, f);
     if (m0.rc != GS_OK) m0.err = gsh::last_error();
     const uint32_t want = (uint32_t)g->mem.size() - 1;
     while (g->done.load(std::memory_order_acquire) < want) cpu_relax();
+    bool ok = true;
+    for (const Member& m : g->mem) ok = ok && m.rc == GS_OK;
+    if (g->rccl) {
+      g->gather_ok.store(ok, std::memory_order_release);
+      g->gather_seq.store(seq, std::memory_order_release);
+      if (ok) {
+        m0.rc = member_gather_rccl(g, m0, f);
+        if (m0.rc == GS_OK) m0.rc = member_gathered(g, m0, f);
+        if (m0.rc != GS_OK) m0.err = gsh::last_error();
+      }
+      while (g->gathered.load(std::memory_order_acquire) < want) cpu_relax();
+    }
     for (Member& m : g->mem)
       if (m.rc != GS_OK) {
+        // a band failed (no collective was issued), or a gather call failed
+        // after others were issued: either way the group's streams can no
+        // longer be trusted to drain in step
+        g->failed = true;
         set_error(m.err);
         return m.rc;
       }
@@ -1152,7 +1189,18 @@ int set_sh(Group* g, const float* f_dc, const float* f_rest, size_t n, int degre
       const gs_renderer* share = nullptr;
       for (const gs_renderer* o : first)
         if (o->device == c->device) share = o;
-      if ((rc = gsr::set_sh(c, f_dc, f_rest, n, degree, share)) != GS_OK) return rc;
+      if ((rc = gsr::set_sh(c, f_dc, f_rest, n, degree, share)) != GS_OK) {
+        // a renderer that shares another's copy may now point at a copy its
+        // owner replaced: every sharer drops its pointer (DC colour again)
+        for (Member& mm : g->mem)
+          for (gs_renderer* o : mm.slot)
+            if (o->d_sh && !o->owns_sh) {
+              o->d_sh = nullptr;
+              o->buf.sh = nullptr;
+              o->sh_degree = -1;
+            }
+        return rc;
+      }
       if (!share) first.push_back(c);
     }
   return GS_OK;

@@ -98,6 +98,7 @@ struct gs_renderer {
   uint32_t* h_counters = nullptr;  // mapped pinned mirror of d_zero: counters[16] + tile_count[T]
   std::vector<uint32_t> hist_snapshot;
   std::mutex hist_mu;
+  bool hist_moved = false;  // (under hist_mu) gs_set_band_rows after the snapshot's frame
   bool frame_pending = false;
   // gs_set_band_rows moved the band after the last enqueued frame: that
   // frame's readbacks are refused (its geometry is not the renderer's now)

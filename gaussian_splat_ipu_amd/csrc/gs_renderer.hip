@@ -316,12 +316,14 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // the short lists' tiles, which lazy frames allow (their big lists keep the
   // one-pixel waves whose state the continuation resumes): config 3 8 196,
   // config 5 1 520 -> 1 482, so not the default.
+  // blend_wave_px2 maps a wave onto a 16x8 half of a 16x16 tile: other
+  // shapes with four 8x8 blocks (32x8, 8x32) keep one pixel per lane
+  const bool tile16 = tw == 16 && th == 16;
   const int px2 = r->env_blend_px2 >= 0 ? r->env_blend_px2 : 1;
-  fp.blend_px2 = (px2 > 0 && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !fp.blend_sort &&
-                  (!fp.lazy || px2 == 2)) ? px2 : 0;
+  fp.blend_px2 = (px2 > 0 && tile16 && !fp.blend_sort && (!fp.lazy || px2 == 2)) ? px2 : 0;
   // row bands (the in-blend sort): two-pixel lanes, two tiles per workgroup
   // (GSPLAT_BAND_PX2=1, A/B)
-  if (fp.blend_sort && !fp.lazy && r->env_band_px2 > 0) fp.blend_px2 = 1;
+  if (tile16 && fp.blend_sort && !fp.lazy && r->env_band_px2 > 0) fp.blend_px2 = 1;
   // two-pixel lanes walk a tile's list in half the waves, so a heavy tile's
   // walk is twice as long: its waves start first (the sort queues' order,
   // longest lists first) -- config 3 blend 86.4 -> 79.4 us alone, 8 451 ->
@@ -419,10 +421,18 @@ int set_sh(gs_renderer* r, const float* f_dc, const float* f_rest, size_t n, int
       for (int k = 1; k < K; ++k) h[(size_t)(k * 3 + c) * nn + i] = f_rest[o * 45 + (size_t)c * 15 + (k - 1)];
     }
   }
+  // the new copy first: if it fails, the renderer (and any renderer sharing
+  // its old copy) keeps the old coefficients
+  void* d_new = nullptr;
+  GS_HIP(hipMalloc(&d_new, h.size() * 4));
+  const hipError_t e = hipMemcpy(d_new, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(d_new);
+    return hip_fail(e, "gs_set_sh: hipMemcpy");
+  }
   drop();
-  GS_HIP(hipMalloc(&r->d_sh, h.size() * 4));
+  r->d_sh = d_new;
   r->owns_sh = true;
-  GS_HIP(hipMemcpy(r->d_sh, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   r->buf.sh = (const float*)r->d_sh;
   r->sh_degree = degree;
   return GS_OK;
@@ -494,6 +504,12 @@ int enqueue_frame(gs_renderer* r) {
   r->last_fp = fp;
   r->have_fp = true;
   r->band_moved = false;
+  // this frame's band (gs_set_band_rows may have moved it since the last one)
+  r->stats.n_tiles = (uint32_t)r->n_tiles;
+  r->stats.tiles_y = (uint32_t)r->band_nrows;
+  r->stats.band_stride = (uint32_t)r->band_stride;
+  r->stats.band_y0 = (uint32_t)r->band_py0;
+  r->stats.band_rows = (uint32_t)r->band_rows;
   hipStream_t s = r->stream;
   // BGR8 destination of this frame (gs_set_bgr8_target)
   r->buf.bgr = r->bgr_target ? r->bgr_target : r->own_bgr;
@@ -573,7 +589,10 @@ int finish_frame(gs_renderer* r) {
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
   r->stats.paths = r->have_fp ? ((r->last_fp.bin_agg ? GS_PATH_BIN_AGG : 0u) |
-                                 (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u))
+                                 (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u) |
+                                 (r->last_fp.blend_px2 ? GS_PATH_BLEND_PX2 : 0u) |
+                                 (r->last_fp.lazy ? GS_PATH_LAZY : 0u) |
+                                 (r->last_fp.big_separate ? GS_PATH_BIG_LISTS : 0u))
                               : 0u;
   r->stats.blend_records = r->stats.blend_cont_records = r->stats.cont_keys = 0;
   r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = r->stats.cont_full_sorts = 0;
@@ -582,8 +601,10 @@ int finish_frame(gs_renderer* r) {
     // profiled frame: the list records the blend read.  The waves of a tile
     // each stage a prefix of the same list (the tile's records come from HBM
     // once, the other waves' reads hit L2), so a tile counts its longest prefix.
+    // (the frame's tiles: the band may have moved since it was enqueued)
+    const int nt_f = r->last_fp.n_tiles;
     const size_t cpt = (size_t)r->last_fp.chunks_per_tile;
-    const size_t nw = std::min(r->bcount_words / 2, (size_t)r->n_tiles * cpt);
+    const size_t nw = std::min(r->bcount_words / 2, (size_t)nt_f * cpt);
     std::vector<uint32_t> bc(2 * nw);
     GS_HIP(hipMemcpy(bc.data(), r->buf.blend_count, nw * 4, hipMemcpyDeviceToHost));
     GS_HIP(hipMemcpy(bc.data() + nw, r->buf.blend_count + r->bcount_words / 2, nw * 4, hipMemcpyDeviceToHost));
@@ -597,13 +618,13 @@ int finish_frame(gs_renderer* r) {
       // (the continuation ran the waves of the c[0] big lists only)
       if (r->last_fp.lazy && t < (size_t)c[0] * cpt) r->stats.blend_cont_records += m1;
     }
-    if (c[0] > 0 && r->n_tiles > 0) {
+    if (c[0] > 0 && nt_f > 0) {
       // the big lists' binned pairs (bench.py's sort bytes)
-      std::vector<uint32_t> ts((size_t)r->n_tiles + 1), bt(c[0]);
+      std::vector<uint32_t> ts((size_t)nt_f + 1), bt(c[0]);
       GS_HIP(hipMemcpy(ts.data(), r->buf.tile_start, ts.size() * 4, hipMemcpyDeviceToHost));
       GS_HIP(hipMemcpy(bt.data(), r->buf.big_tiles, (size_t)c[0] * 4, hipMemcpyDeviceToHost));
       for (uint32_t j = 0; j < c[0]; ++j)
-        if (bt[j] < (uint32_t)r->n_tiles) r->stats.big_pairs += ts[bt[j] + 1] - ts[bt[j]];
+        if (bt[j] < (uint32_t)nt_f) r->stats.big_pairs += ts[bt[j] + 1] - ts[bt[j]];
     }
     if (r->last_fp.lazy && c[0] > 0) {
       // the continuation's lists and their filtered key counts
@@ -640,6 +661,7 @@ int finish_frame(gs_renderer* r) {
   {
     std::lock_guard<std::mutex> lk(r->hist_mu);
     r->hist_snapshot.assign(r->h_counters + 16, r->h_counters + 16 + nt);
+    r->hist_moved = r->band_moved;  // (a frame enqueued before a move: still refused, as the frame readbacks)
   }
   r->have_frame = true;
   return GS_OK;
@@ -1079,11 +1101,7 @@ int set_band_rows(gs_renderer* r, int ty0, int ty1, int pad_rows) {
   r->band_rows_padded = pad_rows * th_px;
   r->n_tiles = r->tiles_x * r->band_nrows;
   r->bgr_bytes = (size_t)r->cfg.width * r->band_rows_padded * 3;
-  r->stats.n_tiles = (uint32_t)r->n_tiles;
-  r->stats.tiles_y = (uint32_t)r->band_nrows;
-  r->stats.band_stride = 1;
-  r->stats.band_y0 = (uint32_t)r->band_py0;
-  r->stats.band_rows = (uint32_t)r->band_rows;
+  // (the stats keep the last frame's band until the next frame is enqueued)
   return GS_OK;
 }
 
@@ -1399,7 +1417,11 @@ int gs_set_band_rows(gs_renderer* r, uint32_t row_begin, uint32_t row_end, uint3
   // would read it with the new band's geometry) until the next frame.
   const int pad = std::max<int>((int)(row_end - row_begin), (int)pad_rows);
   const int rc = gsr::set_band_rows(r, (int)row_begin, (int)row_end, pad);
-  if (rc == GS_OK && r->have_fp) r->band_moved = true;
+  if (rc == GS_OK && r->have_fp) {
+    r->band_moved = true;
+    std::lock_guard<std::mutex> lk(r->hist_mu);
+    r->hist_moved = true;  // (the snapshot is the old band's until the next frame completes)
+  }
   return rc;
 }
 
@@ -1483,6 +1505,10 @@ int gs_read_tile_histogram(gs_renderer* r, uint32_t* dst, size_t n) {
   if (!r || !dst) return GS_EINVAL;
   if (r->grp) return gsg::read_tile_histogram(r->grp, dst, n);
   std::lock_guard<std::mutex> lk(r->hist_mu);
+  if (r->hist_moved) {
+    set_error("gs_read_tile_histogram: the band moved (gs_set_band_rows) after the last frame; render a frame first");
+    return GS_EINVAL;
+  }
   if (n < r->hist_snapshot.size()) {
     set_error("gs_read_tile_histogram: destination too small");
     return GS_EINVAL;

@@ -217,8 +217,11 @@ class GpuSplatter:
         (gs_set_band_rows; the renderer must have been created with room for
         them, e.g. band_rows=(0, tiles_y))."""
         check(lib().gs_set_band_rows(self._h, int(row_begin), int(row_end), int(pad_rows)), "gs_set_band_rows")
-        st = self.stats()
-        self.n_tiles, self.band_y0, self.band_rows = st["n_tiles"], st["band_y0"], st["band_rows"]
+        # (the stats keep the last frame's band until the next frame)
+        th = self.fb.tile_height
+        self.n_tiles = (int(row_end) - int(row_begin)) * self.fb.tiles_across
+        self.band_y0 = int(row_begin) * th
+        self.band_rows = min(self.fb.height, int(row_end) * th) - self.band_y0
 
     def set_stream(self, stream_ptr: int | None) -> None:
         check(lib().gs_set_stream(self._h, C.c_void_p(stream_ptr or 0)))

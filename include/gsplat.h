@@ -199,8 +199,16 @@ typedef struct gs_frame_stats {
                              continuation's windows                        */
 } gs_frame_stats;
 
-/* gs_frame_stats.paths bits (ABI 11) */
-enum { GS_PATH_BIN_AGG = 1, GS_PATH_BLEND_SORT = 2 };
+/* gs_frame_stats.paths bits (ABI 11; bits 2-4 ABI 12): which kernels the
+   last frame launched, so a profile's per-kernel counters can be matched to
+   the frame path (bench.py's roofline) */
+enum {
+  GS_PATH_BIN_AGG = 1,     /* aggregated binning (gs_agg_scan / gs_agg_emit)     */
+  GS_PATH_BLEND_SORT = 2,  /* tile sort inside the blend (gs_blend_sort)         */
+  GS_PATH_BLEND_PX2 = 4,   /* two pixels per blend lane (gs_blend_px2)           */
+  GS_PATH_LAZY = 8,        /* lazy big lists (prefix select / sort, continuation) */
+  GS_PATH_BIG_LISTS = 16   /* the big-list launches ran (lists > 2048 keys)       */
+};
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */
 enum {

@@ -13,7 +13,20 @@ import pytest
 import bench
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF = os.path.join(ROOT, "profiles", "r03_end")
+
+
+def _newest_profiles() -> str:
+    """The newest round's profile directory holding the round-end PMC summaries
+    (profiles/r0N_*/pmc_c3.json)."""
+    ds = sorted(os.path.dirname(p) for p in glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_c3.json")))
+    return ds[-1] if ds else os.path.join(ROOT, "profiles", "r04_final")
+
+
+PROF = _newest_profiles()
+# the paths the default frames take (gs_frame_stats.paths): config 3 whole
+# frames blend two pixels per lane; config 5 (big lists) the lazy one-pixel blend
+C3_PATHS = bench.PATH_BLEND_PX2
+C5_PATHS = bench.PATH_LAZY | bench.PATH_BIG_LISTS
 
 
 def _stats(**kw):
@@ -101,22 +114,60 @@ def test_launch_modes():
         bench.launch_mode(2, 1, split=4)
 
 
-@pytest.mark.parametrize("line,pmc", [("bench_c3_pmc.json", "pmc_c3.json"), ("bench_c5.json", "pmc_c5.json")])
-def test_committed_lines_within_pmc(line, pmc):
+@pytest.mark.parametrize("line,pmc,paths", [("bench_c3_pmc.json", "pmc_c3.json", C3_PATHS),
+                                             ("bench_c5.json", "pmc_c5.json", C5_PATHS)])
+def test_committed_lines_within_pmc(line, pmc, paths):
     lp, pp = os.path.join(PROF, line), os.path.join(PROF, pmc)
     if not (os.path.exists(lp) and os.path.exists(pp)):
         pytest.skip("round-end profiles not present")
     d = json.loads(open(lp).read().strip().splitlines()[-1])
     kernels = json.load(open(pp))["kernels"]
+    paths = d["frame"].get("paths", paths)
     for stage, k in d["kernels"].items():
         lb = k.get("layout_bytes", k.get("alg_bytes"))  # (round-3 lines: alg_bytes was the layout model)
         if lb is None:
             continue
-        names = [x for x in bench.STAGE_KERNELS.get(stage, []) if x in kernels]
-        if not names:
-            continue
-        hbm = sum(kernels[x]["hbm_bytes_per_launch"] for x in names)
+        hbm, _, missing = bench.stage_pmc(stage, paths, kernels)
+        assert not missing, (stage, missing)
         assert lb <= 1.1 * hbm, (stage, lb, hbm)
+
+
+def test_stage_kernels_follow_the_frame_paths():
+    """The roofline's PMC figures come from the kernels the timed frames
+    launched (a line read another path's kernel)."""
+    sk = bench.stage_kernels
+    assert sk("blend", C3_PATHS) == [("gs_blend_px2", 1)]
+    assert sk("blend", C5_PATHS) == [("gs_blend", 1)]
+    assert sk("blend", bench.PATH_BLEND_SORT | bench.PATH_BIN_AGG) == [("gs_blend_sort", 1)]
+    assert sk("scan", bench.PATH_BIN_AGG) == [("gs_agg_scan", 1)]
+    assert sk("scan", 0) == [("gs_count", 1), ("gs_colscan", 1), ("gs_scan_multi", 1)]
+    assert [k for k, _ in sk("sort", C5_PATHS)] == ["gs_sort_tiles", "gs_big_prefix", "gs_big_split",
+                                                   "gs_big_select", "gs_big_psort"]
+    assert ("gs_blend_cont", 2) in sk("blend_cont", C5_PATHS)
+    # launches per frame weight the per-launch counters; a missing kernel is reported
+    ks = {"gs_big_cont": {"hbm_bytes_per_launch": 10.0, "SQ_INSTS_VALU": 1.0},
+          "gs_blend_cont": {"hbm_bytes_per_launch": 3.0, "SQ_INSTS_VALU": 2.0}}
+    hb, vi, missing = bench.stage_pmc("blend_cont", C5_PATHS, ks)
+    assert hb is None and "gs_big_bsort" in missing
+    for k in ("gs_big_prefix", "gs_big_count", "gs_big_bscan", "gs_big_scatter", "gs_big_bsort"):
+        ks[k] = {"hbm_bytes_per_launch": 1.0, "SQ_INSTS_VALU": 0.0}
+    hb, vi, missing = bench.stage_pmc("blend_cont", C5_PATHS, ks)
+    assert (hb, vi, missing) == (10.0 + 2 * 3.0 + 5.0, 1.0 + 2 * 2.0, [])
+
+
+@pytest.mark.parametrize("pmc,paths", [("pmc_c3.json", C3_PATHS), ("pmc_c5.json", C5_PATHS)])
+def test_round_pmc_holds_the_default_kernels(pmc, paths):
+    """The newest round-end PMC summaries (and profiles/pmc_latest.json, the
+    bench's default for config 3) hold every kernel the default frames launch."""
+    pp = os.path.join(PROF, pmc)
+    if not os.path.exists(pp):
+        pytest.skip("round-end profiles not present")
+    files = [pp] + ([os.path.join(ROOT, "profiles", "pmc_latest.json")] if pmc == "pmc_c3.json" else [])
+    for f in files:
+        kernels = json.load(open(f))["kernels"]
+        for stage in ("project", "scan", "emit", "sort", "blend") + (("blend_cont",) if paths & bench.PATH_LAZY else ()):
+            _, _, missing = bench.stage_pmc(stage, paths, kernels)
+            assert not missing, (f, stage, missing)
 
 
 def _lines_with_survey_model():

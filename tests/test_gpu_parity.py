@@ -623,9 +623,15 @@ def test_set_band_rows_keeps_the_in_flight_frame(pc12):
         assert "overflow" in str(e.value).lower()
         with pytest.raises(GsError):
             s.get_frame_buffer()  # the frame before the move
+        with pytest.raises(GsError):
+            s.get_histogram()  # ... and its histogram
+        assert s.stats()["band_y0"] == 0 and s.stats()["n_tiles"] == fb.tiles_down * fb.tiles_across
         s.execute()  # regrows, renders the moved band
         np.testing.assert_array_equal(s.get_frame_buffer(), bgr[10 * TH:30 * TH])
         assert s.stats()["pair_capacity"] > 1024
+        assert s.stats()["band_y0"] == 10 * TH and s.stats()["n_tiles"] == 20 * fb.tiles_across
+        np.testing.assert_array_equal(s.get_histogram(),
+                                      full.get_histogram().reshape(fb.tiles_down, -1)[10:30].reshape(-1))
 
 
 @pytest.mark.parametrize("agg", ["0", "1"])
@@ -771,5 +777,23 @@ def test_band_px2_bit_exact(pc12, monkeypatch):
     for band_index in (0, 3, 7):
         s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=8, band_index=band_index)
         assert s.stats()["paths"] & 2
+        _assert_parity(s, f, g, check_proj=False)
+        s.close()
+
+
+@pytest.mark.parametrize("tw,th", [(32, 8), (8, 32)])
+def test_four_block_tiles_other_than_16x16(pc12, tw, th):
+    """Tiles of four 8x8 blend blocks that are not 16x16 (32x8, 8x32) keep
+    one pixel per lane: the two-pixel blend maps a wave onto a 16x8 half of a
+    16x16 tile.  Whole frames with partial edge tiles, and a row
+    band (the in-blend sort, one workgroup per tile), bit for bit."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = pc12
+    W, H = 1000, 700
+    view, proj = camera.headless(bb, W, H)
+    for band_count, band_index in [(1, 0), (8, 3)]:
+        s, f = _frame_pair(g, view, proj, W, H, tw, th, 1.0, band_count=band_count, band_index=band_index)
+        assert not s.stats()["paths"] & 4  # (GS_PATH_BLEND_PX2)
         _assert_parity(s, f, g, check_proj=False)
         s.close()

@@ -10,7 +10,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-from bench import STAGE_KERNELS  # noqa: E402
+from bench import stage_pmc, stage_kernels  # noqa: E402
 
 
 def main():
@@ -22,8 +22,12 @@ def main():
         if "alg_bytes" not in k:
             continue
         lb = k.get("layout_bytes", k["alg_bytes"])
-        names = [n for n in STAGE_KERNELS.get(stage, []) if n in pmc]
-        hbm = sum(pmc[n]["hbm_bytes_per_launch"] for n in names)
+        paths, bg = line["frame"].get("paths", 0), bool(line["frame"].get("bin_global", 0))
+        hbm, _, missing = stage_pmc(stage, paths, pmc, bg)
+        names = [f"{n} x{c}" for n, c in stage_kernels(stage, paths, bg)]
+        if missing:
+            print(f"{stage:12s} PMC summary lacks {', '.join(missing)}")
+            continue
         r8 = hbm / k["alg_bytes"] if k["alg_bytes"] else float("nan")
         rl = lb / hbm if hbm else float("nan")
         print(f"{stage:12s} {1e3 * k['avg_ms']:8.1f} {k['alg_bytes'] / 1e6:9.1f} {lb / 1e6:10.1f} {hbm / 1e6:9.1f} "
