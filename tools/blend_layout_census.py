@@ -1,0 +1,152 @@
+"""Blend layout census (CPU, oracle data): how much walking, staging and
+masked-off work each lane layout of the 16x16-tile blend costs on the bench
+scene, to choose the layout before building it.
+
+Layouts (a wave walks its tile's depth-sorted list in batches of 64; a lane
+walks, in list order, the batch's records whose integer alpha box meets any
+of its pixels, until all of its pixels have saturated; the wave stages the
+next batch until every lane is done):
+  px1  4 waves per tile, an 8x8 block each, one pixel per lane
+  px2  2 waves per tile, a 16x8 half each, a horizontal pixel pair per lane
+  px4  1 wave per tile, a 2x2 pixel quad per lane
+  px4h 1 wave per tile, a 4x1 pixel run per lane
+Per layout, summed over the sampled tiles and scaled to the frame:
+  iters    wave record-steps (per batch: the most records any lane walked)
+  staged   records staged (each wave its own copy)
+  evals    pixel-record evaluations the lanes run (every pixel of a walking
+           lane, live or not) and the useful ones (the pixel's box holds the
+           record and the pixel is still live)
+  tail     the heaviest tile's longest wave, in record-steps
+  python tools/blend_layout_census.py [--tiles 400]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+from gaussian_splat_ipu_amd import camera, scene  # noqa: E402
+from oracle import oracle  # noqa: E402
+from blend_census import boxes  # noqa: E402
+
+TW = 16
+# lane -> list of tile-local pixel indices (y * 16 + x), per wave
+LAYOUTS = {}
+
+
+def _layout_px1():
+    waves = []
+    for by in (0, 8):
+        for bx in (0, 8):
+            waves.append([[(by + l // 8) * TW + bx + l % 8] for l in range(64)])
+    return waves
+
+
+def _layout_px2():
+    return [[[(8 * h + l // 8) * TW + 2 * (l % 8), (8 * h + l // 8) * TW + 2 * (l % 8) + 1] for l in range(64)]
+            for h in (0, 1)]
+
+
+def _layout_px4():
+    out = []
+    for l in range(64):
+        x, y = 2 * (l % 8), 2 * (l // 8)
+        out.append([y * TW + x, y * TW + x + 1, (y + 1) * TW + x, (y + 1) * TW + x + 1])
+    return [out]
+
+
+def _layout_px4h():
+    return [[[(l // 4) * TW + 4 * (l % 4) + k for k in range(4)] for l in range(64)]]
+
+
+LAYOUTS = {"px1": _layout_px1(), "px2": _layout_px2(), "px4": _layout_px4(), "px4h": _layout_px4h()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--tiles", type=int, default=400)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    W, H = 1920, 1080
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=a.n, seed=1, sh_degree=0)))
+    view, proj = camera.headless(bb, W, H)
+    fr = oracle.make_frame(view, proj, W, H, TW, TW, camera.FOV_DEFAULT, 1.0)
+    p = oracle.project(g, fr, 8)
+    ts, lst = oracle.bin_lists(p, fr, 8)
+    T = ts.size - 1
+    tx_n = -(-W // TW)
+    op = oracle._g(g)[:, 7]
+    pcut_all, bx0, bx1, by0, by1 = boxes(p["mean2d"], p["conic"], op)
+    rng = np.random.default_rng(a.seed)
+    lens = np.diff(ts)
+    pick = np.unique(np.concatenate([rng.choice(T, a.tiles // 2, replace=False),
+                                     rng.choice(T, a.tiles // 2, p=lens / lens.sum()),
+                                     [int(np.argmax(lens))]]))
+    acc = {k: dict(iters=0, staged=0, evals=0, useful=0, batches=0, tail=0) for k in LAYOUTS}
+    for t in pick:
+        ids = lst[ts[t]:ts[t + 1]]
+        tx, ty = t % tx_n, t // tx_n
+        X0, Y0 = tx * TW, ty * TW
+        keep = ~((bx0[ids] > X0 + TW - 1) | (bx1[ids] < X0) | (by0[ids] > Y0 + TW - 1) | (by1[ids] < Y0))
+        ids = ids[keep]
+        L = ids.size
+        if L == 0:
+            continue
+        ys, xs = np.mgrid[Y0:Y0 + TW, X0:X0 + TW]
+        px = xs.reshape(-1).astype(np.float64)
+        py = ys.reshape(-1).astype(np.float64)
+        valid = (px < W) & (py < H)
+        inb = ((bx0[ids][:, None] <= px[None]) & (bx1[ids][:, None] >= px[None]) &
+               (by0[ids][:, None] <= py[None]) & (by1[ids][:, None] >= py[None]) & valid[None])  # [L, 256]
+        m = p["mean2d"][ids].astype(np.float64)
+        c = p["conic"][ids].astype(np.float64)
+        o = op[ids].astype(np.float64)
+        dx = m[:, 0:1] - px[None]
+        dy = m[:, 1:2] - py[None]
+        power = -0.5 * (c[:, 0:1] * dx * dx + c[:, 2:3] * dy * dy) - c[:, 1:2] * dx * dy
+        alpha = np.minimum(0.99, o[:, None] * np.exp(power))
+        hit = inb & (power <= 0) & (alpha >= 1 / 255.0) & (o[:, None] != 0)
+        # the record at which each pixel breaks (T' < 1e-4), L if never
+        om = np.where(hit, 1.0 - alpha, 1.0)
+        Tc = np.cumprod(om, axis=0)
+        brk = hit & (Tc < 1e-4)
+        done_at = np.where(brk.any(axis=0), np.argmax(brk, axis=0), L)  # last record walked
+        done_at = np.where(valid, done_at, -1)
+        rec = np.arange(L)[:, None]
+        live = inb & (rec <= done_at[None])  # useful evaluations: box holds it, pixel live
+        for name, waves in LAYOUTS.items():
+            A = acc[name]
+            for lanes in waves:
+                P = np.array(lanes)  # [64, k]
+                k = P.shape[1]
+                lane_end = done_at[P].max(axis=1)  # the lane walks until its last pixel breaks
+                union = inb[:, P].any(axis=2)  # [L, 64]
+                walk = union & (rec <= lane_end[None])
+                wave_iters = 0
+                for base in range(0, L, 64):
+                    if base > lane_end.max():
+                        break
+                    A["batches"] += 1
+                    A["staged"] += min(64, L - base)
+                    w = walk[base:base + 64]
+                    it = int(w.sum(axis=0).max())
+                    wave_iters += it
+                    A["evals"] += int(w.sum()) * k
+                A["iters"] += wave_iters
+                A["tail"] = max(A["tail"], wave_iters)
+                A["useful"] += int(live[:, P.reshape(-1)].sum())
+    scale = T / pick.size
+    print(f"tiles sampled {pick.size} of {T}, longest list {lens.max()} (sampled)")
+    print(f"{'layout':6s} {'waves':>6s} {'iters':>10s} {'staged':>10s} {'batches':>9s} {'evals':>11s} "
+          f"{'useful':>11s} {'use/eval':>8s} {'tail iters':>10s}")
+    for name, A in acc.items():
+        nw = len(LAYOUTS[name]) * T
+        print(f"{name:6s} {nw:6d} {A['iters'] * scale:10.0f} {A['staged'] * scale:10.0f} {A['batches'] * scale:9.0f} "
+              f"{A['evals'] * scale:11.0f} {A['useful'] * scale:11.0f} {A['useful'] / max(A['evals'], 1):8.3f} "
+              f"{A['tail']:10d}")
+
+
+if __name__ == "__main__":
+    main()
