@@ -268,6 +268,7 @@ _SIGS = {
     "gs_cam_translate": (C.c_int, [_FP, _FP, _FP]),
     "gs_cam_mvp_start": (C.c_int, [_FP]),
     "gs_cam_headless": (C.c_int, [_FP, C.c_uint32, C.c_uint32, C.c_float, _FP, _FP]),
+    "gs_test_set": (C.c_int, [C.c_char_p, C.c_int64]),
 }
 
 _lib = None

@@ -7,7 +7,8 @@
 //
 // Two ways to form a group:
 //   * gs_create with cfg->num_gpus = G: one process drives G devices
-//     (ncclCommInitAll; one ncclAllGather per device inside ncclGroupStart/End);
+//     (ncclCommInitAll; one host thread per device enqueues its band and then,
+//     once every band is enqueued, its own ncclAllGather);
 //   * gs_create_rank: one process per GPU (ncclCommInitRank from an id rank 0
 //     made), as torchrun launches bench.py.
 //
@@ -436,9 +437,8 @@ int member_render(Group* g, Member& m, const FrameCmd& f) {
 }
 
 // Member m's side of the frame's all-gather over RCCL, on its communication
-// stream after its band: grouped = inside the caller's ncclGroupStart/End
-// (one thread drives every member), else this thread's own call on m's
-// communicator (one thread per member).
+// stream after its band: this thread's own call on m's communicator (one
+// thread per member).
 int member_gather_rccl(Group* g, Member& m, const FrameCmd& f) {
   int rc = set_dev(m.device);
   if (rc != GS_OK) return rc;
@@ -586,20 +586,14 @@ int enqueue(Group* g) {
         set_error(m.err);
         return m.rc;
       }
-  } else {
-    for (Member& m : g->mem)
-      if ((rc = member_render(g, m, f)) != GS_OK) return rc;
+  } else {  // one member (world 1, or one rank of a multi-process group)
+    Member& m = g->mem[0];
+    if ((rc = member_render(g, m, f)) != GS_OK) return rc;
     if (g->rccl) {
-      const bool grouped = g->mem.size() > 1;
-      if (grouped) GS_NCCL(rccl().GroupStart());
-      for (Member& m : g->mem) {
-        rc = member_gather_rccl(g, m, f);
-        if (rc != GS_OK) {
-          if (grouped) (void)rccl().GroupEnd();
-          return rc;
-        }
+      if ((rc = member_gather_rccl(g, m, f)) != GS_OK) {
+        g->failed = true;
+        return rc;
       }
-      if (grouped) GS_NCCL(rccl().GroupEnd());
     }
   }
   if (!g->rccl) {  // copies read every member's band (emulated bands on one device)
@@ -858,12 +852,9 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
     int cnt = -1;
     if (rccl().CommCount && rccl().CommCount(g->mem[0].comm, &cnt) == ncclSuccess) g->comm_ranks = cnt;
   }
-  // one enqueue thread per member past the first (GSPLAT_GROUP_THREADS=0: the
-  // caller's thread enqueues every member, A/B)
+  // one enqueue thread per member past the first
   {
-    static const bool threads_env =
-        !(std::getenv("GSPLAT_GROUP_THREADS") && std::strcmp(std::getenv("GSPLAT_GROUP_THREADS"), "0") == 0);
-    g->threaded = threads_env && g->mem.size() > 1;
+    g->threaded = g->mem.size() > 1;
     if (g->threaded)
       for (size_t k = 1; k < g->mem.size(); ++k) g->workers.emplace_back(worker_main, g, (int)k);
   }

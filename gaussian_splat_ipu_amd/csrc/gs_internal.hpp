@@ -88,7 +88,6 @@ struct gs_renderer {
   size_t chunk_entries = 0;     // chunk table size (chunks x tiles)
   bool chunk_adaptive = false;  // bands: more, smaller chunks (make_params)
   bool bin_agg = false;         // aggregated binning (gs_kernels.hip: agg_count, gs_agg_scan/emit)
-  int bin_agg_mode = -1;        // GSPLAT_BIN_AGG: -1 auto (by the frame's tiles), 0 off, 1 always
   bool pair_cull = false;       // chunked binning into the alpha-box tiles only
   size_t zero_bytes = 0;
   size_t bgr_bytes = 0;
@@ -103,10 +102,6 @@ struct gs_renderer {
   // gs_set_band_rows moved the band after the last enqueued frame: that
   // frame's readbacks are refused (its geometry is not the renderer's now)
   bool band_moved = false;
-  // A/B hooks, read once at gs_create (GSPLAT_BLEND_LPT 0 | 1, GSPLAT_MEAN_W1,
-  // GSPLAT_RECT8: 0 turns the layout off; GSPLAT_BLEND_PERSIST = G resident
-  // blend workgroups); -1 = unset
-  int env_blend_lpt = -1, env_mean_w1 = -1, env_rect8 = -1, env_blend_sort = -1, env_emit_grid = -1, env_project_grid = -1, env_rec48 = 0, env_pass2_grid = 0, env_blend_px2 = -1, env_band_px2 = 0, env_blend_seg = -1;
   uint8_t* own_bgr = nullptr;     // the renderer's BGR8 band buffer
   uint8_t* bgr_target = nullptr;  // gs_set_bgr8_target: frames write their BGR8 here instead
   uint8_t* last_bgr = nullptr;    // where the last enqueued frame wrote its BGR8

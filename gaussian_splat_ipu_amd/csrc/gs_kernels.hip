@@ -72,11 +72,9 @@ __device__ __forceinline__ uint32_t depth_key_of(float z) {
 
 constexpr uint2 kEmptyRect = {1u, 1u};  // tx0 = 1 > tx1 = 0
 
-// the alpha box of record g (the z, w of its last float4: the second of the
-// 32-B record, the third of the 48-B one)
+// the alpha box of record g (the z, w of the second float4 of its 32-B record)
 __device__ __forceinline__ uint2 rec_box(const FrameParams& fp, const Buffers& b, uint32_t g) {
-  const unsigned long long q = fp.rec48 ? 3ull * g + 2ull : 2ull * g + 1ull;
-  return reinterpret_cast<const uint2*>(b.rec)[q * 2ull + 1ull];
+  return reinterpret_cast<const uint2*>(b.rec)[(2ull * g + 1ull) * 2ull + 1ull];
 }
 
 // FrameParams::rect8: a rectangle's four tile bounds, 8 bits each
@@ -326,11 +324,11 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   // without the band cull every live Gaussian needs its colour and rotation:
   // load them with the mean (one memory round trip instead of two)
   if (!fp.band_cull) {
-    if (!fp.mean_w1 || fp.rec48) col = b.colour[i];  // (its w is the opacity, as mean_op's)
+    if (!fp.mean_w1) col = b.colour[i];  // (its w is the opacity, as mean_op's)
     rot = b.rot[i];
   }
-  // the record: 32 B per Gaussian (48 B with the colour: rec48, and the readback)
-  float4* rec = b.rec + ((fp.full_record || fp.rec48) ? 3 : 2) * (size_t)i;
+  // the record: 32 B per Gaussian (48 B with the colour for the readback)
+  float4* rec = b.rec + (fp.full_record ? 3 : 2) * (size_t)i;
   uint2 rect = kEmptyRect, crect = kEmptyRect;
   uint32_t dkey = 0xFFFFFFFFu;
   if (!(sg.w <= 0.0f)) {  // codelets.cpp:456: if (g.gid <= 0) continue;
@@ -384,7 +382,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       return false;
     }
     if (fp.band_cull) {
-      if (!fp.mean_w1 || fp.rec48) col = b.colour[i];  // (its w is the opacity, as mean_op's)
+      if (!fp.mean_w1) col = b.colour[i];  // (its w is the opacity, as mean_op's)
       rot = b.rot[i];
     }
     if (fp.sh_degree >= 0 && b.sh) sh_colour(fp, b, i, mean, col);
@@ -473,13 +471,8 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       rec[2] = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
     } else if ((binned.x & 0xFFFFu) <= (binned.x >> 16)) {
       rec[0] = rec0;
-      if (fp.rec48) {  // the staged layout: colour and opacity beside the conic
-        rec[1] = make_float4(k1, pcut, col.x, col.y);
-        rec[2] = make_float4(col.z, col.w, __uint_as_float(b01), __uint_as_float(b23));
-      } else {
-        rec[1] = make_float4(k1, pcut, __uint_as_float(b01), __uint_as_float(b23));
-        if (fp.sh_degree >= 0 && b.sh) b.col_out[i] = col;
-      }
+      rec[1] = make_float4(k1, pcut, __uint_as_float(b01), __uint_as_float(b23));
+      if (fp.sh_degree >= 0 && b.sh) b.col_out[i] = col;
     }
   } else if (fp.full_record) {  // empty slot: never binned; a neutral record for the readback
     rec[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -711,40 +704,27 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
   if (threadIdx.x == 0) b.block_rendered[blk] = (uint32_t)v;
 }
 
-// one workgroup per block, or (FrameParams::project_grid) a grid of that
-// many workgroups walking the blocks
-// MODE: the paths compiled into the instantiation (a smaller kernel beside
+// one workgroup per block (a grid of workgroups walking the blocks held
+// 73-113 VGPRs inside the loop instead of 51-57: config 3 7 824 against
+// 8 275 frames/s).  MODE: the paths compiled into the instantiation (a smaller kernel beside
 // the other frames' kernels in the CU pair's instruction cache: config 3's
 // projection 35.5 -> 32.4 us, 7 782 -> 8 048 frames/s with the lean one).
 // kProjLean: a whole frame's plain projection (no band cull, no aggregated
 // counting, no readback record, no SH, no global-atomic binning);
 // kProjBand: a row band's (band cull and aggregated counting, nothing else);
-// kProjAgg: a whole frame's with the aggregated counting (GSPLAT_BIN_AGG=1);
 // kProjAny: every path, chosen at run time.
-enum { kProjAny = 0, kProjLean = 1, kProjBand = 2, kProjAgg = 3 };
-// WALK: the workgroups walk the blocks (FrameParams::project_grid); the
-// one-block-per-workgroup form is its own instantiation (inside the walking
-// loop the projection holds 73-113 VGPRs instead of 57, 4-6 waves per SIMD
-// instead of 8)
-template <bool P2, int MODE, bool WALK>
+enum { kProjAny = 0, kProjLean = 1, kProjBand = 2 };
+template <bool P2, int MODE>
 __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrProject);
   if constexpr (MODE != kProjAny) {
     fp.band_cull = MODE == kProjBand ? 1 : 0;
-    fp.bin_agg = (MODE == kProjBand || MODE == kProjAgg) ? 1 : 0;
+    fp.bin_agg = MODE == kProjBand ? 1 : 0;
     fp.full_record = 0;
     fp.sh_degree = -1;
     fp.bin_global = 0;
   }
-  if constexpr (!WALK) {
-    project_block<P2>(fp, b, blockIdx.x);
-  } else {
-    const int nb = (fp.n + 255) / 256;
-    for (int blk = blockIdx.x; blk < nb; blk += gridDim.x) {
-      project_block<P2>(fp, b, blk);
-      __syncthreads();  // the next block rewrites the LDS
-    }
-  }
+  project_block<P2>(fp, b, blockIdx.x);
 }
 
 // --------------------------------------------------------------------- scan
@@ -2979,8 +2959,7 @@ __device__ __forceinline__ int blend_tile_of(const FrameParams& fp, const Buffer
 // wid = the wave's (tile slot, 8x8 block) item; st: the wave's LDS staging
 // of one batch (3 x 64 float4)
 template <int BQW, bool HWEXP>
-__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64],
-                                           int tile_in = -1) {
+__device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
   if (slot >= fp.n_tiles) return;
@@ -3002,7 +2981,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   // where the tile order puts them (8 bands: blend 35.7 -> 29.3 us).  The
   // full frame keeps the tile order (neighbouring tiles share records in L2:
   // 75.1 against 76.1 us in queue order).
-  const int tile = tile_in >= 0 ? tile_in : (fp.blend_cont ? (int)b.big_tiles[jb] : blend_tile_of(fp, b, slot));
+  const int tile = fp.blend_cont ? (int)b.big_tiles[jb] : blend_tile_of(fp, b, slot);
   const int lane = threadIdx.x & 63;
   const int myq = lane >> 2;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
@@ -3078,13 +3057,6 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   // view-dependent one), assembled as the staged 48-B layout
   const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
   auto load_rec = [&](uint32_t g, float4& r0, float4& r1, float4& r2) {
-    if (fp.rec48) {  // one 48-B record (rec48)
-      const float4* q3 = b.rec + 3 * (size_t)g;
-      r0 = q3[0];
-      r1 = q3[1];
-      r2 = q3[2];
-      return;
-    }
     const float4* qq = b.rec + 2 * (size_t)g;
     r0 = qq[0];
     const float4 t = qq[1];    // k1 pcut boxx boxy
@@ -3299,15 +3271,12 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
 
 // wid = (tile slot) * 2 + half; st: the wave's LDS staging of one batch
 template <bool HWEXP>
-// (tile_in >= 0: the tile, and count_slot its group of four words in
-// blend_count, given by the caller)
-__device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64],
-                                               int tile_in = -1, int count_slot = -1) {
+__device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
   const int slot = wid >> 1, half = wid & 1;
   if (slot >= fp.n_tiles) return;
   int tile;
   uint32_t s, L;
-  if (fp.blend_seg && !fp.blend_sort && tile_in < 0) {
+  if (fp.blend_seg) {
     // the slot's tile and list segment in one load (the sort launch's);
     // otherwise the queue entry, then the tile's start and end
     const uint4 sg = b.blend_seg[slot];
@@ -3315,7 +3284,7 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
     s = sg.y;
     L = sg.z;
   } else {
-    tile = tile_in >= 0 ? tile_in : blend_tile_of(fp, b, slot);
+    tile = blend_tile_of(fp, b, slot);
     tile_segment(fp, b, tile, s, L);
   }
   const int lane = threadIdx.x & 63;
@@ -3338,13 +3307,6 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
   auto load_idx = [&](uint32_t k) -> uint32_t { return blend_idx(fp, list, L, k); };
   const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
   auto load_rec = [&](uint32_t g, float4& r0, float4& r1, float4& r2) {
-    if (fp.rec48) {
-      const float4* q3 = b.rec + 3 * (size_t)g;
-      r0 = q3[0];
-      r1 = q3[1];
-      r2 = q3[2];
-      return;
-    }
     const float4* qq = b.rec + 2 * (size_t)g;
     r0 = qq[0];
     const float4 t = qq[1];    // k1 pcut boxx boxy
@@ -3404,9 +3366,8 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
   // profiled frames: the staged records at this tile's wave slots 0 / 1 (2 / 3
   // unused: zeroed, the host takes the tile's largest)
   if (fp.count_records && lane == 0) {
-    const int cs = count_slot >= 0 ? count_slot : slot;
-    b.blend_count[4 * cs + half] = staged;
-    b.blend_count[4 * cs + 2 + half] = 0u;
+    b.blend_count[4 * slot + half] = staged;
+    b.blend_count[4 * slot + 2 + half] = 0u;
   }
   if (va) store_pixel(fp, b, px, tyb * fp.tile_h + ly, qa);
   if (vb) store_pixel(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
@@ -3418,28 +3379,6 @@ __global__ __launch_bounds__(64 * GS_PX2_WPG) void gs_blend_px2_kernel(FramePara
   __shared__ float4 s_rec[GS_PX2_WPG][3][64];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   blend_wave_px2<HWEXP>(fp, b, blockIdx.x * GS_PX2_WPG + wave, s_rec[wave]);
-}
-
-template <bool HWEXP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void gs_blend_px2h_kernel(FrameParams fp, Buffers b) {
-  GS_PROBE_SCOPE(kPrBlend);
-  __shared__ float4 s_rec[4][3][64];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // blend_px2 == 2: the lists longer than one wave's register sort (the big
-  // and medium queues, longest first) keep one pixel per lane and four waves
-  // per tile -- their waves' serial walks set the kernel's tail -- and the
-  // short lists (the small queue, tile order) take two pixels per lane, two
-  // tiles per workgroup.  Grid: n_tiles workgroups, the surplus exits.
-  const uint32_t nh = b.counters[0] + b.counters[7], ns = b.counters[9];
-  const uint32_t w = blockIdx.x;
-  if (w < nh) {
-    const int tile = (int)(w < b.counters[0] ? b.big_tiles[w] : b.medium_tiles[w - b.counters[0]]);
-    blend_wave<4, HWEXP>(fp, b, (int)w * 4 + wave, s_rec[wave], tile);
-    return;
-  }
-  const uint32_t k = 2u * (w - nh) + (uint32_t)(wave >> 1);
-  if (k >= ns) return;
-  blend_wave_px2<HWEXP>(fp, b, (int)k * 2 + (wave & 1), s_rec[wave], (int)b.small_tiles[k], (int)(nh + k));
 }
 
 // The sort inside the blend (FrameParams::blend_sort; one workgroup = the
@@ -3508,25 +3447,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
   blend_wave<4, HWEXP>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
 }
 
-// The in-blend sort with two-pixel lanes (FrameParams::blend_px2 with
-// blend_sort): a workgroup = two tiles (LPT slots 2w, 2w + 1), sorted one
-// after the other by all four waves, then blended by two waves each.
-template <bool HWEXP>
-__global__ __launch_bounds__(256) void gs_blend_sort_px2_kernel(FrameParams fp, Buffers b) {
-  GS_PROBE_SCOPE(kPrBlend);
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int slot0 = 2 * (int)blockIdx.x;
-  if (slot0 >= fp.n_tiles) return;
-#pragma unroll 1
-  for (int k = 0; k < 2; ++k) {
-    if (slot0 + k >= fp.n_tiles) break;  // (uniform)
-    blend_sort_tile(fp, b, blend_tile_of(fp, b, slot0 + k), reinterpret_cast<unsigned long long*>(lds));
-    __syncthreads();  // the list's stores done; the LDS free again
-  }
-  blend_wave_px2<HWEXP>(fp, b, (int)blockIdx.x * 4 + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
-}
-
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
 // the prefix blend).  A grid-stride loop over the waves of the big lists
 // only: a grid of every tile's waves, nearly all of which exit at once, cost
@@ -3558,23 +3478,15 @@ void launch_copy_word(hipStream_t s, uint32_t* dst, const uint32_t* src) {
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
   const int nb = (fp.n + 255) / 256;
-  const int grid = fp.project_grid > 0 ? std::min(nb, fp.project_grid) : nb;
   const bool plain = !fp.full_record && !(fp.sh_degree >= 0 && b.sh) && !fp.bin_global;
-  if (grid < nb) {  // (A/B: GSPLAT_PROJECT_GRID)
-    if (fp.pow2)
-      gs_project_kernel<true, kProjAny, true><<<grid, 256, 0, s>>>(fp, b);
-    else
-      gs_project_kernel<false, kProjAny, true><<<grid, 256, 0, s>>>(fp, b);
-  } else if (fp.pow2 && plain && !fp.band_cull && !fp.bin_agg) {
-    gs_project_kernel<true, kProjLean, false><<<grid, 256, 0, s>>>(fp, b);
+  if (fp.pow2 && plain && !fp.band_cull && !fp.bin_agg) {
+    gs_project_kernel<true, kProjLean><<<nb, 256, 0, s>>>(fp, b);
   } else if (fp.pow2 && plain && fp.band_cull && fp.bin_agg) {
-    gs_project_kernel<true, kProjBand, false><<<grid, 256, 0, s>>>(fp, b);
-  } else if (fp.pow2 && plain && !fp.band_cull && fp.bin_agg) {
-    gs_project_kernel<true, kProjAgg, false><<<grid, 256, 0, s>>>(fp, b);
+    gs_project_kernel<true, kProjBand><<<nb, 256, 0, s>>>(fp, b);
   } else if (fp.pow2) {
-    gs_project_kernel<true, kProjAny, false><<<grid, 256, 0, s>>>(fp, b);
+    gs_project_kernel<true, kProjAny><<<nb, 256, 0, s>>>(fp, b);
   } else {
-    gs_project_kernel<false, kProjAny, false><<<grid, 256, 0, s>>>(fp, b);
+    gs_project_kernel<false, kProjAny><<<nb, 256, 0, s>>>(fp, b);
   }
 }
 
@@ -3666,27 +3578,12 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (waves == 0) return;
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
-  if (fp.blend_px2 && !fp.blend_sort) {  // (16x16 tiles, no lazy lists: two waves per tile)
-    if (fp.blend_px2 == 2) {
-      if (fp.fast_exp)
-        gs_blend_px2h_kernel<true><<<(unsigned)fp.n_tiles, 256, 0, s>>>(fp, b);
-      else
-        gs_blend_px2h_kernel<false><<<(unsigned)fp.n_tiles, 256, 0, s>>>(fp, b);
-      return;
-    }
+  if (fp.blend_px2) {  // (16x16 tiles, whole frames without lazy lists: two waves per tile)
     const unsigned g2 = (unsigned)((2L * fp.n_tiles + GS_PX2_WPG - 1) / GS_PX2_WPG);
     if (fp.fast_exp)
       gs_blend_px2_kernel<true><<<g2, 64 * GS_PX2_WPG, 0, s>>>(fp, b);
     else
       gs_blend_px2_kernel<false><<<g2, 64 * GS_PX2_WPG, 0, s>>>(fp, b);
-    return;
-  }
-  if (fp.blend_sort && fp.blend_px2) {  // (two tiles per workgroup)
-    const unsigned g2 = (unsigned)((fp.n_tiles + 1) / 2);
-    if (fp.fast_exp)
-      gs_blend_sort_px2_kernel<true><<<g2, 256, 0, s>>>(fp, b);
-    else
-      gs_blend_sort_px2_kernel<false><<<g2, 256, 0, s>>>(fp, b);
     return;
   }
   if (fp.blend_sort) {  // (blend_bqw == 4, chunks_per_tile == GS_BLEND_WPG: one workgroup per tile)
@@ -3735,12 +3632,12 @@ void launch_blend_cont(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   // lists); its kernels return at once when counters[1] says no list
   // outlived its window.  Full grids: 256-workgroup grid-stride grids made
   // the frames that do have pass-2 lists slower (config 5: continuation
-  // 204 -> 246 us, 1 535 -> 1 492 frames/s; GSPLAT_PASS2_GRID, A/B)
+  // 204 -> 246 us, 1 535 -> 1 492 frames/s)
   FrameParams f2 = fp;
   f2.big_pass = 2;
   gs_big_prefix_kernel<<<1, 1024, 0, s>>>(f2, b);
   // (the splitters of every big list were chosen by the frame's first split pass)
-  const unsigned g2 = fp.pass2_grid > 0 ? (unsigned)fp.pass2_grid : 4096u;
+  const unsigned g2 = 4096u;
   launch_big_buckets(f2, b, s, g2);
   f2.blend_cont = 1;
   const unsigned grid2 = std::min(grid, g2);

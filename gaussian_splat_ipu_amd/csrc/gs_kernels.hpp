@@ -46,12 +46,10 @@ struct FrameParams {
   int blend_seg;        // (blend_lpt, two-pixel lanes, the sort launch sorts every list) the
                         //   sort launch writes each slot's (tile, start, length), the blend
                         //   reads it in one load
-  int project_grid;     // > 0: the projection as this many workgroups walking the blocks (A/B)
-  int emit_grid;
-  int pass2_grid;       // > 0: the lazy continuation's pass-2 grid-stride grids (A/B; default 4096)
-  int rec48;            // the 48-B record with the colour and opacity in it (the blend's staged layout): no colour gather        // > 0: the aggregated emit as this many workgroups walking the blocks (A/B)
-  int blend_sort;
-  int blend_px2;        // two pixels per blend lane (16x16 tiles, no in-blend sort): 1 every tile (no lazy lists), 2 the short lists       // each blend workgroup (one 16x16 tile) sorts its tile's list first: no tile-sort launch
+  int emit_grid;        // the aggregated emit's workgroups, walking the projection blocks
+  int blend_sort;       // each blend workgroup (one 16x16 tile) sorts its tile's list first: no
+                        //   tile-sort launch (row bands)
+  int blend_px2;        // two pixels per blend lane (16x16 tiles, whole frames without lazy lists)
   unsigned long long pair_cap;
   int write_rgba;
   int bgr_pitch;      // bytes per row of the BGR8 output

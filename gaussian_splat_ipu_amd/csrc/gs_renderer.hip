@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -46,18 +47,16 @@ int select_device(gs_renderer* r) {
   return GS_OK;
 }
 
-// GSPLAT_DEBUG_POISON=1: every device buffer is filled with 0xA5 bytes when it
-// is allocated (before any initialisation the renderer does itself), so a
-// kernel that reads memory no earlier stage of the frame wrote gives a
-// different frame than in a fresh process (tests/test_gpu_poison.py).  A
-// comma-separated list of buffer names poisons just those.
+// gs_test_set (include/gsplat.h): the test hooks gs_create reads
+std::atomic<int64_t> g_test_chunk_size{0}, g_test_bin_agg{-1}, g_test_poison{0};
+
+// gs_test_set("debug_poison", 1): every device buffer is filled with 0xA5
+// bytes when it is allocated (before any initialisation the renderer does
+// itself), so a kernel that reads memory no earlier stage of the frame wrote
+// gives a different frame than in a fresh process (tests/test_gpu_poison.py).
 void poison(void* p, size_t bytes, const char* name) {
-  const char* ev = std::getenv("GSPLAT_DEBUG_POISON");
-  if (!p || !bytes || !ev || !*ev || std::strcmp(ev, "0") == 0) return;
-  if (std::strcmp(ev, "1") != 0) {
-    const std::string list = std::string(",") + ev + ",";
-    if (list.find(std::string(",") + name + ",") == std::string::npos) return;
-  }
+  (void)name;
+  if (!p || !bytes || g_test_poison.load() == 0) return;
   (void)hipMemset(p, 0xA5, bytes);
 }
 
@@ -247,25 +246,16 @@ gsk::FrameParams make_params(const gs_renderer* r) {
                        : fp.blend_bqw == 8 ? (int)((tw / 16) * (th / 4))
                                            : (int)((((tw + 1) / 2) * ((th + 1) / 2) + 15) / 16);
   fp.blend_lpt = r->band_nrows < r->tiles_y ? 1 : 0;
-  if (r->env_blend_lpt >= 0) fp.blend_lpt = r->env_blend_lpt;  // (A/B)
   // the tile sort inside the blend's workgroups (16x16 tiles: one workgroup
   // per tile) for row bands: 8 bands of config 4, 38.2 -> 37.2 us per frame;
   // whole frames keep the sort launch (config 3: 7 980 against 7 800
   // frames/s, the sort launch overlapping the other frames' blends better;
-  // config 5 1 440 against 1 453).  GSPLAT_BLEND_SORT=0 / 1 forces it off /
-  // on (A/B).
-  // the aggregated emit as 2048 workgroups walking the 256-Gaussian blocks
-  // (one resident round: 8 per CU) rather than one per block: a band's culled
-  // blocks cost a loop iteration, not a workgroup (GSPLAT_EMIT_GRID = G, 0:
-  // one workgroup per block).  The projection keeps one workgroup per block
-  // by default (GSPLAT_PROJECT_GRID = G walks): inside the walking loop it
-  // needs 73-113 VGPRs instead of 51-57 (gs_kernels.hip)
-  fp.emit_grid = r->env_emit_grid >= 0 ? r->env_emit_grid : 2048;
-  fp.rec48 = r->env_rec48 > 0 ? 1 : 0;  // (A/B: GSPLAT_REC48=1)
-  fp.pass2_grid = r->env_pass2_grid;     // (A/B: GSPLAT_PASS2_GRID=G)
-  fp.project_grid = r->env_project_grid >= 0 ? r->env_project_grid : 0;
-  fp.blend_sort = (fp.blend_bqw == 4 && fp.chunks_per_tile == 4 &&
-                   (r->env_blend_sort == 1 || (r->env_blend_sort < 0 && r->band_nrows < r->tiles_y))) ? 1 : 0;
+  // config 5 1 440 against 1 453).
+  // The aggregated emit runs as 2048 workgroups walking the 256-Gaussian
+  // blocks (one resident round: 8 per CU) rather than one per block: a band's
+  // culled blocks cost a loop iteration, not a workgroup.
+  fp.emit_grid = 2048;
+  fp.blend_sort = (fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && r->band_nrows < r->tiles_y) ? 1 : 0;
   fp.pair_cap = r->pair_cap;
   fp.write_rgba = (r->cfg.flags & GS_FLAG_NO_RGBA32F) ? 0 : 1;
   fp.bgr_pitch = (int)r->cfg.width * 3;
@@ -288,51 +278,38 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // binning (config 3: 8 087 against 8 057 frames/s; config 5's 32 400
   // tiles: 1 447 against 1 444, its projection 156 against 224 us from the
   // clustered scene's hot-tile atomics)
-  fp.bin_agg = (r->bin_agg && !r->lattice &&
-                (r->bin_agg_mode == 1 || (r->band_nrows < r->tiles_y && r->n_tiles <= kAggMaxTiles))) ? 1 : 0;
+  fp.bin_agg = (r->bin_agg && !r->lattice && r->band_nrows < r->tiles_y && r->n_tiles <= kAggMaxTiles) ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && ((r->n_chunks > 0 && fp.emit_wide) || fp.bin_agg)) ? 1 : 0;
-  fp.mean_w1 = (r->scene_w1 && r->env_mean_w1 != 0) ? 1 : 0;  // (A/B: GSPLAT_MEAN_W1=0)
+  fp.mean_w1 = r->scene_w1 ? 1 : 0;
   // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
-  fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256 && r->env_rect8 != 0) ? 1 : 0;
+  fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256) ? 1 : 0;
   // the big-list launch only when the last frame the device completed had
   // big lists (a hint read from the mapped counters: either choice sorts
   // every list, the other launch handles them otherwise)
   fp.big_separate = (r->h_counters && ((volatile const uint32_t*)r->h_counters)[0] > 0) ? 1 : 0;
   // lazy big lists: sort only the lists' nearest keys before the blend
-  // (GSPLAT_LAZY=0 sorts every big list in full first)
-  {
-    static const bool lazy_env = !(std::getenv("GSPLAT_LAZY") && std::strcmp(std::getenv("GSPLAT_LAZY"), "0") == 0);
-    fp.lazy = (fp.big_separate && lazy_env && r->d_lazy && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 &&
-               !r->bin_global && r->n_chunks > 0) ? 1 : 0;
-  }
+  fp.lazy = (fp.big_separate && r->d_lazy && fp.blend_bqw == 4 && fp.chunks_per_tile == 4 && !r->bin_global &&
+             r->n_chunks > 0) ? 1 : 0;
   fp.big_pass = 0;
   fp.blend_cont = 0;
   // two pixels per blend lane on whole frames without lazy big lists
   // (config 3: 8 235 -> 8 454 frames/s, three interleaved repeats, although
   // the blend alone, one frame in flight, takes 87 instead of 77 us: half
   // the waves, each with two pixel chains, leave CUs to the other frames and
-  // stage each tile's records twice instead of four times).
-  // GSPLAT_BLEND_PX2=0 keeps one pixel per lane; =2 takes two pixels only on
-  // the short lists' tiles, which lazy frames allow (their big lists keep the
-  // one-pixel waves whose state the continuation resumes): config 3 8 196,
-  // config 5 1 520 -> 1 482, so not the default.
+  // stage each tile's records twice instead of four times).  Lazy frames
+  // (config 5) keep one pixel per lane: the continuation resumes those waves.
   // blend_wave_px2 maps a wave onto a 16x8 half of a 16x16 tile: other
-  // shapes with four 8x8 blocks (32x8, 8x32) keep one pixel per lane
+  // shapes with four 8x8 blocks (32x8, 8x32) keep one pixel per lane.
   const bool tile16 = tw == 16 && th == 16;
-  const int px2 = r->env_blend_px2 >= 0 ? r->env_blend_px2 : 1;
-  fp.blend_px2 = (px2 > 0 && tile16 && !fp.blend_sort && (!fp.lazy || px2 == 2)) ? px2 : 0;
-  // row bands (the in-blend sort): two-pixel lanes, two tiles per workgroup
-  // (GSPLAT_BAND_PX2=1, A/B)
-  if (tile16 && fp.blend_sort && !fp.lazy && r->env_band_px2 > 0) fp.blend_px2 = 1;
+  fp.blend_px2 = (tile16 && !fp.blend_sort && !fp.lazy) ? 1 : 0;
   // two-pixel lanes walk a tile's list in half the waves, so a heavy tile's
   // walk is twice as long: its waves start first (the sort queues' order,
   // longest lists first) -- config 3 blend 86.4 -> 79.4 us alone, 8 451 ->
-  // 8 524 frames/s, three interleaved repeats (GSPLAT_BLEND_LPT=0: tile order)
-  if (fp.blend_px2 == 1 && r->env_blend_lpt < 0) fp.blend_lpt = 1;
+  // 8 524 frames/s, three interleaved repeats
+  if (fp.blend_px2) fp.blend_lpt = 1;
   // ... and read their slot's tile and list segment in one load, written by
   // the sort launch (which sorts every list when big_separate is off)
-  fp.blend_seg = (fp.blend_px2 == 1 && fp.blend_lpt && !fp.blend_sort && !fp.big_separate && !fp.lazy &&
-                  r->env_blend_seg != 0) ? 1 : 0;
+  fp.blend_seg = (fp.blend_px2 && !fp.big_separate) ? 1 : 0;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
@@ -743,17 +720,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->n = n;
   r->profile = (cfg->flags & GS_FLAG_PROFILE) != 0;
   r->pair_cull = (cfg->flags & GS_FLAG_NO_PAIR_CULL) == 0;
-  if (const char* ev = std::getenv("GSPLAT_BLEND_LPT")) r->env_blend_lpt = std::atoi(ev) != 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_MEAN_W1")) r->env_mean_w1 = std::atoi(ev) != 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_RECT8")) r->env_rect8 = std::atoi(ev) != 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_EMIT_GRID")) r->env_emit_grid = std::max(0, std::atoi(ev));
-  if (const char* ev = std::getenv("GSPLAT_REC48")) r->env_rec48 = std::atoi(ev) > 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_BLEND_PX2")) r->env_blend_px2 = std::max(0, std::min(2, std::atoi(ev)));
-  if (const char* ev = std::getenv("GSPLAT_BAND_PX2")) r->env_band_px2 = std::atoi(ev) > 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_BLEND_SEG")) r->env_blend_seg = std::atoi(ev) != 0 ? 1 : 0;
-  if (const char* ev = std::getenv("GSPLAT_PASS2_GRID")) r->env_pass2_grid = std::max(0, std::atoi(ev));
-  if (const char* ev = std::getenv("GSPLAT_PROJECT_GRID")) r->env_project_grid = std::max(0, std::atoi(ev));
-  if (const char* ev = std::getenv("GSPLAT_BLEND_SORT")) r->env_blend_sort = std::strcmp(ev, "0") == 0 ? 0 : 1;  // else -1: auto
   int dev = cfg->device;
   if (dev < 0) {
     hipError_t e = hipGetDevice(&dev);
@@ -945,16 +911,11 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
     cs = std::min<size_t>(cs, 65535);
     // chunks of <= 65535 Gaussians (16-bit LDS counters): scenes beyond
     // ~16.7 M take more than 256 chunks, which gs_colscan_kernel handles with a
-    // second read of the extra rows.  Test hooks: GSPLAT_BIN_CHUNK_SIZE sets
-    // the chunk size (many chunks at a small N); GSPLAT_BIN_MAX_CHUNKS sends
-    // scenes of more chunks to the global-atomic path.
-    const char* fixed_cs = std::getenv("GSPLAT_BIN_CHUNK_SIZE");
-    if (fixed_cs) cs = (size_t)std::max(64, std::min(65535, std::atoi(fixed_cs)));
-    size_t max_chunks = SIZE_MAX;
-    if (const char* ev = std::getenv("GSPLAT_BIN_MAX_CHUNKS")) max_chunks = (size_t)std::max(1, std::atoi(ev));
-    if ((n + cs - 1) / cs > max_chunks) {
-      r->bin_global = 1;
-    } else {
+    // second read of the extra rows.  Test hook (gs_test_set): the chunk
+    // size, to reach many chunks at a small N.
+    const int64_t fixed_cs = g_test_chunk_size.load();
+    if (fixed_cs > 0) cs = (size_t)std::max<int64_t>(64, std::min<int64_t>(65535, fixed_cs));
+    {
       if ((e = gsk::init_kernel_attributes()) != hipSuccess) return fail(hip_fail(e, "hipFuncSetAttribute"));
       r->chunk_size = (int)cs;
       r->n_chunks = (int)((n + cs - 1) / cs);
@@ -963,16 +924,14 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       // (make_params), so the densest chunk -- the binning's critical path --
       // shrinks with the band instead of staying a whole-frame chunk
       r->chunk_entries = (size_t)r->n_chunks * (size_t)std::max(r->n_tiles, r->tiles_x * r->tiles_y);
-      r->chunk_adaptive = fixed_cs == nullptr && max_chunks == SIZE_MAX;
+      r->chunk_adaptive = fixed_cs <= 0;
       // the aggregated binning for grids of up to kAggMaxTiles tiles (frames
       // at 1080p, any row band of a 4K frame split over >= 2 GPUs), the
       // chunked count / column scan / emit beyond (config 5's 4K frame on one
       // GPU: its clustered workgroups fill few tiles, whose LDS atomics cost
-      // the projection more than the chunked passes take).  GSPLAT_BIN_AGG=0 /
-      // 1 forces either (A/B, tests).
-      const char* agg_env = std::getenv("GSPLAT_BIN_AGG");
-      r->bin_agg_mode = agg_env ? (std::strcmp(agg_env, "0") == 0 ? 0 : 1) : -1;
-      r->bin_agg = r->bin_agg_mode != 0 && fixed_cs == nullptr;
+      // the projection more than the chunked passes take).  Test hook
+      // (gs_test_set "bin_agg" 0): row bands bin with the chunked passes too.
+      r->bin_agg = g_test_bin_agg.load() != 0 && fixed_cs <= 0;
       if (r->bin_agg) {  // per projection block: its tile box and its offsets in each tile
         const size_t nb = (nn + 255) / 256;
         const size_t agg_bytes = nb * 16 + nb * (size_t)gsk::kAggCap * 4;
@@ -1310,6 +1269,22 @@ using namespace gsr;
 extern "C" {
 
 int gs_abi_version(void) { return GSPLAT_ABI_VERSION; }
+
+int gs_test_set(const char* key, int64_t value) {
+  if (!key) return GS_EINVAL;
+  const std::string k(key);
+  if (k == "bin_chunk_size" && value >= 0) {
+    gsr::g_test_chunk_size.store(value);
+  } else if (k == "bin_agg" && (value == -1 || value == 0)) {
+    gsr::g_test_bin_agg.store(value);
+  } else if (k == "debug_poison" && (value == 0 || value == 1)) {
+    gsr::g_test_poison.store(value);
+  } else {
+    gsh::set_error("gs_test_set: unknown key or value");
+    return GS_EINVAL;
+  }
+  return GS_OK;
+}
 
 const char* gs_last_error(void) { return gsh::last_error(); }
 

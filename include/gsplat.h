@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 11
+#define GSPLAT_ABI_VERSION 12
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -490,6 +490,21 @@ int gs_cam_mvp_start(float* out);
  * fov, width/height).  Outputs are ROW-MAJOR (ready for gs_set_view/projection). */
 int gs_cam_headless(const float* bb6, uint32_t width, uint32_t height, float fov,
                     float* view_rm, float* proj_rm);
+
+/* ------------------------------------------------------------ test hooks
+ * ABI 12.  For the parity tests only: process-wide values that gs_create
+ * reads, so a small scene reaches a path that otherwise needs a large one.
+ * No environment variable selects a kernel or a path: a production caller
+ * that never calls this gets the documented automatic choices.
+ *   "bin_chunk_size"  Gaussians per binning chunk (0 = automatic): small
+ *                     chunks reach the > 256-chunk column scan at 120 k
+ *                     Gaussians instead of 16.7 M
+ *   "bin_agg"         -1 = automatic; 0 = row bands bin with the chunked
+ *                     passes too (the path of bands wider than 16 384 tiles)
+ *   "debug_poison"    1 = every device buffer starts as 0xA5 bytes instead
+ *                     of zeros (reads of memory no stage wrote show up)
+ * Returns GS_EINVAL for an unknown key or value. */
+int gs_test_set(const char* key, int64_t value);
 
 #ifdef __cplusplus
 }

@@ -32,3 +32,22 @@ def pc12_scene(built):
     ply = scene.load_ply(PC12)
     g, bb = scene.prepare_scene(ply)
     return g, bb
+
+
+# gs_test_set keys (include/gsplat.h) and their automatic values
+TEST_HOOK_DEFAULTS = {"bin_chunk_size": 0, "bin_agg": -1, "debug_poison": 0}
+
+
+@pytest.fixture
+def test_hook(built):
+    """gs_test_set: a process-wide test hook read by gs_create (no environment
+    variable selects a path); every hook is back at its automatic value after
+    the test."""
+    from gaussian_splat_ipu_amd._lib import check, lib
+
+    def set_hook(key, value):
+        check(lib().gs_test_set(key.encode(), int(value)), "gs_test_set")
+
+    yield set_hook
+    for k, v in TEST_HOOK_DEFAULTS.items():
+        lib().gs_test_set(k.encode(), v)

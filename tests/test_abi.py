@@ -47,7 +47,7 @@ def test_abi_version_and_config_defaults(built):
     from gaussian_splat_ipu_amd import _lib
 
     L = _lib.lib()
-    assert L.gs_abi_version() == 11
+    assert L.gs_abi_version() == 12
     cfg = _lib.Config()
     assert L.gs_config_init(ctypes.byref(cfg)) == 0
     # tile_config.hpp:5-15 and codelets.cpp:622
@@ -113,7 +113,7 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
                     "-L", libdir, "-lgsplat", f"-Wl,-rpath,{libdir}"], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    assert int(out[0]) == 11
+    assert int(out[0]) == 12
     # the ctypes mirrors have the C layouts
     assert int(out[2]) == ctypes.sizeof(_lib.Config)
     assert int(out[3]) == ctypes.sizeof(_lib.FrameStats)
@@ -149,3 +149,29 @@ def test_balanced_bands_matches_the_python_rule(built):
     b = (ctypes.c_uint32 * 4)()
     one = np.ones(2)
     assert L.gs_balanced_bands(one.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 2, 3, b) == _lib.GS_EINVAL
+
+
+def test_no_environment_variable_selects_a_path(built):
+    """a production libgsplat.so reads no GSPLAT_* variable that
+    picks a kernel or a path.  The only names in the binary are the RCCL
+    library override and the timeline probe's output file (probe builds); the
+    test hooks are an explicit call (gs_test_set)."""
+    import re
+
+    from gaussian_splat_ipu_amd import _lib
+
+    data = open(_lib.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"GSPLAT_[A-Z0-9_]+", data))
+    assert names <= {b"GSPLAT_RCCL", b"GSPLAT_PROBE_FILE"}, names
+
+
+def test_test_hooks_accept_only_their_keys(built):
+    from gaussian_splat_ipu_amd import _lib
+
+    L = _lib.lib()
+    assert L.gs_test_set(b"bin_chunk_size", 0) == 0
+    assert L.gs_test_set(b"bin_agg", -1) == 0
+    assert L.gs_test_set(b"debug_poison", 0) == 0
+    assert L.gs_test_set(b"bin_agg", 1) == _lib.GS_EINVAL  # (only -1 / 0)
+    assert L.gs_test_set(b"blend_px2", 0) == _lib.GS_EINVAL
+    assert L.gs_test_set(None, 0) == _lib.GS_EINVAL

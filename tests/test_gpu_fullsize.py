@@ -260,47 +260,25 @@ def test_overflow_is_sticky_across_async_frames(built):
 
 
 @pytest.mark.parametrize("chunk,pair_cull", [(256, True), (128, True), (256, False)])
-def test_binning_more_than_256_chunks(built, monkeypatch, chunk, pair_cull):
+def test_binning_more_than_256_chunks(built, test_hook, chunk, pair_cull):
     """Scenes beyond 256 binning chunks (~16.7 M Gaussians at 65535 per chunk)
     stay on the chunked binning: gs_colscan_kernel reads a wave's rows past
-    its 16th twice.  GSPLAT_BIN_CHUNK_SIZE shrinks the chunks so 120 k
+    its 16th twice.  The bin_chunk_size test hook shrinks the chunks so 120 k
     Gaussians make 469 / 938 of them; the frame and the lists stay bit-exact."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
 
     g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=120_000, seed=2, sh_degree=0)))
     view, proj = camera.headless(bb, 1920, 1080)
-    monkeypatch.setenv("GSPLAT_BIN_CHUNK_SIZE", str(chunk))
+    test_hook("bin_chunk_size", chunk)
     s = _splatter(g, view, proj, 1920, 1080, 16, pair_cull=pair_cull)
-    monkeypatch.delenv("GSPLAT_BIN_CHUNK_SIZE")
+    test_hook("bin_chunk_size", 0)
     assert s.stats()["bin_global"] == 0
     f = O.make_frame(view, proj, 1920, 1080, 16, 16, camera.FOV_DEFAULT, 1.0)
     ref = O.render(g, f)
     for _ in range(2):
         s.execute()
         _check_frame(s, g, f, ref)
-    s.close()
-
-
-def test_binning_forced_to_global_atomics(built, monkeypatch):
-    """GSPLAT_BIN_MAX_CHUNKS sends a scene of more chunks to the global-atomic
-    binning (the path for tile grids too large for one CU's LDS); the frame
-    stays bit-exact."""
-    from gaussian_splat_ipu_amd import camera, scene
-    from oracle import oracle as O
-
-    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=2, sh_degree=0)))
-    view, proj = camera.headless(bb, 960, 540)
-    monkeypatch.setenv("GSPLAT_BIN_MAX_CHUNKS", "2")  # 20000 Gaussians = 5 chunks of 4096
-    s = _splatter(g, view, proj, 960, 540, 16)
-    monkeypatch.delenv("GSPLAT_BIN_MAX_CHUNKS")
-    assert s.stats()["bin_global"] == 1
-    s.execute()
-    f = O.make_frame(view, proj, 960, 540, 16, 16, camera.FOV_DEFAULT, 1.0)
-    _check_frame(s, g, f, O.render(g, f))
-    s.close()
-    s = _splatter(g, view, proj, 960, 540, 16)
-    assert s.stats()["bin_global"] == 0
     s.close()
 
 
@@ -334,9 +312,8 @@ def test_ref_tile_major_readback(built, tw, th):
 
 
 # ------------------------------------------------------------- lazy big lists
-@pytest.mark.parametrize("px2", ["0", "2"])
 @pytest.mark.parametrize("op_lo,op_hi", [(0.004, 0.02), (0.02, 0.3)])
-def test_lazy_big_lists_continuation(built, monkeypatch, op_lo, op_hi, px2):
+def test_lazy_big_lists_continuation(built, op_lo, op_hi):
     """Big lists (> 2048 keys) of faint Gaussians: pixels outlive the sorted
     prefix of ~1.5 k keys, so their blend waves save their state and continue
     over the sorted window of the next keys (pass 1); waves that outlive the
@@ -344,12 +321,9 @@ def test_lazy_big_lists_continuation(built, monkeypatch, op_lo, op_hi, px2):
     gs_kernels.hip, lazy big lists).  The second frame of the renderer takes
     that path; the frame must equal the oracle's bit for bit.  op 0.004-0.02:
     nearly every big tile continues, and some pixels never saturate (pass 2);
-    0.02-0.3: some do.  px2 2: the short lists' tiles blend two pixels per
-    lane beside the big lists' one-pixel waves."""
+    0.02-0.3: some do."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
-
-    monkeypatch.setenv("GSPLAT_BLEND_PX2", px2)
 
     src = scene.load_ply(PC12)
     centres = np.stack([src["x"], src["y"], src["z"]], 1)[::4]

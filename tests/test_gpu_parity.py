@@ -130,31 +130,31 @@ def test_synthetic_1080p_16x16(built):
     _assert_parity(s, f, g)
 
 
-@pytest.mark.parametrize("bsort,rec48,px2", [("0", "0", "0"), ("1", "0", "0"), ("0", "1", "0"), ("0", "0", "1"),
-                                              ("0", "0", "2")])
-def test_large_tile_lists_take_the_radix_path(built, monkeypatch, bsort, rec48, px2):
+@pytest.mark.parametrize("band", [None, 0, 1])
+def test_large_tile_lists_take_the_radix_path(built, band):
     """A clustered scene (config 5's construction) puts > 2048 Gaussians on
     some tiles: those go through the block-wide LSD radix sort, first inside
-    the tile-sort launch (bsort 1: inside the blend's workgroups), then
-    (second frame) in the separate big-list launch.  rec48: the 48-B record
-    with the colour in it (the lazy lists' alpha boxes read from it too)."""
+    the tile-sort launch (a whole frame) or inside the blend's workgroups
+    (band 0 / 1 of two: the in-blend sort), then (second frame) in the
+    separate big-list launches (lazy prefixes, the continuation)."""
     from gaussian_splat_ipu_amd import camera, scene
-
-    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
-    monkeypatch.setenv("GSPLAT_REC48", rec48)
-    monkeypatch.setenv("GSPLAT_BLEND_PX2", px2)  # (the first frame; the lazy lists' frames keep one pixel per lane)
 
     src = scene.load_ply(PC12)
     cl = np.stack([src["x"], src["y"], src["z"]], 1)[:200]
     ply = scene.synthetic(scene.SynthSpec(n=150_000, seed=8, sh_degree=0, cluster_xyz=cl, cluster_sigma=0.02))
     g, bb = scene.prepare_scene(ply)
     view, proj = camera.headless(bb, 1280, 720)
-    s, f = _frame_pair(g, view, proj, 1280, 720, 16, 16, 1.0)
+    if band is None:
+        s, f = _frame_pair(g, view, proj, 1280, 720, 16, 16, 1.0)
+    else:
+        s, f = _frame_pair(g, view, proj, 1280, 720, 16, 16, 1.0, band_count=2, band_index=band)
+        assert s.stats()["paths"] & 2  # (GS_PATH_BLEND_SORT)
     _assert_parity(s, f, g)
     assert s.stats()["n_big_tiles"] > 0
     # the next frame sees big lists in the last completed frame's counters and
-    # sorts them in their own 1024-thread launch (gs_sort_big_kernel)
+    # sorts them in their own launches (lazy prefixes, 16x16 tiles)
     s.execute()
+    assert s.stats()["paths"] & 16  # (GS_PATH_BIG_LISTS)
     _assert_parity(s, f, g)
 
 
@@ -515,10 +515,10 @@ def test_render_server_cli(built, tmp_path):
     assert out2.read_bytes() == data
 
 
-@pytest.mark.parametrize("bsort", ["0", "1", "px2", "px2h"])
+@pytest.mark.parametrize("band", [None, 0, 1])
 @pytest.mark.parametrize("half_width,log_scale,planes", [
     (1.5, -3.8, 4), (0.3, -4.0, 4), (1.5, -3.8, 64), (0.3, -4.0, 400), (0.3, -4.0, 1)])
-def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale, planes, bsort):
+def test_equal_depths_keep_input_order(built, half_width, log_scale, planes, band):
     """Gaussians on planes of constant clip z (a view that only translates
     along z), in shuffled input order: the tile lists hold runs of equal
     depth, whose order must be the input index's (the oracle's stable order),
@@ -527,13 +527,11 @@ def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale
     first frame, the big-list sample sort on the second).  4 planes make long
     runs (the list is re-sorted), 64 / 400 planes mostly short ones (put in
     order in place); one plane gives big lists of a single depth (one
-    sample-sort bucket > 2048 keys: its radix path).  bsort 1: the tile
-    sort inside the blend's workgroups."""
+    sample-sort bucket > 2048 keys: its radix path).  A whole frame (the
+    sort launch, two-pixel blend lanes) and the two bands of a 2-way split
+    (the tile sort inside the blend's workgroups)."""
     from gaussian_splat_ipu_amd import camera, scene
     from oracle import oracle as O
-
-    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort if bsort in ("0", "1") else "0")
-    monkeypatch.setenv("GSPLAT_BLEND_PX2", {"px2": "1", "px2h": "2"}.get(bsort, "0"))
 
     g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=5, sh_degree=0)))
     a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
@@ -547,16 +545,20 @@ def test_equal_depths_keep_input_order(built, monkeypatch, half_width, log_scale
     a[:, 12:15] = log_scale + rng.normal(0.0, 0.2, (n, 3))
     _, proj = camera.headless(bb, 1280, 720)
     view = np.float32([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, -4.0, 0, 0, 0, 1])
-    s, f = _frame_pair(a, view, proj, 1280, 720, 16, 16, 1.0)
+    if band is None:
+        s, f = _frame_pair(a, view, proj, 1280, 720, 16, 16, 1.0)
+        f_all = f
+    else:
+        s, f = _frame_pair(a, view, proj, 1280, 720, 16, 16, 1.0, band_count=2, band_index=band)
+        f_all = O.make_frame(view, proj, 1280, 720, 16, 16, camera.FOV_DEFAULT, 1.0)
     ref = _assert_parity(s, f, a)
     # the lists really hold equal depths next to each other
-    p = O.project(a, f)
-    ts, lst = O.bin_lists(p, f)
+    p = O.project(a, f_all)
+    ts, lst = O.bin_lists(p, f_all)
     z = p["clip_z"][lst]
     same = (z[1:] == z[:-1]) & (np.diff(np.searchsorted(ts, np.arange(len(lst)), side="right")) == 0)
     assert same.sum() > 500
-    if half_width < 1.0:
-        assert s.stats()["n_big_tiles"] > 0
+    if half_width < 1.0 and s.stats()["n_big_tiles"] > 0:
         s.execute()  # big lists through the big-list sample sort
         _assert_parity(s, f, a)
     assert ref["stats"]["n_pairs"] > 0
@@ -634,32 +636,40 @@ def test_set_band_rows_keeps_the_in_flight_frame(pc12):
                                       full.get_histogram().reshape(fb.tiles_down, -1)[10:30].reshape(-1))
 
 
-@pytest.mark.parametrize("agg", ["0", "1"])
+@pytest.mark.parametrize("agg", [True, False])
 @pytest.mark.parametrize("tile", [(16, 16), (32, 20)])
-def test_binning_paths_bit_exact(pc12, monkeypatch, agg, tile):
-    """Both binning paths -- the aggregated one (per-tile counters summed by
-    the projection's workgroups, one-workgroup scan, emit by returning
-    atomics per (workgroup, tile)) and the chunked one (count / column scan /
-    emit) -- give the oracle's lists, histogram and frame bit for bit."""
+def test_binning_paths_bit_exact(pc12, test_hook, agg, tile):
+    """Both binning paths of a row band -- the aggregated one (per-tile
+    counters summed by the projection's workgroups, one-workgroup scan, emit
+    by returning atomics per (workgroup, tile); bands up to 16 384 tiles) and
+    the chunked one (count / column scan / emit; wider bands, and every whole
+    frame) -- give the oracle's lists, histogram and frame bit for bit."""
     from gaussian_splat_ipu_amd import camera
 
-    monkeypatch.setenv("GSPLAT_BIN_AGG", agg)
+    if not agg:
+        test_hook("bin_agg", 0)
     g, bb = pc12
     W, H = 1920, 1080
     view, proj = camera.headless(bb, W, H)
+    for band_count, band_index in [(3, 1), (8, 3)]:
+        s, f = _frame_pair(g, view, proj, W, H, tile[0], tile[1], 1.0, band_count=band_count, band_index=band_index)
+        assert bool(s.stats()["paths"] & 1) == agg  # (GS_PATH_BIN_AGG)
+        _assert_parity(s, f, g, check_proj=False)
+        s.close()
     s, f = _frame_pair(g, view, proj, W, H, tile[0], tile[1], 1.0)
+    assert not s.stats()["paths"] & 1
     _assert_parity(s, f, g, check_proj=False)
     s.close()
 
 
-def test_aggregated_binning_4k_clustered(built, monkeypatch):
-    """The aggregated binning forced onto a 4K frame (32 400 tiles: the scan
-    runs four 8192-tile rounds) of a clustered scene (workgroups whose pairs
-    fall in a few tiles take the ballot path), three orbit views."""
+def test_aggregated_binning_4k_clustered(built):
+    """The aggregated binning of the two bands of a 4K frame (16 200 tiles
+    each: the scan runs two 8192-tile rounds) of a clustered scene
+    (workgroups whose pairs fall in a few tiles take the ballot path), three
+    orbit views."""
     from conftest import PC12
     from gaussian_splat_ipu_amd import camera, scene
 
-    monkeypatch.setenv("GSPLAT_BIN_AGG", "1")
     src = scene.load_ply(PC12)
     centres = np.stack([src["x"], src["y"], src["z"]], 1)
     g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=150_000, seed=8, sh_degree=0, cluster_xyz=centres,
@@ -668,115 +678,52 @@ def test_aggregated_binning_4k_clustered(built, monkeypatch):
     _, proj = camera.headless(bb, W, H)
     for k in (0, 40, 80):
         view = camera.orbit_view(k)
-        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0)
-        _assert_parity(s, f, g, check_proj=False)
-        s.close()
+        for band in (0, 1):
+            s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=2, band_index=band)
+            assert s.stats()["paths"] & 1  # (GS_PATH_BIN_AGG)
+            _assert_parity(s, f, g, check_proj=False)
+            s.close()
 
 
-@pytest.mark.parametrize("bsort", ["0", "1"])
-def test_blend_sort_paths_bit_exact(pc12, monkeypatch, bsort):
-    """The tile sort inside the blend's workgroups (GSPLAT_BLEND_SORT=1:
-    every 16x16 tile's workgroup sorts its list, then blends it) and the
-    separate sort launch give the oracle's lists, histogram and frame bit for
-    bit -- on a whole frame and on a row band (the default picks the in-blend
-    sort for bands only); the paths the frame took are in stats()["paths"]."""
+def test_blend_sort_paths_bit_exact(pc12):
+    """The tile sort inside the blend's workgroups (row bands of 16x16 tiles:
+    every tile's workgroup sorts its list, then blends it one pixel per lane)
+    and the separate sort launch (whole frames: two-pixel lanes) give the
+    oracle's lists, histogram and frame bit for bit; the paths each frame took
+    are in stats()["paths"]."""
     from gaussian_splat_ipu_amd import camera
 
-    monkeypatch.setenv("GSPLAT_BLEND_SORT", bsort)
     g, bb = pc12
     W, H = 1920, 1080
     view, proj = camera.headless(bb, W, H)
     for band_count, band_index in [(1, 0), (8, 3)]:
         s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
-        assert bool(s.stats()["paths"] & 2) == (bsort == "1")
+        paths = s.stats()["paths"]
+        assert bool(paths & 2) == (band_count > 1)  # (GS_PATH_BLEND_SORT)
+        assert bool(paths & 4) == (band_count == 1)  # (GS_PATH_BLEND_PX2)
         _assert_parity(s, f, g, check_proj=False)
         s.close()
 
 
 
-@pytest.mark.parametrize("grid", ["0", "7", "256"])
-def test_walking_grids_cover_every_block(pc12, monkeypatch, grid):
-    """GSPLAT_PROJECT_GRID=G / GSPLAT_EMIT_GRID=G: the projection and the
-    aggregated emit as G workgroups walking the 256-Gaussian blocks (LDS
-    reused block after block) bin every pair as the one-workgroup-per-block
-    launches do: a row band (band cull) and a whole frame with the aggregated
-    binning forced, bit for bit against the oracle."""
-    from gaussian_splat_ipu_amd import camera
-
-    monkeypatch.setenv("GSPLAT_PROJECT_GRID", grid)
-    monkeypatch.setenv("GSPLAT_EMIT_GRID", grid)
-    monkeypatch.setenv("GSPLAT_BIN_AGG", "1")
-    g, bb = pc12
-    W, H = 1920, 1080
-    view, proj = camera.headless(bb, W, H)
-    for band_count, band_index in [(1, 0), (8, 3)]:
-        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
-        assert s.stats()["paths"] & 1
-        _assert_parity(s, f, g, check_proj=False)
-        s.close()
-
-
-
-def test_rec48_bit_exact(pc12, monkeypatch):
-    """GSPLAT_REC48=1: the projection writes the 48-B record with the colour
-    and opacity in it and the blend reads it in one piece instead of
-    gathering the colour: a whole frame and a row band, bit for bit against
-    the oracle (the SH colour through it: test_sh.py)."""
-    from gaussian_splat_ipu_amd import camera
-
-    monkeypatch.setenv("GSPLAT_REC48", "1")
-    g, bb = pc12
-    W, H = 1920, 1080
-    view, proj = camera.headless(bb, W, H)
-    for band_count, band_index in [(1, 0), (8, 3)]:
-        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
-        _assert_parity(s, f, g, check_proj=False)
-        s.close()
-
-
-@pytest.mark.parametrize("lpt", ["auto", "0", "noseg"])
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("bin_global", [False, True])
 @pytest.mark.parametrize("W,H", [(1920, 1080), (1000, 700)])
-def test_blend_px2_bit_exact(pc12, monkeypatch, W, H, mode, lpt):
-    """GSPLAT_BLEND_PX2=1: two pixels per blend lane (a 16x8 half of the tile
-    per wave, one mask per pixel pair, two independent chains per record)
-    gives the oracle's frame bit for bit: a whole frame (partial tiles at the
-    right and bottom edges for 1000x700) and a row band with the sort launch
-    (the in-blend sort keeps the one-pixel lanes).  Mode 2: only the small
-    queue's tiles take two pixels per lane, the longer lists one.  Whole
-    frames with two-pixel lanes take the tiles longest list first by default
-    (lpt "auto"), reading each slot's tile and list segment from the sort
-    launch's table; "noseg" reads the queues and tile starts instead
-    (GSPLAT_BLEND_SEG=0); "0" keeps the tile order."""
+def test_blend_px2_bit_exact(pc12, W, H, bin_global):
+    """Two pixels per blend lane (whole frames of 16x16 tiles: a 16x8 half of
+    the tile per wave, one mask per pixel pair, two independent chains per
+    record, tiles longest list first) gives the oracle's frame bit for bit,
+    partial edge tiles included (1000x700).  The chunked binning has each
+    slot's tile and list segment written by the sort launch; the global-atomic
+    binning's frames read the queues and tile starts instead.  A row band
+    keeps one pixel per lane (the in-blend sort)."""
     from gaussian_splat_ipu_amd import camera
 
-    monkeypatch.setenv("GSPLAT_BLEND_PX2", mode)
-    monkeypatch.setenv("GSPLAT_BLEND_SORT", "0")
-    if lpt == "noseg":
-        monkeypatch.setenv("GSPLAT_BLEND_SEG", "0")
-    elif lpt != "auto":
-        monkeypatch.setenv("GSPLAT_BLEND_LPT", lpt)
     g, bb = pc12
     view, proj = camera.headless(bb, W, H)
     for band_count, band_index in [(1, 0), (8, 3)]:
-        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index)
-        _assert_parity(s, f, g, check_proj=False)
-        s.close()
-
-
-def test_band_px2_bit_exact(pc12, monkeypatch):
-    """GSPLAT_BAND_PX2=1: row bands with the in-blend sort and two-pixel
-    lanes (two tiles per workgroup, sorted one after the other), bit for
-    bit against the oracle on three bands of an 8-way split."""
-    from gaussian_splat_ipu_amd import camera
-
-    monkeypatch.setenv("GSPLAT_BAND_PX2", "1")
-    g, bb = pc12
-    W, H = 1920, 1080
-    view, proj = camera.headless(bb, W, H)
-    for band_index in (0, 3, 7):
-        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=8, band_index=band_index)
-        assert s.stats()["paths"] & 2
+        s, f = _frame_pair(g, view, proj, W, H, 16, 16, 1.0, band_count=band_count, band_index=band_index,
+                           bin_global=bin_global)
+        assert bool(s.stats()["paths"] & 4) == (band_count == 1)
         _assert_parity(s, f, g, check_proj=False)
         s.close()
 

@@ -1,5 +1,5 @@
-"""Frames from recycled device memory (GSPLAT_DEBUG_POISON=1: every device
-buffer the renderer allocates starts as 0xA5 bytes instead of the zeros a fresh
+"""Frames from recycled device memory (gs_test_set("debug_poison", 1): every
+device buffer the renderer allocates starts as 0xA5 bytes instead of the zeros a fresh
 process's first allocation happens to hold).  A stage that reads memory no
 earlier stage of the frame wrote gives a different frame -- or faults -- here,
 while passing every test in a fresh process.  Each case is checked bit for
@@ -20,8 +20,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def poison(monkeypatch):
-    monkeypatch.setenv("GSPLAT_DEBUG_POISON", "1")
+def poison(test_hook):
+    test_hook("debug_poison", 1)
 
 
 @pytest.fixture(scope="module")

@@ -76,15 +76,12 @@ def test_sh_oracle_degree0_is_the_prepared_colour_and_matches_numpy(built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("group,rec48,px2", [(False, "0", "0"), (True, "0", "0"), (False, "1", "0"), (False, "0", "1")])
-def test_sh_frames_match_the_oracle(built, monkeypatch, group, rec48, px2):
+@pytest.mark.parametrize("group", [False, True])
+def test_sh_frames_match_the_oracle(built, group):
     """Degree 3 at two views (and degree 0 == the default frame; off again
-    after degree -1), single renderer and a 2-band group; rec48: the SH
-    colour carried in the 48-B record."""
+    after degree -1), single renderer (two-pixel blend lanes) and a 2-band
+    group (the in-blend sort, one pixel per lane)."""
     from gaussian_splat_ipu_amd import camera, scene
-
-    monkeypatch.setenv("GSPLAT_REC48", rec48)
-    monkeypatch.setenv("GSPLAT_BLEND_PX2", px2)
     from gaussian_splat_ipu_amd.splatter import GpuSplatter
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
     from oracle import oracle as O
