@@ -133,10 +133,13 @@ struct Member {
   std::vector<gs_renderer*> slot;     // F band renderers (each its own stream)
   hipStream_t comm_stream = nullptr;  // all-gathers, in frame order
   ncclComm_t comm = nullptr;
-  uint8_t* d_send = nullptr;          // F x slot_cap: the band + footer of each in-flight frame
-  uint8_t* d_recv = nullptr;          // F x world x slot_cap: the gathered frames
+  // F x world x slot_cap: the gathered frames.  The band renders straight
+  // into its own part of the slot (rank x the frame's bytes per rank) and
+  // the all-gather runs in place (sendbuff = recvbuff + rank x count): no
+  // send buffer, no local copy of the band
+  uint8_t* d_recv = nullptr;
   std::vector<hipEvent_t> ev_render;    // per slot: the band is rendered
-  std::vector<hipEvent_t> ev_gathered;  // per slot: the all-gather read the send slot
+  std::vector<hipEvent_t> ev_gathered;  // per slot: the all-gather has read this member's part
   // set by the scan of any of this GPU's band frames that overflowed since
   // the last sync; copied into footer word kFootSticky before every gather
   uint32_t* d_sticky = nullptr;
@@ -414,6 +417,12 @@ int harvest_timing(Group* g, int i, bool block) {
   return GS_OK;
 }
 
+// member m's part of the frame's all-gather slot: its band and footer,
+// at rank x the frame's bytes per rank
+inline uint8_t* own_part(const Group* g, const Member& m, const FrameCmd& f) {
+  return m.d_recv + (size_t)f.i * g->world * g->slot_cap + (size_t)m.rank * f.bytes;
+}
+
 // Member m's band of the frame f: moved to the frame's split, rendered on
 // its band renderer's stream into its all-gather send slot.
 int member_render(Group* g, Member& m, const FrameCmd& f) {
@@ -425,10 +434,17 @@ int member_render(Group* g, Member& m, const FrameCmd& f) {
   std::memcpy(c->proj_rm, g->proj, sizeof(g->proj));
   c->fov = g->fov;
   c->scale_div = g->sd;
-  c->bgr_target = m.d_send + (size_t)f.i * g->slot_cap;
+  c->bgr_target = own_part(g, m, f);
   c->buf.footer = (uint32_t*)(c->bgr_target + f.bgr_part);
-  // the gather of frame k - F read this send slot
-  if (f.was_used) GS_HIP(hipStreamWaitEvent(c->stream, m.ev_gathered[f.i], 0));
+  // the gather of frame k - F read this part of the slot (the copy gather:
+  // every member's comm stream read it)
+  if (f.was_used) {
+    if (g->rccl) {
+      GS_HIP(hipStreamWaitEvent(c->stream, m.ev_gathered[f.i], 0));
+    } else {
+      for (const Member& o : g->mem) GS_HIP(hipStreamWaitEvent(c->stream, o.ev_gathered[f.i], 0));
+    }
+  }
   if (f.timed) GS_HIP(hipEventRecord(m.ev_t0[f.i], c->stream));
   if ((rc = gsr::enqueue_frame(c)) != GS_OK) return rc;
   GS_HIP(hipEventRecord(m.ev_render[f.i], c->stream));
@@ -445,10 +461,11 @@ int member_gather_rccl(Group* g, Member& m, const FrameCmd& f) {
   GS_HIP(hipStreamWaitEvent(m.comm_stream, m.ev_render[f.i], 0));
   // the GPU's sticky overflow bit into the footer: every frame up to this
   // one has finished its render here (the gathers run in frame order)
-  gsk::launch_copy_word(m.comm_stream, (uint32_t*)(m.d_send + (size_t)f.i * g->slot_cap + f.bgr_part) +
-                                           gsk::kFootSticky, m.d_sticky);
-  GS_NCCL(rccl().AllGather(m.d_send + (size_t)f.i * g->slot_cap, m.d_recv + (size_t)f.i * g->world * g->slot_cap,
-                           f.bytes, ncclUint8, m.comm, m.comm_stream));
+  uint8_t* part = own_part(g, m, f);
+  gsk::launch_copy_word(m.comm_stream, (uint32_t*)(part + f.bgr_part) + gsk::kFootSticky, m.d_sticky);
+  // in place: sendbuff == recvbuff + rank * sendcount
+  GS_NCCL(rccl().AllGather(part, m.d_recv + (size_t)f.i * g->world * g->slot_cap, f.bytes, ncclUint8, m.comm,
+                           m.comm_stream));
   return GS_OK;
 }
 
@@ -602,8 +619,9 @@ int enqueue(Group* g) {
       for (Member& o : g->mem) GS_HIP(hipStreamWaitEvent(m.comm_stream, o.ev_render[i], 0));
       uint8_t* recv = m.d_recv + (size_t)i * g->world * g->slot_cap;
       for (const Member& o : g->mem) {
-        GS_HIP(hipMemcpyAsync(recv + (size_t)o.rank * f.bytes, o.d_send + (size_t)i * g->slot_cap, f.bytes,
-                              hipMemcpyDeviceToDevice, m.comm_stream));
+        if (&o != &m)  // (m's own band is already in place)
+          GS_HIP(hipMemcpyAsync(recv + (size_t)o.rank * f.bytes, own_part(g, o, f), f.bytes,
+                                hipMemcpyDeviceToDevice, m.comm_stream));
         // o's sticky bit into its gathered footer (this stream has waited for
         // every frame of o up to this one)
         GS_HIP(hipMemcpyAsync((uint32_t*)(recv + (size_t)o.rank * f.bytes + f.bgr_part) + gsk::kFootSticky,
@@ -667,7 +685,6 @@ void release(Group* g) {
     for (gs_renderer* c : m.slot) gsr::destroy(c);
     m.slot.clear();
     if (m.comm) (void)rccl().CommDestroy(m.comm);
-    if (m.d_send) (void)hipFree(m.d_send);
     if (m.d_recv) (void)hipFree(m.d_recv);
     if (m.d_sticky) (void)hipFree(m.d_sticky);
     for (hipEvent_t e : m.ev_render)
@@ -795,9 +812,6 @@ int create(const gs_gaussian3d* gs, size_t n, const gs_config* cfg, const gs_com
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&m.comm_stream, hipStreamNonBlocking)) != hipSuccess)
       return fail(gsr::hip_fail(e, "hipStreamCreate(comm)"));
-    if ((e = hipMalloc(&m.d_send, (size_t)g->F * g->slot_cap)) != hipSuccess)
-      return fail(gsr::hip_fail(e, "hipMalloc(all-gather send)"));
-    gsr::poison(m.d_send, (size_t)g->F * g->slot_cap, "send");
     if ((e = hipMalloc(&m.d_recv, (size_t)g->F * g->world * g->slot_cap)) != hipSuccess)
       return fail(gsr::hip_fail(e, "hipMalloc(all-gather recv)"));
     if ((e = hipMemset(m.d_recv, 0, (size_t)g->F * g->world * g->slot_cap)) != hipSuccess)

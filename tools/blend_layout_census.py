@@ -68,7 +68,11 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--tiles", type=int, default=400)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=64, help="records staged per batch (a lane walks its whole batch mask)")
+    ap.add_argument("--layouts", default="px1,px2,px4,px4h")
     a = ap.parse_args()
+    B = a.batch
+    lay = {k: LAYOUTS[k] for k in a.layouts.split(",")}
     W, H = 1920, 1080
     g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=a.n, seed=1, sh_degree=0)))
     view, proj = camera.headless(bb, W, H)
@@ -84,7 +88,7 @@ def main():
     pick = np.unique(np.concatenate([rng.choice(T, a.tiles // 2, replace=False),
                                      rng.choice(T, a.tiles // 2, p=lens / lens.sum()),
                                      [int(np.argmax(lens))]]))
-    acc = {k: dict(iters=0, staged=0, evals=0, useful=0, batches=0, tail=0) for k in LAYOUTS}
+    acc = {k: dict(iters=0, staged=0, evals=0, useful=0, batches=0, tail=0) for k in lay}
     for t in pick:
         ids = lst[ts[t]:ts[t + 1]]
         tx, ty = t % tx_n, t // tx_n
@@ -116,7 +120,7 @@ def main():
         done_at = np.where(valid, done_at, -1)
         rec = np.arange(L)[:, None]
         live = inb & (rec <= done_at[None])  # useful evaluations: box holds it, pixel live
-        for name, waves in LAYOUTS.items():
+        for name, waves in lay.items():
             A = acc[name]
             for lanes in waves:
                 P = np.array(lanes)  # [64, k]
@@ -125,12 +129,12 @@ def main():
                 union = inb[:, P].any(axis=2)  # [L, 64]
                 walk = union & (rec <= lane_end[None])
                 wave_iters = 0
-                for base in range(0, L, 64):
+                for base in range(0, L, B):
                     if base > lane_end.max():
                         break
                     A["batches"] += 1
-                    A["staged"] += min(64, L - base)
-                    w = walk[base:base + 64]
+                    A["staged"] += min(B, L - base)
+                    w = walk[base:base + B]
                     it = int(w.sum(axis=0).max())
                     wave_iters += it
                     A["evals"] += int(w.sum()) * k
@@ -141,8 +145,9 @@ def main():
     print(f"tiles sampled {pick.size} of {T}, longest list {lens.max()} (sampled)")
     print(f"{'layout':6s} {'waves':>6s} {'iters':>10s} {'staged':>10s} {'batches':>9s} {'evals':>11s} "
           f"{'useful':>11s} {'use/eval':>8s} {'tail iters':>10s}")
+    print(f"batch {B}")
     for name, A in acc.items():
-        nw = len(LAYOUTS[name]) * T
+        nw = len(lay[name]) * T
         print(f"{name:6s} {nw:6d} {A['iters'] * scale:10.0f} {A['staged'] * scale:10.0f} {A['batches'] * scale:9.0f} "
               f"{A['evals'] * scale:11.0f} {A['useful'] * scale:11.0f} {A['useful'] / max(A['evals'], 1):8.3f} "
               f"{A['tail']:10d}")
