@@ -69,6 +69,9 @@ def parse():
                     help="frames of the isolated one-in-flight pass that times each kernel "
                     "(stage HIP events) for the kernel table and the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prewarm-ms", type=float, default=0.0,
+                    help="untimed frames for this long before the --warmup steps (the GPU's clocks ramp "
+                    "over the first ~100 frames after the copy-peak measurement; reported in the line)")
     ap.add_argument("--copy-peak-s", type=float, default=0.06,
                     help="seconds of 2 GiB copies for peak_measured (before the timed region; >= 6 copies)")
     ap.add_argument("--split", type=int, default=0,
@@ -411,6 +414,15 @@ def main():
     # the achievable copy rate, measured before the timed region (its copies
     # keep the GPU busy for ~0.1 s, as a long run's first frames would)
     peak_measured = measured_copy_peak(torch, a.copy_peak_s)
+    # pre-warm: untimed frames for --prewarm-ms (beyond the --warmup steps),
+    # reported in the line
+    prewarm = {"ms": a.prewarm_ms, "frames": 0}
+    if a.prewarm_ms > 0:
+        tp = time.perf_counter()
+        while (time.perf_counter() - tp) * 1e3 < a.prewarm_ms:
+            for _ in range(8):
+                one_frame()
+            prewarm["frames"] += 8
     for _ in range(a.warmup):
         one_frame()
     sync_all()
@@ -691,6 +703,7 @@ def main():
             "n_gpus": ngpu,
             "steps": a.steps,
             "warmup": a.warmup,
+            "prewarm": prewarm,
             "ms_per_step": round(ms_per_step, 4),
             "frame_latency_ms": latency_ms,
             "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / a.steps, 4),

@@ -463,9 +463,12 @@ int member_gather_rccl(Group* g, Member& m, const FrameCmd& f) {
   // one has finished its render here (the gathers run in frame order)
   uint8_t* part = own_part(g, m, f);
   gsk::launch_copy_word(m.comm_stream, (uint32_t*)(part + f.bgr_part) + gsk::kFootSticky, m.d_sticky);
-  // in place: sendbuff == recvbuff + rank * sendcount
-  GS_NCCL(rccl().AllGather(part, m.d_recv + (size_t)f.i * g->world * g->slot_cap, f.bytes, ncclUint8, m.comm,
-                           m.comm_stream));
+  // in place: sendbuff == recvbuff + rank * sendcount.  A world of one has
+  // nothing to exchange: its band is the whole gathered slot already (RCCL's
+  // one-rank all-gather still copied the 6.2-MB slot onto itself, 14 us)
+  if (g->world > 1)
+    GS_NCCL(rccl().AllGather(part, m.d_recv + (size_t)f.i * g->world * g->slot_cap, f.bytes, ncclUint8, m.comm,
+                             m.comm_stream));
   return GS_OK;
 }
 
