@@ -695,7 +695,7 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
     // entirely writes only its V (0): count and emit skip such blocks
     // without reading their rectangles, so nothing else needs writing.
     // (A test of per-block bounds before any Gaussian is read was slower:
-    // DESIGN.md §8, "block bounds")
+    // DESIGN.md §4, "Tried and dropped", the two round-2 block-test entries)
     bool culled = false;
     if (i < fp.n) {
       // one 16-B load (the mean and the largest scale) instead of two
