@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch", type=int, default=64, help="records staged per batch (a lane walks its whole batch mask)")
     ap.add_argument("--layouts", default="px1,px2,px4,px4h")
+    ap.add_argument("--no-lane-exit", action="store_true",
+                    help="lanes stop only at batch boundaries (no per-record saturation exit)")
     a = ap.parse_args()
     B = a.batch
     lay = {k: LAYOUTS[k] for k in a.layouts.split(",")}
@@ -127,7 +129,12 @@ def main():
                 k = P.shape[1]
                 lane_end = done_at[P].max(axis=1)  # the lane walks until its last pixel breaks
                 union = inb[:, P].any(axis=2)  # [L, 64]
-                walk = union & (rec <= lane_end[None])
+                if a.no_lane_exit:
+                    # live at the batch start: the lane walks its whole batch mask
+                    bstart = (rec // B) * B
+                    walk = union & (bstart <= lane_end[None])
+                else:
+                    walk = union & (rec <= lane_end[None])
                 wave_iters = 0
                 for base in range(0, L, B):
                     if base > lane_end.max():
