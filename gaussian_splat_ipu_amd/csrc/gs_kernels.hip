@@ -1576,6 +1576,7 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
   const int g0 = c * fp.chunk_size;
   const int g1 = min(fp.n, g0 + fp.chunk_size);
   const uint32_t* row = b.chunk_off + (size_t)c * T;
+  const int lane = threadIdx.x & 63;
   if (fp.emit_wide) {
     // one u32 cursor per tile, seeded with the chunk's first slot of the
     // tile: a single LDS atomic returns the pair's final position
@@ -1615,12 +1616,32 @@ __global__ __launch_bounds__(1024) void gs_emit_chunk_kernel(FrameParams fp, Buf
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint32_t x0 = r[k].x & 0xFFFFu, x1 = r[k].x >> 16, y0 = r[k].y & 0xFFFFu, y1 = r[k].y >> 16;
+        // Runs of equal rectangles among the wave's lanes (consecutive
+        // Gaussians in Morton order often bin into the same tiles, as in the
+        // count): the run's first lane reserves the run's slots in each tile
+        // with one LDS atomic and the run's lanes take consecutive slots
+        // (coalesced 8-B stores).  The run's lanes share the rectangle, so
+        // they walk the tile loops in step and the leader's reservation is
+        // read in the same iteration.  Slots within a tile are the atomics'
+        // order either way; the sort sets the list order.
+        const uint2 rk = r[k];
+        const uint32_t px = (uint32_t)__shfl_up((int)rk.x, 1, 64), py = (uint32_t)__shfl_up((int)rk.y, 1, 64);
+        const bool start = lane == 0 || rk.x != px || rk.y != py;
+        const unsigned long long st = ballot64(start);
+        const unsigned long long upto = lane == 63 ? st : (st & ((2ull << lane) - 1ull));
+        const int leader = 63 - __builtin_clzll(upto);  // (bit 0 is always set)
+        const unsigned long long above = lane == 63 ? 0ull : (st & ~((2ull << lane) - 1ull));
+        const uint32_t len = above ? (uint32_t)(__builtin_ctzll(above) - lane) : (uint32_t)(64 - lane);
+        const uint32_t rank = (uint32_t)(lane - leader);
+        const uint32_t x0 = rk.x & 0xFFFFu, x1 = rk.x >> 16, y0 = rk.y & 0xFFFFu, y1 = rk.y >> 16;
         const unsigned long long key = ((unsigned long long)dk[k] << 32) | (uint32_t)(i0 + k * 1024 + (int)threadIdx.x);
         if (x0 > x1) continue;
         for (uint32_t y = y0; y <= y1; ++y)
           for (uint32_t x = x0; x <= x1; ++x) {
-            const uint32_t pos = atomicAdd(&cnt[y * fp.tiles_x + x], 1u);
+            uint32_t base = 0u;
+            if (start) base = atomicAdd(&cnt[y * fp.tiles_x + x], len);
+            base = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)base);
+            const uint32_t pos = base + rank;
             if (pos < fp.pair_cap) b.pairs[pos] = key;
           }
       }
