@@ -62,17 +62,6 @@
 #ifndef GS_BLEND_PX4
 #define GS_BLEND_PX4 0
 #endif
-// record prefetch depth (batches) of the one-pixel blend in row bands (the
-// in-blend sort's kernel) and in the lazy lists' continuation
-#ifndef GS_BAND_DEPTH
-#define GS_BAND_DEPTH 1
-#endif
-#ifndef GS_CONT_DEPTH
-#define GS_CONT_DEPTH 1
-#endif
-#ifndef GS_BAND_WPE  // waves per SIMD the in-blend sort's kernel is built for
-#define GS_BAND_WPE GS_BLEND_WPE
-#endif
 #ifndef GS_PX4_WPG
 #define GS_PX4_WPG 4
 #endif
@@ -3007,11 +2996,7 @@ __device__ __forceinline__ int blend_tile_of(const FrameParams& fp, const Buffer
 
 // wid = the wave's (tile slot, 8x8 block) item; st: the wave's LDS staging
 // of one batch (3 x 64 float4)
-// DEPTH: batches of records in registers ahead of the one being staged (1;
-// 2 for the row bands' and the continuation's launches, whose few waves walk
-// long lists and wait on each batch's gather, and whose occupancy is not set
-// by registers)
-template <int BQW, bool HWEXP, int DEPTH = 1>
+template <int BQW, bool HWEXP>
 __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
@@ -3118,15 +3103,9 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
     r2 = make_float4(c.z, c.w, t.z, t.w);
   };
   float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
-  float4 c0 = a0, c1 = a0, c2 = a0;  // (DEPTH 2) the batch after a's
   uint32_t g_cur = load_idx(lane);
   if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
-  uint32_t g_c = 0xFFFFFFFFu;
-  if constexpr (DEPTH == 2) {
-    g_c = load_idx(64 + lane);
-    if (g_c != 0xFFFFFFFFu) load_rec(g_c, c0, c1, c2);
-  }
-  uint32_t g_next = load_idx(64 * DEPTH + lane);
+  uint32_t g_next = load_idx(64 + lane);
 
   uint32_t staged = 0;  // records staged (profiled frames)
   for (uint32_t base = 0; base < L; base += 64) {
@@ -3145,21 +3124,11 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
     // the batch takes the clamp-free exponential when every record's pcut
     // is >= -80 (wave-uniform, so the record loop carries no per-step test)
     const bool fast = ballot64(rok && !(a1.y >= -80.0f)) == 0ull;
-    // prefetch: records DEPTH batches ahead, indices one batch beyond them
-    if constexpr (DEPTH == 2) {
-      g_cur = g_c;
-      a0 = c0;
-      a1 = c1;
-      a2 = c2;
-      g_c = g_next;
-      c0 = c1 = c2 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (g_c != 0xFFFFFFFFu) load_rec(g_c, c0, c1, c2);
-    } else {
-      g_cur = g_next;
-      a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
-    }
-    g_next = load_idx(base + 64 * (DEPTH + 1) + lane);
+    // prefetch the next batch
+    g_cur = g_next;
+    a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
+    g_next = load_idx(base + 128 + lane);
 
     // m = the batch's records whose box touches this lane's quad (bit k =
     // record k).  Blocks: per quad column / row one ballot, then each lane
@@ -3689,7 +3658,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
 // of code (the CU pair's instruction cache is shared with the other frames'
 // kernels: config 3 7 703 -> 7 839 frames/s, blend 79.2 -> 76.7 us without it)
 template <bool HWEXP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BAND_WPE, 8))) void gs_blend_sort_kernel(FrameParams fp, Buffers b) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WPE, 8))) void gs_blend_sort_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrBlend);
   __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -3699,7 +3668,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BAND_WPE
   // the list's stores are done (s_waitcnt in the barrier) before any wave
   // reads it, and the sort's LDS is free for the staging
   __syncthreads();
-  blend_wave<4, HWEXP, GS_BAND_DEPTH>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
+  blend_wave<4, HWEXP>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
 }
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
@@ -3715,7 +3684,7 @@ __global__ __launch_bounds__(256) void gs_blend_cont_kernel(FrameParams fp, Buff
   const int wave = GS_BLEND_WPG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nblk = (int)((b.counters[0] * (uint32_t)fp.chunks_per_tile + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x)
-    blend_wave<4, HWEXP, GS_CONT_DEPTH>(fp, b, blk * GS_BLEND_WPG + wave, s_rec[wave]);
+    blend_wave<4, HWEXP>(fp, b, blk * GS_BLEND_WPG + wave, s_rec[wave]);
 }
 
 
