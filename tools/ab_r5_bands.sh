@@ -6,6 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${TAG:-abb}
 mkdir -p $O
+shopt -s nullglob
 libs="base"
 for d in tmp_ab/*/; do libs="$libs $(basename $d)"; done
 path() { [ "$1" = base ] && echo "$PWD/gaussian_splat_ipu_amd/lib/libgsplat.so" || echo "$PWD/tmp_ab/$1/libgsplat.so"; }
