@@ -17,8 +17,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _newest_profiles() -> str:
     """The newest round's profile directory holding the round-end PMC summaries
-    (profiles/r0N_*/pmc_c3.json)."""
-    ds = sorted(os.path.dirname(p) for p in glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_c3.json")))
+    of configs 3 and 5 (profiles/r0N_*/pmc_c3.json, pmc_c5.json)."""
+    ds = sorted(os.path.dirname(p) for p in glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_c3.json"))
+                if os.path.exists(os.path.join(os.path.dirname(p), "pmc_c5.json")))
+    # (the newest round first; within a round, its end set over earlier ones)
+    ds.sort(key=lambda d: (os.path.basename(d)[:3], os.path.basename(d).endswith(("final", "end"))))
     return ds[-1] if ds else os.path.join(ROOT, "profiles", "r04_final")
 
 
