@@ -69,6 +69,9 @@ def parse():
                     help="frames of the isolated one-in-flight pass that times each kernel "
                     "(stage HIP events) for the kernel table and the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-frames", type=int, default=120,
+                    help="frames of the end-to-end pass after the timed region (each frame's BGR8 read back to "
+                    "pinned host memory; reported as end_to_end, never as value); 0 = skip")
     ap.add_argument("--prewarm-ms", type=float, default=0.0,
                     help="untimed frames for this long before the --warmup steps (the GPU's clocks ramp "
                     "over the first ~100 frames after the copy-peak measurement; reported in the line)")
@@ -464,6 +467,37 @@ def main():
         d1 = frame_digest(r.get_frame_buffer())
         check.append(d0 == d1)
     frame_check = {"renderers": len(check), "last_timed_frame_equals_blocking_render": all(check)}
+
+    # end to end with the readback (the reference's frame timer
+    # includes getFrameBuffer, splat.cpp:246-268): every frame's BGR8 copied
+    # to pinned host memory (gs_read_bgr8) while the next frames render.
+    # Reported beside the headline, never as `value` (one GPU, one process)
+    e2e = None
+    if not group and a.e2e_frames > 0:
+        nbytes = H * W * 3
+        hosts = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(2)]
+        F_ = len(R)
+        sync_all()
+        torch.cuda.synchronize()
+        te0 = time.perf_counter()
+        for k in range(a.e2e_frames + F_ - 1):
+            if k < a.e2e_frames:
+                r = R[k % F_]
+                if a.config5:
+                    r.set_view_wire(views[k % 120])
+                r.execute_async()
+            j = k - (F_ - 1)  # the oldest frame in flight: read it back
+            if j >= 0:
+                R[j % F_].get_frame_buffer(out=hosts[j % 2])
+        te1 = time.perf_counter()
+        e2e = {
+            "frames_per_s": round(a.e2e_frames / (te1 - te0), 1),
+            "frames": a.e2e_frames,
+            "readback": f"BGR8 {H}x{W}x3 ({nbytes} B) per frame into pinned host memory (gs_read_bgr8), "
+                        f"{F_} frames in flight",
+            "note": "PCIe-inclusive rate, the reference's timing definition (its timer includes the readback); "
+                    "not the headline value (inputs and outputs resident in HBM)",
+        }
     st = s.stats()
     bands = s.bands() if group else None
 
@@ -729,6 +763,7 @@ def main():
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "n_pairs_binned", "max_list", "n_tiles",
                                          "n_big_tiles", "paths", "bin_global")},
             "frame_check": frame_check,
+            "end_to_end": e2e,
             "kernels": kern,
             "roofline": roofline,
             "cpu_baseline": cpu,

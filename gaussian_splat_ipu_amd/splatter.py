@@ -245,9 +245,14 @@ class GpuSplatter:
         check(lib().gs_sync(self._h), "gs_sync")
 
     # ------------------------------------------------------------ outputs
-    def get_frame_buffer(self) -> np.ndarray:
-        """IpuSplatter::getFrameBuffer: rows x W x 3 uint8 BGR, row-major."""
-        out = np.empty((self.band_rows, self.fb.width, 3), np.uint8)
+    def get_frame_buffer(self, out: np.ndarray | None = None) -> np.ndarray:
+        """IpuSplatter::getFrameBuffer: rows x W x 3 uint8 BGR, row-major
+        (into ``out`` when given: a C-contiguous uint8 array of at least that
+        many bytes, e.g. pinned host memory)."""
+        if out is None:
+            out = np.empty((self.band_rows, self.fb.width, 3), np.uint8)
+        elif not (out.dtype == np.uint8 and out.flags.c_contiguous and out.nbytes >= self.band_rows * self.fb.width * 3):
+            raise ValueError("get_frame_buffer: out must be a C-contiguous uint8 array of rows x W x 3 bytes")
         check(lib().gs_read_bgr8(self._h, out.ctypes.data_as(C.POINTER(C.c_uint8)), out.nbytes), "gs_read_bgr8")
         return out
 

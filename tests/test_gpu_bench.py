@@ -51,3 +51,15 @@ def test_bench_refuses_more_gpus_than_visible():
                          capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert out.returncode != 0
     assert "HIP device" in out.stderr
+
+
+def test_bench_single_gpu_line_reports_end_to_end():
+    """The one-GPU line: `value` from the device-resident frames, and beside it
+    the end-to-end rate with every frame's BGR8 read back to pinned host
+    memory (the reference's timer includes its readback)."""
+    d = _bench("--n", "200000", "--steps", "60", "--warmup", "20", "--profile-frames", "6", "--e2e-frames", "30",
+               "--no-cpu-baseline")
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    e = d["end_to_end"]
+    assert e["frames"] == 30 and 0 < e["frames_per_s"]
+    assert d["roofline"]["traffic_kernels"] == ["gs_blend_px2"]
