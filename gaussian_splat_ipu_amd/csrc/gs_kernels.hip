@@ -39,39 +39,9 @@
 #ifndef GS_SORT_UNROLL_E
 #define GS_SORT_UNROLL_E 4
 #endif
-#ifndef GS_BLEND_PIXEL_MASKS
-#define GS_BLEND_PIXEL_MASKS 1
-#endif
-// blend: per-lane masks read back from a VGPR table of the ballots with
-// ds_bpermute (1) or selected from them with compare / select chains (0)
-#ifndef GS_BLEND_PERMUTE_MASKS
-#define GS_BLEND_PERMUTE_MASKS 1
-#endif
-// two-pixel blend: both pixels' decisions before either update branch (1),
-// or one pixel's composite after the other's (0)
-#ifndef GS_PX2_INTERLEAVE
-#define GS_PX2_INTERLEAVE 1
-#endif
 // two-pixel blend: waves per workgroup (2 = one tile, 4 = two tiles)
 #ifndef GS_PX2_WPG
 #define GS_PX2_WPG 4
-#endif
-// whole-frame blend of 16x16 tiles: 1 = four pixels (a 2x2 quad) per lane,
-// one wave per tile (each tile's records gathered and staged once); 0 = two
-// pixels per lane, two waves per tile
-#ifndef GS_BLEND_PX4
-#define GS_BLEND_PX4 0
-#endif
-#ifndef GS_PX4_WPG
-#define GS_PX4_WPG 4
-#endif
-#ifndef GS_PX4_WPE  // > 0: at least this many waves per SIMD (caps the VGPRs)
-#define GS_PX4_WPE 0
-#endif
-#if GS_PX4_WPE > 0
-#define GS_PX4_ATTR __attribute__((amdgpu_waves_per_eu(GS_PX4_WPE, 8)))
-#else
-#define GS_PX4_ATTR
 #endif
 // the one-pixel blend kernels' fewest waves per SIMD (8: at most 64 VGPRs)
 #ifndef GS_BLEND_WPE
@@ -3135,17 +3105,16 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
     // ANDs its column's and row's masks; quad runs: one ballot per quad.
     unsigned long long m = 0ull;
     if constexpr (BQW != 0) {
-      // Quad (or pixel, GS_BLEND_PIXEL_MASKS) columns and rows of the block:
-      // one ballot per column / row, each a single unsigned compare
-      // (c - lo <= span; a lane without a record never matches), then each
-      // lane selects its column's and row's masks and ANDs them.
-      constexpr int SH = GS_BLEND_PIXEL_MASKS ? 0 : 1;
-      constexpr int NC = (2 * bqw) >> SH, NR = (32 / bqw) >> SH;
+      // Pixel columns and rows of the block: one ballot per column / row,
+      // each a single unsigned compare (c - lo <= span; a lane without a
+      // record never matches), then each lane selects its column's and row's
+      // masks and ANDs them.  (Quad-granular masks: round 2, 21 % more
+      // evaluations.)
+      constexpr int NC = 2 * bqw, NR = 32 / bqw;
       const int bx = tile_x0 + q_x, by = tile_y0 + q_y;
-      const int xlo = rok ? (rx0 - bx) >> SH : 0x40000000, xsp = rok ? ((rx1 - bx) >> SH) - xlo : 0;
-      const int ylo = rok ? (ry0 - by) >> SH : 0x40000000, ysp = rok ? ((ry1 - by) >> SH) - ylo : 0;
-      const int mycol = (lx - q_x) >> SH, myrow = (ly - q_y) >> SH;
-#if GS_BLEND_PERMUTE_MASKS
+      const int xlo = rok ? rx0 - bx : 0x40000000, xsp = rok ? (rx1 - bx) - xlo : 0;
+      const int ylo = rok ? ry0 - by : 0x40000000, ysp = rok ? (ry1 - by) - ylo : 0;
+      const int mycol = lx - q_x, myrow = ly - q_y;
       // the ballots (wave-uniform) go into one VGPR, lanes 2c / 2c + 1 for
       // column c and 2 (NC + w) / + 1 for row w; each lane then reads its
       // column's and row's words back with ds_bpermute (4 crossbar reads
@@ -3160,20 +3129,6 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
       const uint32_t mrl = (uint32_t)__builtin_amdgcn_ds_bpermute(ar, (int)tab);
       const uint32_t mrh = (uint32_t)__builtin_amdgcn_ds_bpermute(ar + 4, (int)tab);
       m = ((unsigned long long)(mch & mrh) << 32) | (unsigned long long)(mcl & mrl);
-#else
-      unsigned long long mc = 0ull, mr = 0ull;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const unsigned long long bc = ballot64((uint32_t)(c - xlo) <= (uint32_t)xsp);
-        mc = (mycol == c) ? bc : mc;
-      }
-#pragma unroll
-      for (int w = 0; w < NR; ++w) {
-        const unsigned long long br = ballot64((uint32_t)(w - ylo) <= (uint32_t)ysp);
-        mr = (myrow == w) ? br : mr;
-      }
-      m = mc & mr;
-#endif
     } else {
       int cx = q_x, cy = q_y;
 #pragma unroll
@@ -3269,7 +3224,6 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
     const float pb = (h0 * dxb * dxb + h2dd) - k1 * dxb * dy;
     const float ea = EXP == kExpHw ? gs_expf_hw(pa) : (EXP == kExpInRange ? gs_expf_inrange(pa) : gs_expf(pa));
     const float eb = EXP == kExpHw ? gs_expf_hw(pb) : (EXP == kExpInRange ? gs_expf_inrange(pb) : gs_expf(pb));
-#if GS_PX2_INTERLEAVE
     // Both pixels' decisions (blend_composite's, same operations) before
     // either update branch: the compiler otherwise sinks pixel b's whole
     // chain below pixel a's update branch, so the two chains ran one after
@@ -3299,10 +3253,6 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
     }
     qa.done = qa.done || brka;
     qb.done = qb.done || brkb;
-#else
-    blend_composite(qa, pa, ea, a1, a2, true);
-    blend_composite(qb, pb, eb, a1, a2, true);
-#endif
     m = (qa.done && qb.done) ? 0ull : m;
   }
 }
@@ -3409,192 +3359,6 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
   }
   if (va) store_pixel(fp, b, px, tyb * fp.tile_h + ly, qa);
   if (vb) store_pixel(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
-}
-
-// Four pixels per lane (GS_BLEND_PX4; FrameParams::blend_px2 whole frames of
-// 16x16 tiles): one wave per tile, lane l the 2x2 quad at (2 (l & 7),
-// 2 (l >> 3)), one mask per quad (8 quad-column and 8 quad-row ballots of
-// the record's alpha box), so each tile's records are gathered and staged
-// once.  Per record the lane shares the LDS reads and the mask walk, the two
-// columns' (h0 dx) dx and k1 dx and the two rows' (h2 dy) dy, and runs each
-// pixel's power, exponential and composite in renderTile's order
-// (codelets.cpp:385-411): the products are those of the one-pixel step, so
-// every pixel's bits are unchanged.  A record is also evaluated for the
-// quad's pixels its box misses: power < pcut there, so it is skipped exactly
-// as the reference skips it.
-struct Px4 {
-  float T[4];
-  float c0[4], c1[4], c2[4], c3[4];  // r, g, b, a accumulators
-  bool done[4];
-};
-
-template <int EXP>
-__device__ __forceinline__ void blend_records_px4(Px4& q, float x0, float y0, float4 (*st)[64], uint32_t w,
-                                                  uint32_t h) {
-  unsigned long long m = ((unsigned long long)h << 32) | w;
-  while (m) {
-    const int ja = __builtin_ctzll(m);
-    m &= m - 1ull;
-    const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
-    asm volatile("" ::"v"(a1.z), "v"(a1.w), "v"(a2.x), "v"(a2.y));  // all loads issued up front
-    const float h0 = a0.z, h2 = a0.w, k1 = a1.x;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
-    const float pcut = a1.y, op = a2.y;
-    const float dx0 = a0.x - x0, dx1 = a0.x - (x0 + 1.0f);
-    const float dy0 = a0.y - y0, dy1 = a0.y - (y0 + 1.0f);
-    const float hx0 = h0 * dx0 * dx0, hx1 = h0 * dx1 * dx1;
-    const float hy0 = h2 * dy0 * dy0, hy1 = h2 * dy1 * dy1;
-    const float kx0 = k1 * dx0, kx1 = k1 * dx1;
-    float pw[4];
-    pw[0] = (hx0 + hy0) - kx0 * dy0;
-    pw[1] = (hx1 + hy0) - kx1 * dy0;
-    pw[2] = (hx0 + hy1) - kx0 * dy1;
-    pw[3] = (hx1 + hy1) - kx1 * dy1;
-    float al[4], tt[4];
-    bool upd[4], brk[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float e = EXP == kExpHw ? gs_expf_hw(pw[k]) : (EXP == kExpInRange ? gs_expf_inrange(pw[k]) : gs_expf(pw[k]));
-      const float v = op * e;
-      al[k] = (v < 0.99f) ? v : 0.99f;  // glm::min(0.99f, v)
-      tt[k] = q.T[k] * (1.0f - al[k]);
-    }
-    asm volatile("" ::"v"(al[0]), "v"(al[1]), "v"(al[2]), "v"(al[3]));
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      // power > 0: skipped; power < pcut: alpha < 1/255 guaranteed (`continue`)
-      const bool hit = !q.done[k] && !(pw[k] > 0.0f) && !(pw[k] < pcut) && !(al[k] < 1.0f / 255.0f);
-      brk[k] = hit && tt[k] < 0.0001f;  // break (codelets.cpp:406-408)
-      upd[k] = hit && !brk[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (__builtin_expect(upd[k], 0)) {
-        q.c0[k] = q.c0[k] + (a1.z * al[k]) * q.T[k];  // colour += gCont * alpha * T
-        q.c1[k] = q.c1[k] + (a1.w * al[k]) * q.T[k];
-        q.c2[k] = q.c2[k] + (a2.x * al[k]) * q.T[k];
-        q.c3[k] = q.c3[k] + (op * al[k]) * q.T[k];
-        q.T[k] = tt[k];
-      }
-      q.done[k] = q.done[k] || brk[k];
-    }
-    m = (q.done[0] && q.done[1] && q.done[2] && q.done[3]) ? 0ull : m;
-  }
-}
-
-// wid = the tile slot (longest lists first); st: the wave's LDS staging
-template <bool HWEXP>
-__device__ __forceinline__ void blend_wave_px4(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
-  const int slot = wid;
-  if (slot >= fp.n_tiles) return;
-  int tile;
-  uint32_t s, L;
-  if (fp.blend_seg) {  // the slot's tile and list segment in one load (the sort launch's)
-    const uint4 sg = b.blend_seg[slot];
-    tile = (int)sg.x;
-    s = sg.y;
-    L = sg.z;
-  } else {
-    tile = blend_tile_of(fp, b, slot);
-    tile_segment(fp, b, tile, s, L);
-  }
-  const int lane = threadIdx.x & 63;
-  const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
-  const int tile_x0 = tx * fp.tile_w;
-  const int tile_y0 = (fp.band_ty0 + tyb * fp.band_stride) * fp.tile_h;
-  const int qc = lane & 7, qr = lane >> 3;  // quad column, quad row
-  const int px = tile_x0 + 2 * qc, py = tile_y0 + 2 * qr;
-  Px4 q;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    q.T[k] = 1.0f;
-    q.c0[k] = q.c1[k] = q.c2[k] = q.c3[k] = 0.0f;
-    q.done[k] = !(px + (k & 1) < fp.width && py + (k >> 1) < fp.height);
-  }
-  const float x0 = (float)px, y0 = (float)py;
-
-  const uint32_t* __restrict__ list = b.list + s;
-  auto load_idx = [&](uint32_t k) -> uint32_t { return blend_idx(fp, list, L, k); };
-  const float4* __restrict__ ccol = (fp.sh_degree >= 0 && b.sh) ? b.col_out : b.colour;
-  auto load_rec = [&](uint32_t g, float4& r0, float4& r1, float4& r2) {
-    const float4* qq = b.rec + 2 * (size_t)g;
-    r0 = qq[0];
-    const float4 t = qq[1];    // k1 pcut boxx boxy
-    const float4 c = ccol[g];  // r g b opacity
-    r1 = make_float4(t.x, t.y, c.x, c.y);
-    r2 = make_float4(c.z, c.w, t.z, t.w);
-  };
-  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
-  uint32_t g_cur = load_idx(lane);
-  if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
-  uint32_t g_next = load_idx(64 + lane);
-
-  auto all_done = [&]() { return q.done[0] && q.done[1] && q.done[2] && q.done[3]; };
-  uint32_t staged = 0;
-  for (uint32_t base = 0; base < L; base += 64) {
-    if (ballot64(!all_done()) == 0ull) break;
-    staged += min(64u, L - base);
-    const bool have = g_cur != 0xFFFFFFFFu;
-    st[0][lane] = make_float4(a0.x, a0.y, -0.5f * a0.z, -0.5f * a0.w);
-    st[1][lane] = a1;
-    st[2][lane] = a2;
-    const uint32_t boxx = __float_as_uint(a2.z), boxy = __float_as_uint(a2.w);
-    const int rx0 = (int)(boxx << 16) >> 16, rx1 = (int)boxx >> 16;
-    const int ry0 = (int)(boxy << 16) >> 16, ry1 = (int)boxy >> 16;
-    const bool rok = have && !(a2.y == 0.0f) && rx0 <= rx1 && ry0 <= ry1;
-    const bool fast = ballot64(rok && !(a1.y >= -80.0f)) == 0ull;
-    g_cur = g_next;
-    a0 = a1 = a2 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g_cur != 0xFFFFFFFFu) load_rec(g_cur, a0, a1, a2);
-    g_next = load_idx(base + 128 + lane);
-    // quad column c meets the box iff floor((rx0 - tx0) / 2) <= c <=
-    // floor((rx1 - tx0) / 2); quad rows likewise
-    const int xlo = rok ? (rx0 - tile_x0) >> 1 : 0x40000000, xsp = rok ? ((rx1 - tile_x0) >> 1) - xlo : 0;
-    const int ylo = rok ? (ry0 - tile_y0) >> 1 : 0x40000000, ysp = rok ? ((ry1 - tile_y0) >> 1) - ylo : 0;
-    uint32_t tab = 0u;
-    BallotTab<0, 0, 8>::run(tab, xlo, xsp);
-    BallotTab<8, 0, 8>::run(tab, ylo, ysp);
-    const int ac = 8 * qc, ar = 8 * (8 + qr);
-    const uint32_t mcl = (uint32_t)__builtin_amdgcn_ds_bpermute(ac, (int)tab);
-    const uint32_t mch = (uint32_t)__builtin_amdgcn_ds_bpermute(ac + 4, (int)tab);
-    const uint32_t mrl = (uint32_t)__builtin_amdgcn_ds_bpermute(ar, (int)tab);
-    const uint32_t mrh = (uint32_t)__builtin_amdgcn_ds_bpermute(ar + 4, (int)tab);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const bool fin = all_done();
-    const uint32_t m_lo = fin ? 0u : (mcl & mrl), m_hi = fin ? 0u : (mch & mrh);
-    if (HWEXP) {
-      blend_records_px4<kExpHw>(q, x0, y0, st, m_lo, m_hi);
-    } else if (fast) {
-      blend_records_px4<kExpInRange>(q, x0, y0, st, m_lo, m_hi);
-    } else {
-      blend_records_px4<kExpExact>(q, x0, y0, st, m_lo, m_hi);
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  // profiled frames: the staged records at this tile's wave slot 0 (1..3 unused)
-  if (fp.count_records && lane == 0) {
-    b.blend_count[4 * slot] = staged;
-    b.blend_count[4 * slot + 1] = b.blend_count[4 * slot + 2] = b.blend_count[4 * slot + 3] = 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int x = px + (k & 1), y = py + (k >> 1);
-    if (x < fp.width && y < fp.height) {
-      Px o;
-      o.c01 = f32x2{q.c0[k], q.c1[k]};
-      o.c23 = f32x2{q.c2[k], q.c3[k]};
-      store_pixel(fp, b, x, tyb * fp.tile_h + 2 * qr + (k >> 1), o);
-    }
-  }
-}
-
-template <bool HWEXP>
-__global__ __launch_bounds__(64 * GS_PX4_WPG) GS_PX4_ATTR void gs_blend_px4_kernel(FrameParams fp, Buffers b) {
-  GS_PROBE_SCOPE(kPrBlend);
-  __shared__ float4 s_rec[GS_PX4_WPG][3][64];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  blend_wave_px4<HWEXP>(fp, b, blockIdx.x * GS_PX4_WPG + wave, s_rec[wave]);
 }
 
 template <bool HWEXP>
@@ -3803,14 +3567,6 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   const unsigned grid = (unsigned)((waves + GS_BLEND_WPG - 1) / GS_BLEND_WPG);
   const unsigned block = 64 * GS_BLEND_WPG;
   if (fp.blend_px2) {  // (16x16 tiles, whole frames without lazy lists: two waves per tile)
-#if GS_BLEND_PX4
-    const unsigned g4 = (unsigned)((fp.n_tiles + GS_PX4_WPG - 1) / GS_PX4_WPG);
-    if (fp.fast_exp)
-      gs_blend_px4_kernel<true><<<g4, 64 * GS_PX4_WPG, 0, s>>>(fp, b);
-    else
-      gs_blend_px4_kernel<false><<<g4, 64 * GS_PX4_WPG, 0, s>>>(fp, b);
-    return;
-#endif
     const unsigned g2 = (unsigned)((2L * fp.n_tiles + GS_PX2_WPG - 1) / GS_PX2_WPG);
     if (fp.fast_exp)
       gs_blend_px2_kernel<true><<<g2, 64 * GS_PX2_WPG, 0, s>>>(fp, b);
