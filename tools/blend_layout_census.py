@@ -70,6 +70,11 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch", type=int, default=64, help="records staged per batch (a lane walks its whole batch mask)")
     ap.add_argument("--layouts", default="px1,px2,px4,px4h")
+    ap.add_argument("--mask", choices=["box", "ellipse", "rows"], default="box",
+                    help="a lane's records: the integer alpha box meets a pixel (the kernels), or the pixel "
+                         "lies in the record's pcut ellipse (an ideal per-pixel mask), or 'rows': the "
+                         "ellipse's x-extent over groups of --row-group pixel rows")
+    ap.add_argument("--row-group", type=int, default=4)
     ap.add_argument("--no-lane-exit", action="store_true",
                     help="lanes stop only at batch boundaries (no per-record saturation exit)")
     a = ap.parse_args()
@@ -122,13 +127,23 @@ def main():
         done_at = np.where(valid, done_at, -1)
         rec = np.arange(L)[:, None]
         live = inb & (rec <= done_at[None])  # useful evaluations: box holds it, pixel live
+        msk = inb & (power >= pcut_all[ids][:, None]) if a.mask == "ellipse" else inb
+        if a.mask == "rows":
+            ell = (inb & (power >= pcut_all[ids][:, None])).reshape(L, TW, TW)  # [L, y, x]
+            G = a.row_group
+            eg = ell.reshape(L, TW // G, G, TW).any(axis=2)  # [L, groups, x]: x in the extent of some row
+            xs_ = np.arange(TW)
+            lo = np.where(eg.any(axis=2), np.argmax(eg, axis=2), TW)
+            hi = np.where(eg.any(axis=2), TW - 1 - np.argmax(eg[:, :, ::-1], axis=2), -1)
+            inx = (xs_[None, None, :] >= lo[:, :, None]) & (xs_[None, None, :] <= hi[:, :, None])  # [L, groups, x]
+            msk = inb & np.repeat(inx, G, axis=1).reshape(L, TW * TW)
         for name, waves in lay.items():
             A = acc[name]
             for lanes in waves:
                 P = np.array(lanes)  # [64, k]
                 k = P.shape[1]
                 lane_end = done_at[P].max(axis=1)  # the lane walks until its last pixel breaks
-                union = inb[:, P].any(axis=2)  # [L, 64]
+                union = msk[:, P].any(axis=2)  # [L, 64]
                 if a.no_lane_exit:
                     # live at the batch start: the lane walks its whole batch mask
                     bstart = (rec // B) * B

@@ -1,0 +1,122 @@
+// valu_rate.hip -- measurement helper (not product code): the SIMD's fp32
+// VALU issue rate on gfx950, to price `valu_issue_frac` (bench.py) in cycles
+// per wave64 instruction.  Each wave runs CH independent v_fma_f32 chains
+// (or v_pk_fma_f32 with PK) for ITERS x 16 steps; the grid puts W waves on
+// each of the 1 024 SIMDs (256 CUs x 4).  Reported per configuration:
+// SIMD cycles per wave64 instruction = kernel time x clock / (instructions
+// per SIMD), the clock measured inside the kernel (s_memtime over
+// s_memrealtime, 100 MHz).  Also one dependent chain (CH = 1, W = 1): the
+// dependent-issue latency.
+//   make -C tools/hip valu_rate && tools/hip/valu_rate > out.json
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                        \
+    }                                                                      \
+  } while (0)
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int CH, bool PK>
+__global__ __launch_bounds__(256) void valu_kernel(float* out, unsigned long long* clk, int iters, float s) {
+  unsigned long long t0 = 0, r0 = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  if constexpr (PK) {
+    f2 a[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) a[c] = f2{(float)threadIdx.x * 1e-7f + c, (float)c * 0.5f};
+    const f2 m = f2{s, s * 0.5f}, k = f2{1e-7f, 2e-7f};
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          a[c] = __builtin_elementwise_fma(a[c], m, k);
+          asm volatile("" : "+v"(a[c]));
+        }
+    }
+    float r = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) r += a[c].x + a[c].y;
+    if (r == 12345.678f) out[threadIdx.x] = r;
+  } else {
+    float a[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) a[c] = (float)threadIdx.x * 1e-7f + c;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          a[c] = __builtin_fmaf(a[c], s, 1e-7f);
+          asm volatile("" : "+v"(a[c]));
+        }
+    }
+    float r = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) r += a[c];
+    if (r == 12345.678f) out[threadIdx.x] = r;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - t0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+}
+
+template <int CH, bool PK>
+static void run(const char* name, int waves_per_simd, int iters, float* out, unsigned long long* clk, bool first) {
+  const int blocks = 256 * waves_per_simd;  // 4 waves per block: one per SIMD
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) valu_kernel<CH, PK><<<blocks, 256>>>(out, clk, iters, 0.999f);
+  CK(hipDeviceSynchronize());
+  const int reps = 10;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) valu_kernel<CH, PK><<<blocks, 256>>>(out, clk, iters, 0.999f);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long h[2];
+  CK(hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost));
+  const double ghz = h[1] ? (double)h[0] / (double)h[1] * 0.1 : 0.0;  // shader ticks per 10 ns
+  const double t = ms * 1e-3 / reps;
+  // wave64 instructions per SIMD (each of the 1 024 SIMDs runs waves_per_simd waves)
+  const double insts = (double)waves_per_simd * iters * 16 * CH;
+  const double cyc = t * ghz * 1e9 / insts;
+  std::printf("%s{\"op\": \"%s\", \"chains\": %d, \"waves_per_simd\": %d, \"us\": %.2f, \"clock_ghz\": %.3f, "
+              "\"simd_cycles_per_inst\": %.3f}",
+              first ? "" : ",\n", name, CH, waves_per_simd, t * 1e6, ghz, cyc);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
+int main() {
+  float* out;
+  unsigned long long* clk;
+  CK(hipMalloc(&out, 4096));
+  CK(hipMalloc(&clk, 16));
+  const int iters = 2048;
+  std::printf("[\n");
+  bool first = true;
+  for (int w : {1, 2, 4, 8}) {
+    run<8, false>("v_fma_f32", w, iters, out, clk, first);
+    first = false;
+  }
+  for (int w : {1, 2, 4, 8}) run<2, false>("v_fma_f32", w, iters, out, clk, false);
+  run<1, false>("v_fma_f32", 1, iters, out, clk, false);
+  for (int w : {1, 4, 8}) run<8, true>("v_pk_fma_f32", w, iters, out, clk, false);
+  std::printf("\n]\n");
+  return 0;
+}
