@@ -8,8 +8,8 @@ O=gpurun_out/${TAG:-ab}
 mkdir -p $O
 shopt -s nullglob
 libs="base"
-for d in tmp_ab/*/; do libs="$libs $(basename $d)"; done
-path() { [ "$1" = base ] && echo "$PWD/gaussian_splat_ipu_amd/lib/libgsplat.so" || echo "$PWD/tmp_ab/$1/libgsplat.so"; }
+for d in ${ABDIR:-tmp_ab}/*/; do libs="$libs $(basename $d)"; done
+path() { [ "$1" = base ] && echo "$PWD/gaussian_splat_ipu_amd/lib/libgsplat.so" || echo "$PWD/${ABDIR:-tmp_ab}/$1/libgsplat.so"; }
 if [ -z "$NO_TESTS" ]; then
 for n in $libs; do
   [ "$n" = base ] && continue

@@ -8,9 +8,9 @@ O=gpurun_out/${TAG:-abb}
 mkdir -p $O
 shopt -s nullglob
 libs="base"
-for d in tmp_ab/*/; do libs="$libs $(basename $d)"; done
-path() { [ "$1" = base ] && echo "$PWD/gaussian_splat_ipu_amd/lib/libgsplat.so" || echo "$PWD/tmp_ab/$1/libgsplat.so"; }
-for n in $libs; do
+for d in ${ABDIR:-tmp_ab}/*/; do libs="$libs $(basename $d)"; done
+path() { [ "$1" = base ] && echo "$PWD/gaussian_splat_ipu_amd/lib/libgsplat.so" || echo "$PWD/${ABDIR:-tmp_ab}/$1/libgsplat.so"; }
+[ -z "$NO_TESTS" ] && for n in $libs; do
   [ "$n" = base ] && continue
   GSPLAT_LIB=$(path $n) timeout -k 10 600 python -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "band or lazy or group or orbit or config5 or large_tile or equal_depths" > $O/test_$n.log 2>&1
   rc=$?
