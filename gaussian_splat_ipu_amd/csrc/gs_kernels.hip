@@ -3293,14 +3293,30 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
 // its records are staged twice instead of four times.  A record is also
 // evaluated for the lane's pixel whose column it does not meet: power <
 // pcut there, so it is skipped exactly as the reference skips it.
+// GS_LANES builds: a lane's record steps, live-pixel evaluations, those whose
+// record's alpha box holds the pixel, and hits
+struct LaneCount {
+  uint32_t steps = 0, evals = 0, box = 0, hits = 0;
+};
+
 template <int EXP>
-__device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[64], uint32_t w, uint32_t h) {
+__device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[64], uint32_t w, uint32_t h,
+                                                  LaneCount& lc) {
   unsigned long long m = ((unsigned long long)h << 32) | w;
   while (m) {
     const int ja = __builtin_ctzll(m);
     m &= m - 1ull;
     const float4 a0 = st[0][ja], a1 = st[1][ja], a2 = st[2][ja];
     asm volatile("" ::"v"(a1.z), "v"(a1.w), "v"(a2.x), "v"(a2.y));  // all loads issued up front
+    if constexpr (GS_LANES != 0) {
+      const uint32_t bx = __float_as_uint(a2.z), by = __float_as_uint(a2.w);
+      const int x0 = (int)(bx << 16) >> 16, x1 = (int)bx >> 16, y0 = (int)(by << 16) >> 16, y1 = (int)by >> 16;
+      const int xa = (int)qa.p.x, xb = (int)qb.p.x, y = (int)qa.p.y;
+      const bool yin = y0 <= y && y <= y1;
+      lc.steps += 1u;
+      lc.evals += (qa.done ? 0u : 1u) + (qb.done ? 0u : 1u);
+      lc.box += ((!qa.done && yin && x0 <= xa && xa <= x1) ? 1u : 0u) + ((!qb.done && yin && x0 <= xb && xb <= x1) ? 1u : 0u);
+    }
     const float h0 = a0.z, h2 = a0.w, k1 = a1.x;  // h0 = -0.5 k0, h2 = -0.5 k2 (staged)
     const float dy = a0.y - qa.p.y;               // (one row: the same dy for both pixels)
     const float h2dd = h2 * dy * dy;
@@ -3322,6 +3338,7 @@ __device__ __forceinline__ void blend_records_px2(Px& qa, Px& qb, float4 (*st)[6
     const bool hitb = !qb.done && !(pb > 0.0f) && !(pb < pcut) && !(alb < 1.0f / 255.0f);
     const bool brka = hita && tta < 0.0001f, brkb = hitb && ttb < 0.0001f;
     const bool upda = hita && !brka, updb = hitb && !brkb;
+    if constexpr (GS_LANES != 0) lc.hits += (hita ? 1u : 0u) + (hitb ? 1u : 0u);
     if (__builtin_expect(upda, 0)) {
       qa.c01.x = qa.c01.x + (a1.z * ala) * qa.T;
       qa.c01.y = qa.c01.y + (a1.w * ala) * qa.T;
@@ -3393,6 +3410,8 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
   uint32_t g_next = load_idx(64 + lane);
 
   uint32_t staged = 0;
+  LaneCount lc;
+  uint32_t wave_steps = 0, batches = 0;  // (GS_LANES builds)
   for (uint32_t base = 0; base < L; base += 64) {
     if (ballot64(!(qa.done && qb.done)) == 0ull) break;
     staged += min(64u, L - base);
@@ -3427,14 +3446,37 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const bool both = qa.done && qb.done;
     const uint32_t m_lo = both ? 0u : (mcl & mrl), m_hi = both ? 0u : (mch & mrh);
+    const uint32_t steps0 = lc.steps;
     if (HWEXP) {
-      blend_records_px2<kExpHw>(qa, qb, st, m_lo, m_hi);
+      blend_records_px2<kExpHw>(qa, qb, st, m_lo, m_hi, lc);
     } else if (fast) {
-      blend_records_px2<kExpInRange>(qa, qb, st, m_lo, m_hi);
+      blend_records_px2<kExpInRange>(qa, qb, st, m_lo, m_hi, lc);
     } else {
-      blend_records_px2<kExpExact>(qa, qb, st, m_lo, m_hi);
+      blend_records_px2<kExpExact>(qa, qb, st, m_lo, m_hi, lc);
+    }
+    if constexpr (GS_LANES != 0) {  // the batch's wave steps: its longest lane walk
+      uint32_t d = lc.steps - steps0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) d = max(d, (uint32_t)__shfl_xor((int)d, o, 64));
+      wave_steps += d;
+      ++batches;
     }
     __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (GS_LANES != 0) {
+    if (b.lanes) {
+      unsigned long long v[4] = {lc.steps, lc.evals, lc.box, lc.hits};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v[k] += (unsigned long long)__shfl_xor((long long)v[k], o, 64);
+      if (lane == 0) {
+        atomicAdd(&b.lanes[0], (unsigned long long)wave_steps);
+        for (int k = 0; k < 4; ++k) atomicAdd(&b.lanes[1 + k], v[k]);
+        atomicAdd(&b.lanes[5], (unsigned long long)batches);
+        atomicAdd(&b.lanes[6], 1ull);
+      }
+    }
   }
   // profiled frames: the staged records at this tile's wave slots 0 / 1 (2 / 3
   // unused: zeroed, the host takes the tile's largest)

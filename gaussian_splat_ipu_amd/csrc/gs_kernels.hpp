@@ -18,6 +18,14 @@ namespace gsk {
 // their atomics over them -- one address per kernel serialised 15 k waves'
 // atomics and stretched the projection 15x)
 constexpr int kProbeFrames = 512, kProbeKernels = 16, kProbeSlots = 256;
+// Blend lane-count builds (-DGS_LANES=1, tools/blend_lanes.py; never the
+// default library): the two-pixel blend adds, per frame, its wave record
+// steps, lane record steps, pixel evaluations (live pixels), the evaluations
+// whose record's alpha box holds the pixel, and the hits (updates and
+// breaks) into Buffers::lanes
+#ifndef GS_LANES
+#define GS_LANES 0
+#endif
 
 struct FrameParams {
   float mvp[16];      // proj * view, glm column-major (codelets.cpp:443)
@@ -89,6 +97,7 @@ struct FrameParams {
 // Device workspace of one renderer.
 struct Buffers {
   unsigned long long* probe;      // (GS_PROBE builds, GSPLAT_PROBE_FILE) [kProbeFrames][kProbeKernels][kProbeSlots][2] or null
+  unsigned long long* lanes;      // (GS_LANES builds, GSPLAT_LANES_FILE) [8] blend counters or null
   // scene (SoA of the 64-B Gaussian3D record, ipu_geometry.hpp:305-311)
   const float4* mean;       // x y z w
   const float4* colour;     // r g b opacity

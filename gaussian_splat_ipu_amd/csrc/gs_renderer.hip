@@ -174,12 +174,32 @@ void dump_probe(gs_renderer* r) {
   }
 }
 
+#if GS_LANES
+// lane-count builds: the blend counters of this renderer's frames appended to
+// GSPLAT_LANES_FILE (tools/blend_lanes.py): 8 u64
+void dump_lanes(gs_renderer* r) {
+  const char* path = std::getenv("GSPLAT_LANES_FILE");
+  unsigned long long h[8] = {};
+  if (!path || hipMemcpy(h, r->buf.lanes, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return;
+  if (FILE* f = std::fopen(path, "ab")) {
+    std::fwrite(h, 8, 8, f);
+    std::fclose(f);
+  }
+}
+#endif
+
 void release(gs_renderer* r) {
   if (!r) return;
   (void)hipSetDevice(r->device);
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->d_scene && r->owns_scene) (void)hipFree(r->d_scene);
   if (r->d_probe) dump_probe(r);
+#if GS_LANES
+  if (r->buf.lanes) {
+    dump_lanes(r);
+    (void)hipFree(r->buf.lanes);
+  }
+#endif
   for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg,
                   r->d_probe})
     if (p) (void)hipFree(p);
@@ -1080,6 +1100,12 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       return fail(hip_fail(e, "hipMemcpy(probe)"));
     r->buf.probe = (unsigned long long*)r->d_probe;
   }
+#if GS_LANES
+  if (std::getenv("GSPLAT_LANES_FILE") && !lattice) {
+    if ((e = hipMalloc(&r->buf.lanes, 64)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(lanes)"));
+    if ((e = hipMemset(r->buf.lanes, 0, 64)) != hipSuccess) return fail(hip_fail(e, "hipMemset(lanes)"));
+  }
+#endif
   *out = r;
   return GS_OK;
 }
