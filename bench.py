@@ -99,6 +99,8 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=30.0,
                     help="cap on the CPU baseline's timed frames (fewer frames if one takes longer)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--cpi-json", default=os.path.join(ROOT, "profiles", "valu_cpi.json"),
+                    help="VALU cycles per instruction of the kernels' hot loops (tools/valu_cpi.py)")
     return ap.parse_args()
 
 
@@ -146,6 +148,20 @@ def stage_pmc(stage: str, paths: int, kernels: dict, bin_global: bool = False):
     hbm = sum(n * kernels[k]["hbm_bytes_per_launch"] for k, n in ks)
     valu = sum(n * kernels[k].get("SQ_INSTS_VALU", 0.0) for k, n in ks)
     return hbm, valu, []
+
+
+def stage_valu_cycles(stage: str, paths: int, kernels: dict, cpi: dict, bin_global: bool = False):
+    """(SIMD cycles of VALU issue per frame of a stage, the cpi used per
+    kernel), or (None, missing names): each launched kernel's PMC
+    SQ_INSTS_VALU x its hot loop's cycles per instruction (tools/valu_cpi.py:
+    the MI355X issues a wave64 v_mul / v_add in ~2 cycles, a v_fma / v_cmp /
+    v_cvt / v_pk_* in ~4, v_exp in ~8, tools/hip/valu_rate.hip)."""
+    ks = stage_kernels(stage, paths, bin_global)
+    missing = [k for k, _ in ks if k not in kernels or k not in cpi]
+    if missing or not ks:
+        return None, missing
+    cyc = sum(n * kernels[k].get("SQ_INSTS_VALU", 0.0) * cpi[k]["cpi"] for k, n in ks)
+    return cyc, {k: cpi[k]["cpi"] for k, _ in ks}
 
 
 def measured_copy_peak(torch, min_s: float = 0.06) -> float:
@@ -591,10 +607,16 @@ def main():
 
     paths = int(st_view.get("paths", 0))
     bin_global = bool(st_view.get("bin_global", 0))
+    cpi = {}
+    if os.path.exists(a.cpi_json):
+        try:
+            cpi = json.load(open(a.cpi_json))
+        except Exception:
+            cpi = {}
 
     def roof(name):
         k = kern[name]
-        pmc = valu = None
+        pmc = valu = valu_cpi = valu_note = None
         launched = [x for x, _ in stage_kernels(name, paths, bin_global)]
         if pm is None:
             note = f"no PMC summary for {pmc_key} in {os.path.relpath(a.pmc_json, ROOT)}"
@@ -605,10 +627,15 @@ def main():
             else:
                 note = None
                 pmc = int(hb)
-                # VALU issue-slot fraction beside the HBM fraction (SURVEY §8 d):
-                # wave64 VALU instructions x 2 cycles over 1024 SIMDs x 2.4 GHz
-                if vi:
-                    valu = round(min(1.0, vi * 2.0 / (1024 * 2.4e9 * k["avg_ms"] * 1e-3)), 3)
+                # VALU pipe fraction beside the HBM fraction (SURVEY §8 d): the
+                # stage's wave64 VALU instructions x their hot loops' measured
+                # cycles per instruction over 1024 SIMDs x 2.4 GHz x the launch
+                cyc, used = stage_valu_cycles(name, paths, pm.get("kernels", {}), cpi, bin_global)
+                if cyc is not None:
+                    valu = round(min(1.0, cyc / (1024 * 2.4e9 * k["avg_ms"] * 1e-3)), 3)
+                    valu_cpi = used
+                elif vi:
+                    valu_note = f"no measured VALU cost for {', '.join(used)} in {os.path.relpath(a.cpi_json, ROOT)}"
         ach = k["alg_GBps"]
         out = {
             "kernel": name,
@@ -623,9 +650,12 @@ def main():
             if k["avg_ms"] > 0 else None,
             "avg_launch_ms": k["avg_ms"],
             "valu_issue_frac": valu,
+            "valu_cpi": valu_cpi,
         }
         if note:
             out["traffic_note"] = note
+        if valu_note:
+            out["valu_note"] = valu_note
         return out
 
     rd = roof(dom)
@@ -649,6 +679,10 @@ def main():
                               "record = list entry + 32-B record + 16-B colour)",
         "avg_launch_ms": rd["avg_launch_ms"],
         "valu_issue_frac": rd["valu_issue_frac"],
+        "valu_cpi": rd["valu_cpi"],
+        "valu_model": "SQ_INSTS_VALU of the launched kernels x their hot loops' SIMD cycles per wave64 instruction "
+                      "(tools/valu_cpi.py from the measured per-instruction costs, tools/hip/valu_rate.hip: "
+                      "v_mul/v_add 2, v_fma/v_cmp/v_cvt/v_pk 4, v_exp 8) over 1024 SIMDs x 2.4 GHz x the launch",
         "traffic_model": "PMC HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) and VALU of the kernels this stage launched in "
                          "the timed frames (gs_frame_stats.paths -> bench.stage_kernels), per launch x launches per "
                          "frame; null with traffic_note when the summary lacks one of them",

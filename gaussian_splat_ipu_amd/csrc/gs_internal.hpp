@@ -120,7 +120,6 @@ struct gs_renderer {
   size_t bcount_words = 0;
   bool last_counted = false;   // the last enqueued frame counted its blend records
   uint64_t frame_seq = 0;
-  uint32_t proj_seq = 0;  // projections launched (FrameParams::block_parity)
   gsr::ProfileSlot ring[gsr::kProfileRing];
   int ring_head = 0;
   double k_ms[GS_K_COUNT] = {0};

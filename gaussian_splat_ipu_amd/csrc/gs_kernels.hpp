@@ -46,9 +46,6 @@ struct FrameParams {
   int band_rows;      // pixel rows of this band's output
   int band_cull;      // skip Gaussians whose extent bound misses the band (GS_FLAG_BAND_CULL)
   float wnorm2;       // >= squared Frobenius norm of the mvp's upper 3x3 (band cull bound)
-  int block_list;     // (band_cull) the projection runs only the 256-Gaussian blocks that
-                      //   gs_block_list_kernel could not prove outside the band
-  int block_parity;   // which of the two block counters this projection appends to / reads
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
   int chunks_per_tile;  // blend waves per tile (16 pixel quads each)
@@ -105,9 +102,6 @@ struct Buffers {
   const float4* scale_gid;  // sx sy sz gid
   const float4* cull;       // band cull: mean xyz + largest log-scale (NaN: empty slot, inf: never culled)
   const float4* mean_op;    // mean xyz + opacity (FrameParams::mean_w1: every mean's w is 1)
-  const float4* block_bounds;  // [2 x ceil(n / 256)] per 256-Gaussian block (device order): the box
-                               //   of its means (lo xyz, 0 | hi xyz, largest log-scale; +inf: the
-                               //   block is never culled)
   // device order: record i is the input Gaussian perm[i] (3D Morton order by
   // default); the depth sort breaks ties by the input index, as the reference
   const uint32_t* perm;     // [n] device index -> input index
@@ -158,8 +152,6 @@ struct Buffers {
                             //   small | medium << 8 | big << 16 counts, max length;
                             //   then the reference list-length sum (lo, hi), 0, 0
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
-  uint32_t* block_list;     // [ceil(n / 256)] FrameParams::block_list: the blocks to project
-  uint32_t* block_count;    // [2] their count, by block_parity (the list kernel zeroes the other)
   uint32_t* host_counters;  // mapped pinned mirror of counters[16] + tile_count[n_tiles],
                             //   written by the chunked scan (no D2H copy per frame)
   uint32_t* host_sticky;    // mapped pinned word: set by the scan of any frame that

@@ -30,10 +30,8 @@ namespace {
 // scene allocation: the 64-B records (SoA), the permutation both ways, then
 // the band cull's 16-B records (16-B aligned)
 size_t cull_offset(size_t nn) { return (nn * (64 + 8) + 15) / 16 * 16; }
-// + the band cull's records (16 B) + mean xyz with the opacity (16 B), then
-// the block bounds (32 B per 256-Gaussian block)
-size_t bounds_offset(size_t nn) { return cull_offset(nn) + nn * 32; }
-size_t scene_bytes(size_t nn) { return bounds_offset(nn) + (nn + 255) / 256 * 32; }
+// + the band cull's records (16 B) + mean xyz with the opacity (16 B)
+size_t scene_bytes(size_t nn) { return cull_offset(nn) + nn * 32; }
 }  // namespace
 
 namespace gsr {
@@ -252,8 +250,6 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
-  // the band's projection only over the blocks a per-block bound keeps
-  fp.block_list = fp.band_cull;
   {
     double w2 = 0.0;  // squared Frobenius norm of the upper 3x3 of the mvp, rounded up
     for (int c = 0; c < 3; ++c)
@@ -497,14 +493,6 @@ int enqueue_lattice(gs_renderer* r, const gsk::FrameParams& fp, ProfileSlot* slo
   return GS_OK;
 }
 
-// a projection's block-list counter: the two alternate list launch by list
-// launch on the renderer's stream (each gs_block_list_kernel zeroes the one
-// the previous list launch filled, for the next)
-gsk::FrameParams with_parity(gs_renderer* r, gsk::FrameParams fp) {
-  if (fp.block_list && fp.band_cull) fp.block_parity = (int)(r->proj_seq++ & 1u);
-  return fp;
-}
-
 int enqueue_frame(gs_renderer* r) {
   // several frames may be in flight on the stream; the host mirrors always
   // hold the last one's counters after gs_sync
@@ -536,7 +524,7 @@ int enqueue_frame(gs_renderer* r) {
   if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
     GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, s));
   if (slot) GS_HIP(hipEventRecord(slot->ev[0], s));
-  gsk::launch_project(with_parity(r, fp), r->buf, s);
+  gsk::launch_project(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[1], s));
   gsk::launch_scan(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[2], s));
@@ -877,34 +865,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         w1 = w1 && s[3] == 1.0f;
       }
       r->scene_w1 = w1;
-      // the block bounds of the band cull's block list (gs_block_list_kernel):
-      // per 256 consecutive Gaussians of the device order, the box of their
-      // means and their largest log-scale; +inf when any of them is never
-      // culled by band_culled_fast (an empty slot, w != 1) or has a
-      // non-finite coordinate
-      for (size_t k = 0; k < (nn + 255) / 256; ++k) {
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        bool never = false;
-        for (size_t i = k * 256; i < std::min(n, k * 256 + 256); ++i) {
-          const float* cr = soa + cull_offset(nn) / 4 + 4 * i;
-          if (!(std::isfinite(cr[0]) && std::isfinite(cr[1]) && std::isfinite(cr[2]) && std::isfinite(cr[3]))) {
-            never = true;
-            break;
-          }
-          for (int c = 0; c < 3; ++c) {
-            lo[c] = std::min(lo[c], cr[c]);
-            hi[c] = std::max(hi[c], cr[c]);
-          }
-          hi[3] = std::max(hi[3], cr[3]);
-        }
-        float* bb = soa + bounds_offset(nn) / 4 + 8 * k;
-        for (int c = 0; c < 3; ++c) {
-          bb[c] = lo[c];
-          bb[4 + c] = hi[c];
-        }
-        bb[3] = 0.0f;
-        bb[7] = (never || !(hi[3] > -INFINITY)) ? INFINITY : hi[3];
-      }
       e = hipMemcpy(r->d_scene, soa, scene_bytes(nn), hipMemcpyHostToDevice);
       (void)hipHostFree(soa);
       if (e != hipSuccess) return fail(hip_fail(e, "hipMemcpy(scene)"));
@@ -918,19 +878,16 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
   r->buf.cull = (const float4*)((const char*)r->d_scene + cull_offset(nn));
   r->buf.mean_op = r->buf.cull + nn;
-  r->buf.block_bounds = (const float4*)((const char*)r->d_scene + bounds_offset(nn));
   r->buf.inv_perm = r->buf.perm + nn;
 
   // per Gaussian: 48 B of record (frames: the 32-B record the blend reads and,
   // with gs_set_sh, the 16-B view-dependent colour; the readback: the 48-B
   // record), its 8-B readback tail, 8-B tile rectangle and its alpha-box cut
   // (rect8: 4 B each), 4-B depth key; plus V per project workgroup
-  // and the band cull's block list with its two counters
   const size_t nblk = (nn + 255) / 256;
-  const size_t gauss_bytes = nn * (48 + 8 + 8 + 8 + 4) + nblk * 8 + 8;
-  if ((e = hipMalloc(&r->d_gauss, gauss_bytes)) != hipSuccess)
+  if ((e = hipMalloc(&r->d_gauss, nn * (48 + 8 + 8 + 8 + 4) + nblk * 4)) != hipSuccess)
     return fail(hip_fail(e, "hipMalloc(per-Gaussian)"));
-  poison(r->d_gauss, gauss_bytes, "gauss");
+  poison(r->d_gauss, nn * (48 + 8 + 8 + 8 + 4) + nblk * 4, "gauss");
   r->buf.rec = (float4*)r->d_gauss;
   r->buf.rec_tail = (float2*)((char*)r->d_gauss + nn * 48);
   r->buf.col_out = (float4*)((char*)r->d_gauss + nn * 32);  // (frames: the record region past the 32-B records)
@@ -938,9 +895,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.crect = (uint2*)((char*)r->d_gauss + nn * 64);
   r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
   r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 76);
-  r->buf.block_list = r->buf.block_rendered + nblk;
-  r->buf.block_count = r->buf.block_list + nblk;
-  if ((e = hipMemset(r->buf.block_count, 0, 8)) != hipSuccess) return fail(hip_fail(e, "hipMemset(block counters)"));
 
   const size_t T = (size_t)std::max(r->n_tiles, 1);
   r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
@@ -1249,7 +1203,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
       fp.lazy = 0;
       if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
         GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, r->stream));
-      gsk::launch_project(with_parity(r, fp), bb, r->stream);
+      gsk::launch_project(fp, bb, r->stream);
       gsk::launch_scan(fp, bb, r->stream);
       gsk::launch_emit(fp, bb, r->stream);
       gsk::launch_sort(fp, bb, r->stream);
@@ -1307,7 +1261,7 @@ int read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     fp.full_record = 1;
     fp.rect8 = 0;  // (the readback takes the 16-bit reference rectangle)
     fp.mean_w1 = 0;  // (and the 48-B record with the colour)
-    gsk::launch_project(with_parity(r, fp), r->buf, r->stream);
+    gsk::launch_project(fp, r->buf, r->stream);
     GS_HIP(hipGetLastError());
     GS_HIP(hipStreamSynchronize(r->stream));
     GS_HIP(hipMemcpy(rec.data(), r->buf.rec, r->n * 48, hipMemcpyDeviceToHost));

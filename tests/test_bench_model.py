@@ -158,6 +158,25 @@ def test_stage_kernels_follow_the_frame_paths():
     assert (hb, vi, missing) == (10.0 + 2 * 3.0 + 5.0, 1.0 + 2 * 2.0, [])
 
 
+def test_valu_cycles_weigh_each_kernel_by_its_measured_cost():
+    """The roofline's VALU fraction: each launched kernel's SQ_INSTS_VALU x
+    its hot loop's measured cycles per instruction (profiles/valu_cpi.json,
+    tools/valu_cpi.py), x its launches per frame; a kernel without a measured
+    cost makes it unknown, not a guess."""
+    ks = {"gs_blend_px2": {"hbm_bytes_per_launch": 1.0, "SQ_INSTS_VALU": 100.0}}
+    cyc, used = bench.stage_valu_cycles("blend", C3_PATHS, ks, {"gs_blend_px2": {"cpi": 2.5}})
+    assert (cyc, used) == (250.0, {"gs_blend_px2": 2.5})
+    cyc, missing = bench.stage_valu_cycles("blend", C3_PATHS, ks, {})
+    assert cyc is None and missing == ["gs_blend_px2"]
+    cpi = json.load(open(os.path.join(ROOT, "profiles", "valu_cpi.json")))
+    for k in ("gs_blend_px2", "gs_blend", "gs_blend_sort"):
+        # between the full-rate (v_mul / v_add: 2) and half-rate (v_fma / v_cmp: 4)
+        # costs, and the rates it came from are committed
+        assert 2.0 <= cpi[k]["cpi"] <= 4.0 and cpi[k]["loop_valu"] > 0, k
+    rates = json.load(open(os.path.join(ROOT, "profiles", "r05_valu", "valu_rate.json")))
+    assert any(e["op"] == "v_fma_f32" and e["waves_per_simd"] == 8 for e in rates)
+
+
 @pytest.mark.parametrize("pmc,paths", [("pmc_c3.json", C3_PATHS), ("pmc_c5.json", C5_PATHS)])
 def test_round_pmc_holds_the_default_kernels(pmc, paths):
     """The newest round-end PMC summaries (and profiles/pmc_latest.json, the

@@ -2,7 +2,8 @@
 (device = 3D Morton order) gs_block_list_kernel's per-block bound keeps for
 each row band, and a soundness check of that bound against the oracle's
 rectangles (no Gaussian of a culled block may have a tile row in the band).
-The bound is restated here in float64 exactly as gs_kernels.hip block_culled.
+The bound is restated in float64 as the (measured and dropped)
+gs_block_list_kernel had it.
 
   python tools/block_cull_census.py [--n 1000000] [--bands 8]
 """

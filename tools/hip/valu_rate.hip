@@ -73,6 +73,82 @@ __global__ __launch_bounds__(256) void valu_kernel(float* out, unsigned long lon
   }
 }
 
+// one instruction (inline asm, operand 0 = the chain register, 1 = a second
+// VGPR, 2 = an SGPR) on 8 independent chains per step
+#define OPK(NAME, ASM)                                                                 \
+  __global__ __launch_bounds__(256) void op_##NAME(float* out, unsigned long long* clk, int iters, float s) { \
+    float a[8];                                                                        \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) a[c] = (float)threadIdx.x * 1e-7f + c; \
+    const float bb = s * 0.5f;                                                         \
+    for (int i = 0; i < iters; ++i) {                                                  \
+      _Pragma("unroll") for (int u = 0; u < 16; ++u)                                   \
+      _Pragma("unroll") for (int c = 0; c < 8; ++c) asm volatile(ASM : "+v"(a[c]) : "v"(bb), "s"(s) : "vcc"); \
+    }                                                                                  \
+    float r = 0.f;                                                                     \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) r += a[c];                           \
+    if (r == 12345.678f) out[threadIdx.x] = r;                                         \
+  }
+OPK(v_mul_f32, "v_mul_f32 %0, %0, %1")
+OPK(v_add_u32, "v_add_u32 %0, %0, %1")
+OPK(v_and_b32, "v_and_b32 %0, %0, %1")
+OPK(v_min_f32, "v_min_f32 %0, %0, %1")
+OPK(v_mov_b32, "v_mov_b32 %0, %1")
+OPK(v_rndne_f32, "v_rndne_f32 %0, %0")
+OPK(v_cvt_i32_f32, "v_cvt_i32_f32 %0, %0")
+OPK(v_ldexp_f32, "v_ldexp_f32 %0, %0, %1")
+OPK(v_ffbl_b32, "v_ffbl_b32 %0, %0")
+OPK(v_cmp_lt_f32, "v_cmp_lt_f32 vcc, %0, %1")
+OPK(v_exp_f32, "v_exp_f32 %0, %0")
+OPK(v_sub_f32, "v_sub_f32 %0, %0, %1")
+OPK(v_lshlrev_b32, "v_lshlrev_b32 %0, 3, %0")
+OPK(v_or_b32, "v_or_b32 %0, %0, %1")
+OPK(v_bfe_u32, "v_bfe_u32 %0, %0, 3, 9")
+OPK(v_max_f32, "v_max_f32 %0, %0, %1")
+OPK(v_mul_lo_u32, "v_mul_lo_u32 %0, %0, %1")
+OPK(v_cvt_f32_u32, "v_cvt_f32_u32 %0, %0")
+OPK(v_sqrt_f32, "v_sqrt_f32 %0, %0")
+OPK(v_rcp_f32, "v_rcp_f32 %0, %0")
+OPK(v_mad_u32_u24, "v_mad_u32_u24 %0, %0, %1, %0")
+OPK(v_fmac_f32, "v_fmac_f32 %0, %1, %1")
+OPK(v_min_u32, "v_min_u32 %0, %0, %1")
+OPK(v_lshl_add_u32, "v_lshl_add_u32 %0, %0, 4, %1")
+__global__ __launch_bounds__(256) void op_v_cndmask_b32(float* out, unsigned long long* clk, int iters, float s) {
+  float a[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) a[c] = (float)threadIdx.x * 1e-7f + c;
+  const float bb = s * 0.5f;
+  const unsigned long long mask = (unsigned long long)iters * 0x9E3779B97F4A7C15ull;  // a loop-invariant SGPR pair
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[c]) : "v"(bb), "s"(mask));
+  }
+  float r = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) r += a[c];
+  if (r == 12345.678f) out[threadIdx.x] = r;
+}
+
+// packed / 64-bit operations on a register pair per chain
+#define OPK2(NAME, ASM)                                                                \
+  __global__ __launch_bounds__(256) void op_##NAME(float* out, unsigned long long* clk, int iters, float s) { \
+    f2 a[8];                                                                           \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) a[c] = f2{(float)threadIdx.x * 1e-7f + c, 0.5f * c}; \
+    const f2 bb = f2{s * 0.5f, s * 0.25f};                                             \
+    for (int i = 0; i < iters; ++i) {                                                  \
+      _Pragma("unroll") for (int u = 0; u < 16; ++u)                                   \
+      _Pragma("unroll") for (int c = 0; c < 8; ++c) asm volatile(ASM : "+v"(a[c]) : "v"(bb)); \
+    }                                                                                  \
+    float r = 0.f;                                                                     \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) r += a[c].x + a[c].y;                \
+    if (r == 12345.678f) out[threadIdx.x] = r;                                         \
+  }
+OPK2(v_pk_mul_f32, "v_pk_mul_f32 %0, %0, %1")
+OPK2(v_pk_add_f32, "v_pk_add_f32 %0, %0, %1")
+OPK2(v_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1")
+OPK2(v_cmp_eq_u64, "v_cmp_eq_u64 s[0:1], %0, %1")
+
 template <int CH, bool PK>
 static void run(const char* name, int waves_per_simd, int iters, float* out, unsigned long long* clk, bool first) {
   const int blocks = 256 * waves_per_simd;  // 4 waves per block: one per SIMD
@@ -102,6 +178,27 @@ static void run(const char* name, int waves_per_simd, int iters, float* out, uns
   CK(hipEventDestroy(e1));
 }
 
+static void run_op(const char* name, void (*k)(float*, unsigned long long*, int, float), float* out,
+                   unsigned long long* clk) {
+  const int w = 8, iters = 1024, blocks = 256 * w;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, clk, iters, 0.999f);
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, clk, iters, 0.999f);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double t = ms * 1e-3 / 5, insts = (double)w * iters * 16 * 8;
+  std::printf(",\n{\"op\": \"%s\", \"chains\": 8, \"waves_per_simd\": %d, \"us\": %.2f, "
+              "\"simd_cycles_per_inst_at_2.4GHz\": %.3f}", name, w, t * 1e6, t * 2.4e9 / insts);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
 int main() {
   float* out;
   unsigned long long* clk;
@@ -117,6 +214,36 @@ int main() {
   for (int w : {1, 2, 4, 8}) run<2, false>("v_fma_f32", w, iters, out, clk, false);
   run<1, false>("v_fma_f32", 1, iters, out, clk, false);
   for (int w : {1, 4, 8}) run<8, true>("v_pk_fma_f32", w, iters, out, clk, false);
+#define RUN_OP(N) run_op(#N, op_##N, out, clk)
+  RUN_OP(v_mul_f32);
+  RUN_OP(v_add_u32);
+  RUN_OP(v_and_b32);
+  RUN_OP(v_min_f32);
+  RUN_OP(v_mov_b32);
+  RUN_OP(v_rndne_f32);
+  RUN_OP(v_cvt_i32_f32);
+  RUN_OP(v_ldexp_f32);
+  RUN_OP(v_ffbl_b32);
+  RUN_OP(v_cmp_lt_f32);
+  RUN_OP(v_exp_f32);
+  RUN_OP(v_sub_f32);
+  RUN_OP(v_lshlrev_b32);
+  RUN_OP(v_or_b32);
+  RUN_OP(v_bfe_u32);
+  RUN_OP(v_max_f32);
+  RUN_OP(v_mul_lo_u32);
+  RUN_OP(v_cvt_f32_u32);
+  RUN_OP(v_sqrt_f32);
+  RUN_OP(v_rcp_f32);
+  RUN_OP(v_mad_u32_u24);
+  RUN_OP(v_fmac_f32);
+  RUN_OP(v_min_u32);
+  RUN_OP(v_lshl_add_u32);
+  RUN_OP(v_cndmask_b32);
+  RUN_OP(v_pk_mul_f32);
+  RUN_OP(v_pk_add_f32);
+  RUN_OP(v_lshl_add_u64);
+  RUN_OP(v_cmp_eq_u64);
   std::printf("\n]\n");
   return 0;
 }
