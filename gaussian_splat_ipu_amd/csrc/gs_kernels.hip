@@ -664,8 +664,9 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
     // the cheap band test first; a block of 256 Gaussians that it culls
     // entirely writes only its V (0): count and emit skip such blocks
     // without reading their rectangles, so nothing else needs writing.
-    // (A test of per-block bounds before any Gaussian is read was slower:
-    // DESIGN.md §4, "Tried and dropped", the two round-2 block-test entries)
+    // (Per-block bounds before any Gaussian is read did not pay: DESIGN.md
+    // §4 "Tried and dropped", the two round-2 block-test entries, and §0's
+    // round-5 block list -- a launch projecting only the listed blocks)
     bool culled = false;
     if (i < fp.n) {
       // one 16-B load (the mean and the largest scale) instead of two
