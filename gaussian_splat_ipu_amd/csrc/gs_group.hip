@@ -462,12 +462,11 @@ int member_gather_rccl(Group* g, Member& m, const FrameCmd& f) {
   uint8_t* part = own_part(g, m, f);
   if (g->world == 1) {
     // nothing to exchange: the frame stays on its render stream (a second
-    // stream's event waits cost the one-GPU group ~10 % of its frames).  The
-    // sticky copy waits for the previous frame's render instead, so every
-    // frame up to this one has finished when it reads the word
-    hipStream_t rs = m.slot[f.i]->stream;
-    if (f.prev >= 0) GS_HIP(hipStreamWaitEvent(rs, m.ev_render[f.prev], 0));
-    gsk::launch_copy_word(rs, (uint32_t*)(part + f.bgr_part) + gsk::kFootSticky, m.d_sticky);
+    // stream's event waits cost the one-GPU group ~10 % of its frames), and
+    // no sticky copy per frame either (a launch and a wait on the previous
+    // frame: 8 079 -> 8 260 frames/s without them) -- with no other rank to
+    // agree with, wait_frames reads the sticky word itself, once per sync
+    (void)part;
     return GS_OK;
   }
   GS_HIP(hipStreamWaitEvent(m.comm_stream, m.ev_render[f.i], 0));
@@ -955,6 +954,13 @@ int wait_frames(Group* g) {
   if (g->last_slot >= 0 && !g->last_read) {
     if ((rc = set_dev(g->mem[0].device)) != GS_OK) return rc;
     if ((rc = copy_footers(g, g->last_slot, g->h_last, nullptr, false)) != GS_OK) return rc;
+    if (g->rccl && g->world == 1) {
+      // (one rank: its sticky word is read here, not copied into every
+      // frame's footer -- member_gather_rccl)
+      uint32_t sticky = 0;
+      GS_HIP(hipMemcpy(&sticky, g->mem[0].d_sticky, 4, hipMemcpyDeviceToHost));
+      g->h_last[gsk::kFootSticky] = sticky;
+    }
     g->last_status = parse_footers(g, g->h_last, g->sinfo[g->last_slot].bounds, true, false);
     g->last_read = true;
   }
