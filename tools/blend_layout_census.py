@@ -75,6 +75,8 @@ def main():
                          "lies in the record's pcut ellipse (an ideal per-pixel mask), or 'rows': the "
                          "ellipse's x-extent over groups of --row-group pixel rows")
     ap.add_argument("--row-group", type=int, default=4)
+    ap.add_argument("--window", type=lambda t: [int(x) for x in t.split(",")], default=[],
+                    help="also cost windows of K staged batches (comma list), lanes running ahead within it")
     ap.add_argument("--no-lane-exit", action="store_true",
                     help="lanes stop only at batch boundaries (no per-record saturation exit)")
     a = ap.parse_args()
@@ -150,6 +152,36 @@ def main():
                     walk = union & (bstart <= lane_end[None])
                 else:
                     walk = union & (rec <= lane_end[None])
+                # (no batch barrier: every lane walks the whole list at its own
+                # pace -- the wave's steps are its slowest lane's total)
+                A.setdefault("free", 0)
+                A["free"] += int(walk.sum(axis=0).max()) if L else 0
+                # a window of K staged batches: each step, every lane with a record
+                # left in the window takes one; when no lane has one left in the
+                # window's first batch, the window slides (the next batch staged)
+                for K in a.window:
+                    key = f"win{K}"
+                    A.setdefault(key, 0)
+                    nb = -(-L // B)
+                    cnt = np.zeros((nb, walk.shape[1]), np.int64)
+                    for bb in range(nb):
+                        cnt[bb] = walk[bb * B:(bb + 1) * B].sum(axis=0)
+                    rem = cnt.copy()
+                    steps = 0
+                    w = 0
+                    while w < nb:
+                        if not rem[w].any():
+                            w += 1
+                            continue
+                        # one step: each lane takes its earliest remaining record in [w, w+K)
+                        hi = min(nb, w + K)
+                        sub = rem[w:hi]
+                        has = sub.any(axis=0)
+                        first = np.argmax(sub > 0, axis=0)
+                        lanes = np.nonzero(has)[0]
+                        rem[w + first[lanes], lanes] -= 1
+                        steps += 1
+                    A[key] += steps
                 wave_iters = 0
                 for base in range(0, L, B):
                     if base > lane_end.max():
@@ -168,6 +200,10 @@ def main():
     print(f"{'layout':6s} {'waves':>6s} {'iters':>10s} {'staged':>10s} {'batches':>9s} {'evals':>11s} "
           f"{'useful':>11s} {'use/eval':>8s} {'tail iters':>10s}")
     print(f"batch {B}")
+    for name, A in acc.items():
+        print(f"{name}: wave steps with a barrier per batch {A['iters'] * scale:.0f}, "
+              f"without (lanes at their own pace) {A.get('free', 0) * scale:.0f}, " +
+              ", ".join(f"window {K}: {A.get(f'win{K}', 0) * scale:.0f}" for K in a.window))
     for name, A in acc.items():
         nw = len(lay[name]) * T
         print(f"{name:6s} {nw:6d} {A['iters'] * scale:10.0f} {A['staged'] * scale:10.0f} {A['batches'] * scale:9.0f} "
