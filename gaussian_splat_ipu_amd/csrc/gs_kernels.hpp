@@ -45,7 +45,6 @@ struct FrameParams {
   int tiles_y;        // tile rows of the whole frame
   int band_rows;      // pixel rows of this band's output
   int band_cull;      // skip Gaussians whose extent bound misses the band (GS_FLAG_BAND_CULL)
-  float wnorm2;       // >= squared Frobenius norm of the mvp's upper 3x3 (band cull bound)
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
   int chunks_per_tile;  // blend waves per tile (16 pixel quads each)

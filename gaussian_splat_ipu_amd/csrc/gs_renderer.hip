@@ -250,12 +250,6 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
-  {
-    double w2 = 0.0;  // squared Frobenius norm of the upper 3x3 of the mvp, rounded up
-    for (int c = 0; c < 3; ++c)
-      for (int rr = 0; rr < 3; ++rr) w2 += (double)fp.mvp[c * 4 + rr] * (double)fp.mvp[c * 4 + rr];
-    fp.wnorm2 = (float)(w2 * 1.0001);
-  }
   fp.n = (int)r->n;
   fp.n_tiles = r->n_tiles;
   // blend: one wave per 16 pixel quads -- an 8x8 or 16x4 pixel block when the
