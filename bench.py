@@ -72,9 +72,10 @@ def parse():
     ap.add_argument("--e2e-frames", type=int, default=120,
                     help="frames of the end-to-end pass after the timed region (each frame's BGR8 read back to "
                     "pinned host memory; reported as end_to_end, never as value); 0 = skip")
-    ap.add_argument("--prewarm-ms", type=float, default=0.0,
-                    help="untimed frames for this long before the --warmup steps (the GPU's clocks ramp "
-                    "over the first ~100 frames after the copy-peak measurement; reported in the line)")
+    ap.add_argument("--prewarm-ms", type=float, default=50.0,
+                    help="untimed frames enqueued for this long (host time) before the --warmup steps, "
+                    "reported in the line as prewarm: the GPU's clocks ramp over the first several hundred "
+                    "frames, so without it a 20-frame window measures the ramp (DESIGN §7); 0 = none")
     ap.add_argument("--copy-peak-s", type=float, default=0.06,
                     help="seconds of 2 GiB copies for peak_measured (before the timed region; >= 6 copies)")
     ap.add_argument("--split", type=int, default=0,
@@ -435,7 +436,9 @@ def main():
     peak_measured = measured_copy_peak(torch, a.copy_peak_s)
     # pre-warm: untimed frames for --prewarm-ms (beyond the --warmup steps),
     # reported in the line
-    prewarm = {"ms": a.prewarm_ms, "frames": 0}
+    prewarm = {"ms": a.prewarm_ms, "frames": 0,
+               "note": "untimed frames enqueued before the warm-up steps (the GPU clocks' ramp, DESIGN §7); "
+                       "the timed region is exactly --steps frames between barriers"}
     if a.prewarm_ms > 0:
         tp = time.perf_counter()
         while (time.perf_counter() - tp) * 1e3 < a.prewarm_ms:
