@@ -6,7 +6,7 @@
 # (1/2/4/8) and 5 (1/8).  Outputs under gpurun_out/r5fin.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r5fin
+O=gpurun_out/${TAG:-r5fin}
 mkdir -p $O
 echo "== tests $(date +%T)"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.txt 2>&1
