@@ -235,10 +235,11 @@ def layout_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_con
     big = st["big_pairs"]
     in_blend = (P - big) * 12 if sort_in_blend else 0
     pre, win = st["big_prefix_keys"], st["big_window_keys"]
-    if band:  # band cull: every Gaussian's 16-B cull record, the band's Gaussians in full
-        project = n * 16 + rendered * (48 + 4 + 32) + n * rect_b
-    else:  # mean + opacity, scales + gid, rotation (48 B); rectangles, depth key; the binned records
-        project = n * (48 + rect_b + 4) + rendered * 32
+    if band:  # band cull: every Gaussian's 16-B cull record and scales + gid, the band's Gaussians in
+        # full (mean + opacity, the cached 3D covariance); rectangles, depth key, records
+        project = n * (16 + 16) + rendered * (16 + 36 + 4 + 32) + n * rect_b
+    else:  # mean + opacity, the cached 3D covariance + gid (56 B); rectangles, depth key; the binned records
+        project = n * (56 + rect_b + 4) + rendered * 32
     chunk_matrix = n_chunks * T * 4
     if pre or win:  # lazy big lists: the select reads every big-list key once,
         # writes the prefixes and windows, and the prefixes are sorted into the lists

@@ -75,6 +75,9 @@ struct gs_renderer {
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
   void* d_lazy = nullptr;       // lazy big lists (16x16 tiles): per-tile tables + saved blend waves
   void* d_agg = nullptr;        // aggregated binning: per projection block its tile box and offsets
+  void* d_cov = nullptr;        // the scene's 3D covariances + gids (Buffers::cov3), 40 B per Gaussian
+  float cov_sd = 0.0f;          // ... computed for this fxy[1]
+  bool cov_valid = false;
   void* d_probe = nullptr;      // (GS_PROBE builds, GSPLAT_PROBE_FILE) the kernels' per-frame start / end ring
   int probe_n = 0;              // frames recorded in it
   // GS_FLAG_LATTICE: the lattice-migration emulator's state (gs_lattice.hip)

@@ -307,12 +307,27 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   } else {
     mean = b.mean[i];
   }
-  const float4 sg = b.scale_gid[i];
-  // without the band cull every live Gaussian needs its colour and rotation:
-  // load them with the mean (one memory round trip instead of two)
+  // FrameParams::cov_cache: the 3D covariance (and the gid) from the scene's
+  // cache instead of the rotation and the scales (the band cull still reads
+  // the scales, for its bound)
+  const size_t nn = (size_t)fp.n;
+  float4 sg;
+  float c3[9];
+  if (fp.cov_cache && !fp.band_cull) {
+    sg = make_float4(0.f, 0.f, 0.f, b.cov3[9 * nn + i]);
+  } else {
+    sg = b.scale_gid[i];
+  }
+  // without the band cull every live Gaussian needs its colour and rotation
+  // (or covariance): load them with the mean (one memory round trip)
   if (!fp.band_cull) {
     if (!fp.mean_w1) col = b.colour[i];  // (its w is the opacity, as mean_op's)
-    rot = b.rot[i];
+    if (fp.cov_cache) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) c3[k] = b.cov3[k * nn + i];
+    } else {
+      rot = b.rot[i];
+    }
   }
   // the record: 32 B per Gaussian (48 B with the colour for the readback)
   float4* rec = b.rec + (fp.full_record ? 3 : 2) * (size_t)i;
@@ -370,11 +385,24 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     }
     if (fp.band_cull) {
       if (!fp.mean_w1) col = b.colour[i];  // (its w is the opacity, as mean_op's)
-      rot = b.rot[i];
+      if (fp.cov_cache) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) c3[k] = b.cov3[k * nn + i];
+      } else {
+        rot = b.rot[i];
+      }
     }
     if (fp.sh_degree >= 0 && b.sh) sh_colour(fp, b, i, mean, col);
-    const M3 C3 = cov3d(rot, div_p2<P2>(sg.x, fp.scale_div, fp.inv_sd), div_p2<P2>(sg.y, fp.scale_div, fp.inv_sd),
-                        div_p2<P2>(sg.z, fp.scale_div, fp.inv_sd));
+    M3 C3;
+    if (fp.cov_cache) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) C3.m[c][r] = c3[c * 3 + r];
+    } else {
+      C3 = cov3d(rot, div_p2<P2>(sg.x, fp.scale_div, fp.inv_sd), div_p2<P2>(sg.y, fp.scale_div, fp.inv_sd),
+                 div_p2<P2>(sg.z, fp.scale_div, fp.inv_sd));
+    }
     M3 cov = m3_mul(m3_mul(m3_t(T), m3_t(C3)), T);
     const float a = cov.m[0][0] + 0.3f;
     const float bb = cov.m[0][1];
@@ -3506,6 +3534,39 @@ __global__ __launch_bounds__(64) void gs_copy_word_kernel(uint32_t* dst, const u
 
 void launch_copy_word(hipStream_t s, uint32_t* dst, const uint32_t* src) {
   gs_copy_word_kernel<<<1, 64, 0, s>>>(dst, src);
+}
+
+// FrameParams::cov_cache: ComputeCov3D (ipu_geometry.hpp:315-323, the scales
+// divided by fxy[1], codelets.cpp:463) of every Gaussian, once per fxy[1]:
+// the same function on the same inputs as the projection's, so the same
+// bits.  It depends on the rotation, the scales and fxy[1] only -- never on
+// the camera -- and took ~29 % of the projection's VALU per frame.
+namespace {
+template <bool P2>
+__global__ __launch_bounds__(256) void gs_cov3d_kernel(FrameParams fp, Buffers b) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= fp.n) return;
+  const size_t nn = (size_t)fp.n;
+  const float4 sg = b.scale_gid[i];
+  b.cov3[9 * nn + i] = sg.w;
+  if (sg.w <= 0.0f) return;  // (an empty slot: the projection skips it)
+  const float4 rot = b.rot[i];
+  const M3 C3 = cov3d(rot, div_p2<P2>(sg.x, fp.scale_div, fp.inv_sd), div_p2<P2>(sg.y, fp.scale_div, fp.inv_sd),
+                      div_p2<P2>(sg.z, fp.scale_div, fp.inv_sd));
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) b.cov3[(size_t)(c * 3 + r) * nn + i] = C3.m[c][r];
+}
+}  // namespace
+
+void launch_cov3d(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (fp.n == 0) return;
+  const int nb = (fp.n + 255) / 256;
+  if (fp.pow2)
+    gs_cov3d_kernel<true><<<nb, 256, 0, s>>>(fp, b);
+  else
+    gs_cov3d_kernel<false><<<nb, 256, 0, s>>>(fp, b);
 }
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {

@@ -84,6 +84,9 @@ struct FrameParams {
   int fast_exp;       // blend: hardware exp2 (GS_FLAG_FAST_EXP, within a stated tolerance)
   int sh_degree;      // > 0: view-dependent colour from spherical harmonics (gs_set_sh)
   float campos[3];    // camera position in the scene's (prepared) frame, for the SH direction
+  int cov_cache;      // Buffers::cov3 holds every Gaussian's 3D covariance for this frame's
+                      //   fxy[1] (gs_cov3d_kernel): the projection reads it instead of the
+                      //   rotation and scales
   int pow2;           // tile size, band stride and fxy[1] are powers of two: the
                       // projection divides by them with exact multiplies / shifts
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)
@@ -101,6 +104,8 @@ struct Buffers {
   const float4* scale_gid;  // sx sy sz gid
   const float4* cull;       // band cull: mean xyz + largest log-scale (NaN: empty slot, inf: never culled)
   const float4* mean_op;    // mean xyz + opacity (FrameParams::mean_w1: every mean's w is 1)
+  float* cov3;              // [10][n] per Gaussian: ComputeCov3D's 9 entries (m[c][r] at c * 3 + r)
+                            //   and its gid, SoA (FrameParams::cov_cache; static per fxy[1])
   // device order: record i is the input Gaussian perm[i] (3D Morton order by
   // default); the depth sort breaks ties by the input index, as the reference
   const uint32_t* perm;     // [n] device index -> input index
@@ -208,6 +213,8 @@ bool bin_lds_fits(int n_tiles);
 hipError_t init_kernel_attributes();
 
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s);
+// the 3D covariances of the scene for fp's fxy[1] into Buffers::cov3
+void launch_cov3d(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s);
 void launch_sort(const FrameParams& fp, const Buffers& b, hipStream_t s);

@@ -198,7 +198,7 @@ void release(gs_renderer* r) {
     (void)hipFree(r->buf.lanes);
   }
 #endif
-  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg,
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg, r->d_cov,
                   r->d_probe})
     if (p) (void)hipFree(p);
   if (r->d_sh && r->owns_sh) (void)hipFree(r->d_sh);
@@ -295,6 +295,7 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.bin_agg = (r->bin_agg && !r->lattice && r->band_nrows < r->tiles_y && r->n_tiles <= kAggMaxTiles) ? 1 : 0;
   fp.pair_cull = (r->pair_cull && !r->bin_global && ((r->n_chunks > 0 && fp.emit_wide) || fp.bin_agg)) ? 1 : 0;
   fp.mean_w1 = r->scene_w1 ? 1 : 0;
+  fp.cov_cache = r->d_cov ? 1 : 0;
   // both rectangles in one 8-B word per Gaussian when every bound fits 8 bits
   fp.rect8 = (fp.pair_cull && r->tiles_x <= 256 && r->band_nrows <= 256) ? 1 : 0;
   // the big-list launch only when the last frame the device completed had
@@ -487,6 +488,18 @@ int enqueue_lattice(gs_renderer* r, const gsk::FrameParams& fp, ProfileSlot* slo
   return GS_OK;
 }
 
+// FrameParams::cov_cache: the scene's 3D covariances for fp's fxy[1], computed
+// on the renderer's stream before the projection that first needs them (the
+// frames in flight on this stream are ordered behind it)
+int ensure_cov(gs_renderer* r, const gsk::FrameParams& fp, hipStream_t s) {
+  if (!fp.cov_cache || (r->cov_valid && r->cov_sd == fp.scale_div)) return GS_OK;
+  gsk::launch_cov3d(fp, r->buf, s);
+  GS_HIP(hipGetLastError());
+  r->cov_sd = fp.scale_div;
+  r->cov_valid = true;
+  return GS_OK;
+}
+
 int enqueue_frame(gs_renderer* r) {
   // several frames may be in flight on the stream; the host mirrors always
   // hold the last one's counters after gs_sync
@@ -517,6 +530,7 @@ int enqueue_frame(gs_renderer* r) {
   // scan); the global-atomic path accumulates tile_count and needs zeros
   if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
     GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, s));
+  if (int rc = ensure_cov(r, fp, s); rc != GS_OK) return rc;
   if (slot) GS_HIP(hipEventRecord(slot->ev[0], s));
   gsk::launch_project(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[1], s));
@@ -889,6 +903,10 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.crect = (uint2*)((char*)r->d_gauss + nn * 64);
   r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
   r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 76);
+  // the 3D covariance cache: 9 entries + the gid per Gaussian (SoA)
+  if ((e = hipMalloc(&r->d_cov, nn * 40)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(covariances)"));
+  poison(r->d_cov, nn * 40, "cov");
+  r->buf.cov3 = (float*)r->d_cov;
 
   const size_t T = (size_t)std::max(r->n_tiles, 1);
   r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
@@ -1197,6 +1215,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
       fp.lazy = 0;
       if (r->bin_global || r->n_chunks == 0 || r->n_tiles == 0)
         GS_HIP(hipMemsetAsync(r->d_zero, 0, r->zero_bytes, r->stream));
+      if ((rc = ensure_cov(r, fp, r->stream)) != GS_OK) return rc;
       gsk::launch_project(fp, bb, r->stream);
       gsk::launch_scan(fp, bb, r->stream);
       gsk::launch_emit(fp, bb, r->stream);
@@ -1255,6 +1274,7 @@ int read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     fp.full_record = 1;
     fp.rect8 = 0;  // (the readback takes the 16-bit reference rectangle)
     fp.mean_w1 = 0;  // (and the 48-B record with the colour)
+    if ((rc = ensure_cov(r, fp, r->stream)) != GS_OK) return rc;
     gsk::launch_project(fp, r->buf, r->stream);
     GS_HIP(hipGetLastError());
     GS_HIP(hipStreamSynchronize(r->stream));

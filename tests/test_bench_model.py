@@ -54,14 +54,14 @@ def test_stage_bytes_from_the_layouts():
     def ab(k, **kw):
         return bench.layout_bytes(k, T, P, n, px, rec, 0, st, nc, 8, **kw)
 
-    # mean + opacity, scales + gid, rotation; two 4-B rectangles, depth key; 32-B records
-    assert ab("project") == n * (48 + 8 + 4) + n * 32
+    # mean + opacity, the cached 3D covariance + gid; two 4-B rectangles, depth key; 32-B records
+    assert ab("project") == n * (56 + 8 + 4) + n * 32
     assert ab("scan") == n * 8 + 3 * nc * T * 4 + T * 12
     assert ab("emit") == n * (4 + 4) + nc * T * 4 + P * 8
     assert ab("sort") == P * 12  # no big lists: read the key, write the list entry
     assert ab("blend") == T * 8 + rec * 52 + px * 19
-    # a band: every Gaussian's 16-B cull record, the band's share in full
-    assert ab("project", share=0.25, band=True) == n * 16 + 0.25 * n * (48 + 4 + 32) + n * 8
+    # a band: every Gaussian's 16-B cull record and scales + gid, the band's share in full
+    assert ab("project", share=0.25, band=True) == n * 32 + 0.25 * n * (16 + 36 + 4 + 32) + n * 8
 
 
 def test_lazy_big_list_sort_bytes():
