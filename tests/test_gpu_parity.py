@@ -477,6 +477,38 @@ def test_orbit_frames(pc12):
         assert_same_bits(s.get_rgba(), ref["rgba"], f"orbit frame {k}")
 
 
+def test_focal_changes_between_frames(pc12):
+    """One renderer, fxy[1] changed between frames: the projection's cached
+    3D covariances (computed once per fxy[1]) follow it, frame for frame
+    against the oracle, including a frame in flight when it changes."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+    from oracle import oracle as O
+
+    g, bb = pc12
+    view, proj = camera.headless(bb, 1280, 720)
+    s = GpuSplatter(g, TiledFramebuffer(1280, 720, 16, 16), device=0)
+    s.set_view_wire(view)
+    s.set_projection_wire(proj)
+
+    def check(sd):
+        ref = O.render(g, O.make_frame(view, proj, 1280, 720, 16, 16, camera.FOV_DEFAULT, sd))
+        assert_same_bits(s.get_rgba(), ref["rgba"], f"fxy[1] = {sd}")
+
+    for sd in (1.0, 0.1, 0.1, 0.5):
+        s.update_focal_lengths(camera.FOV_DEFAULT, sd)
+        s.execute()
+        check(sd)
+    # a change with the previous frame still in flight on the renderer's stream
+    s.update_focal_lengths(camera.FOV_DEFAULT, 0.1)
+    s.execute_async()
+    s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+    s.execute_async()
+    s.sync()
+    check(1.0)
+
+
 def test_render_server_cli(built, tmp_path):
     """The headless render server on the C ABI: same flow and
     log line as splat.cpp; its test.png equals the renderer's BGR8 frame."""
