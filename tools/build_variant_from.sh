@@ -10,4 +10,4 @@ rm -rf $root && mkdir -p $root
 git archive "$rev" include gaussian_splat_ipu_amd/csrc | tar -x -C $root
 for e in "$@"; do (cd $root/gaussian_splat_ipu_amd/csrc && python3 "$e"); done  # (absolute paths)
 make -s -C $root/gaussian_splat_ipu_amd/csrc ../lib/libgsplat.so
-mkdir -p tmp_ab/$name && cp $root/gaussian_splat_ipu_amd/lib/libgsplat.so tmp_ab/$name/
+mkdir -p ${ABDIR:-tmp_ab}/$name && cp $root/gaussian_splat_ipu_amd/lib/libgsplat.so ${ABDIR:-tmp_ab}/$name/
