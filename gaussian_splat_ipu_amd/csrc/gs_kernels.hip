@@ -2921,15 +2921,26 @@ __device__ __forceinline__ void blend_composite(Px& q, float power, float e, con
   q.done = q.done || brk;
 }
 
+// the pixel's RGBA f32 value (+0: a -0 sum stored as +0, as the oracle)
+__device__ __forceinline__ float4 pixel_rgba(const Px& q) {
+  return make_float4(0.0f + q.c01.x, 0.0f + q.c01.y, 0.0f + q.c23.x, 0.0f + q.c23.y);
+}
+
 // row: the pixel's row in this band's output
+__device__ __forceinline__ void store_bgr(const FrameParams& fp, const Buffers& b, int px, int row, const Px& q) {
+  const float4 o = pixel_rgba(q);
+  uint8_t* dst = b.bgr + (size_t)row * fp.bgr_pitch + 3 * (size_t)px;
+  dst[0] = to_u8(o.z);  // RGBA2BGR
+  dst[1] = to_u8(o.y);
+  dst[2] = to_u8(o.x);
+}
+
+// one pixel per lane: a wave's 16-B stores cover whole 128-B lines (8-pixel
+// rows of an 8x8 block), so the streaming stores write each line once
 __device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers& b, int px, int row,
                                             const Px& q) {
-  const float o0 = 0.0f + q.c01.x, o1 = 0.0f + q.c01.y, o2 = 0.0f + q.c23.x, o3 = 0.0f + q.c23.y;
-  if (fp.write_rgba) store_stream(b.rgba + (size_t)row * fp.width + px, make_float4(o0, o1, o2, o3));
-  uint8_t* dst = b.bgr + (size_t)row * fp.bgr_pitch + 3 * (size_t)px;
-  dst[0] = to_u8(o2);  // RGBA2BGR
-  dst[1] = to_u8(o1);
-  dst[2] = to_u8(o0);
+  if (fp.write_rgba) store_stream(b.rgba + (size_t)row * fp.width + px, pixel_rgba(q));
+  store_bgr(fp, b, px, row, q);
 }
 
 // The records of a lane's batch mask (bit k = staged record k), one per
@@ -3433,8 +3444,28 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
     b.blend_count[4 * slot + half] = staged;
     b.blend_count[4 * slot + 2 + half] = 0u;
   }
-  if (va) store_pixel(fp, b, px, tyb * fp.tile_h + ly, qa);
-  if (vb) store_pixel(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
+  // RGBA f32 through the wave's (now idle) staging LDS: a lane's two pixels
+  // are neighbours, so storing them directly would write every other 16 B of
+  // a line per instruction, and streaming stores do not merge the halves in
+  // L2 (PMC WRITE_SIZE 40.9 -> 73.6 MB per launch at config 3).  Row-major in
+  // LDS, each store instruction covers four whole 256-B pixel rows.
+  if (fp.write_rgba) {
+    float4* const sp = &st[0][0];  // st[0], st[1]: the half tile's 128 pixels
+    sp[row * 16 + lx] = pixel_rgba(qa);
+    sp[row * 16 + lx + 1] = pixel_rgba(qb);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 64 * h + lane, r = k >> 4, c = k & 15;
+      const int x = tile_x0 + c, y = tile_y0 + 8 * half + r;
+      if (y < fp.height && x < fp.width)
+        store_stream(b.rgba + (size_t)(tyb * fp.tile_h + 8 * half + r) * fp.width + x, sp[k]);
+    }
+  }
+  if (va) store_bgr(fp, b, px, tyb * fp.tile_h + ly, qa);
+  if (vb) store_bgr(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
 }
 
 template <bool HWEXP>

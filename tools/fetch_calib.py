@@ -3,6 +3,7 @@ PMC counter and the bytes each access pattern really reads from HBM.
 
     hipcc --offload-arch=gfx950 -O3 tools/hip/fetch_calib.hip -o tools/hip/fetch_calib
     rocprofv3 --pmc FETCH_SIZE -d <dir> -o calib --output-format csv -- tools/hip/fetch_calib
+    rocprofv3 --pmc WRITE_SIZE -d <dir>w -o calib --output-format csv -- tools/hip/fetch_calib
     python tools/fetch_calib.py <dir> [--json out.json]
 
 Per kernel (gather32 split into its random-order and runs-of-8 launches by
@@ -22,6 +23,8 @@ BYTES = {  # data + streamed indices per launch (fetch_calib.hip)
     "gather32_runs8": N * 32 + N * 4,
     "gather16": N * 16 + N * 4,
     "gather4": N * 4 + N * 4,
+    "store16": N * 16,
+    "store16nt": N * 16,
 }
 
 
@@ -31,9 +34,15 @@ def main():
     ap.add_argument("--json")
     a = ap.parse_args()
     rows = []
+    wacc = collections.defaultdict(list)
     for f in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
+                if r["Counter_Name"] == "WRITE_SIZE":
+                    if "store16" in r["Kernel_Name"]:
+                        k = "store16nt" if "store16nt" in r["Kernel_Name"] else "store16"
+                        wacc[k].append(float(r["Counter_Value"]) * 1024)
+                    continue
                 if r["Counter_Name"] != "FETCH_SIZE":
                     continue
                 did = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or len(rows))
@@ -56,6 +65,11 @@ def main():
         mean = sum(vs) / len(vs)
         out[k] = {"launches": len(vs), "fetch_bytes": mean, "true_bytes": BYTES[k], "fetch_over_true": mean / BYTES[k]}
         print(f"{k:16s} FETCH_SIZE {mean / 1e6:9.1f} MB  true {BYTES[k] / 1e6:9.1f} MB  ratio {mean / BYTES[k]:.3f}")
+    for k, vs in wacc.items():
+        vs = vs[1:] if len(vs) > 1 else vs
+        mean = sum(vs) / len(vs)
+        out[k] = {"launches": len(vs), "write_bytes": mean, "true_bytes": BYTES[k], "write_over_true": mean / BYTES[k]}
+        print(f"{k:16s} WRITE_SIZE {mean / 1e6:9.1f} MB  true {BYTES[k] / 1e6:9.1f} MB  ratio {mean / BYTES[k]:.3f}")
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(out, fh, indent=1)

@@ -11,6 +11,9 @@
 //   gather4    one u32 per index, random permutation
 //   runs32     32-B records, indices in runs of 8 consecutive records (the
 //              blend's Morton-local records: neighbours share cache lines)
+// and, for WRITE_SIZE (its own --pmc pass), 16-B lane-consecutive stores:
+//   store16    plain global_store_dwordx4
+//   store16nt  the same stores non-temporal (the blend's RGBA pixels)
 //
 //   hipcc --offload-arch=gfx950 -O3 tools/hip/fetch_calib.hip -o tools/hip/fetch_calib
 //   rocprofv3 --pmc FETCH_SIZE -d <dir> -o calib --output-format csv -- tools/hip/fetch_calib
@@ -71,6 +74,18 @@ __global__ void gather4(const uint32_t* __restrict__ w, const uint32_t* __restri
   if (acc == 12345u) out[0] = (float)acc;
 }
 
+__global__ void store16(float4* __restrict__ dst, size_t n, float v) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = make_float4(v, v, v, v);
+}
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__global__ void store16nt(float4* __restrict__ dst, size_t n, float v) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const f32x4_t w = {v, v, v, v};
+  if (i < n) __builtin_nontemporal_store(w, reinterpret_cast<f32x4_t*>(dst + i));
+}
+
 int main() {
   const size_t n = (size_t)1 << 24;  // 16 M items: 256 MB of 16-B, 512 MB of 32-B -- far past the L2s
   float4 *d_a = nullptr, *d_b = nullptr;
@@ -105,6 +120,8 @@ int main() {
     gather16<<<grid, 256>>>(d_a, d_idx, d_out, n);
     gather4<<<grid, 256>>>(d_w, d_idx, d_out, n);
     gather32<<<grid, 256>>>(d_b, d_runs, d_out, n);  // (second gather32 launch of each rep: the runs pattern)
+    store16<<<grid, 256>>>(d_a, n, 1.0f);
+    store16nt<<<grid, 256>>>(d_a, n, 2.0f);
   }
   CK(hipDeviceSynchronize());
   // the bytes each launch reads (the index arrays: 4 B per item, streamed)
@@ -112,6 +129,7 @@ int main() {
   std::printf("gather32 %d launches, %zu bytes per launch (data) + %zu (indices)  [odd launches: random, even: runs of 8]\n",
               2 * reps, n * 32, n * 4);
   std::printf("gather16 %d launches, %zu bytes per launch (data) + %zu (indices)\n", reps, n * 16, n * 4);
+  std::printf("store16 / store16nt %d launches each, %zu bytes per launch (written)\n", reps, n * 16);
   std::printf("gather4 %d launches, %zu bytes per launch (data) + %zu (indices)\n", reps, n * 4, n * 4);
   (void)hipFree(d_a);
   (void)hipFree(d_b);
