@@ -317,7 +317,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   float4 sg;
   float c3[9];
   if (fp.cov_cache && !fp.band_cull) {
-    sg = make_float4(0.f, 0.f, 0.f, load_stream(b.cov3 + 9 * nn + i));
+    sg = make_float4(0.f, 0.f, 0.f, 1.0f);  // (liveness: the sign of Sigma[2][2], below)
   } else {
     sg = b.scale_gid[i];
   }
@@ -328,6 +328,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
     if (fp.cov_cache) {
 #pragma unroll
       for (int k = 0; k < 9; ++k) c3[k] = load_stream(b.cov3 + k * nn + i);
+      if (c3[8] < 0.0f) sg.w = 0.0f;
     } else {
       rot = b.rot[i];
     }
@@ -3464,8 +3465,34 @@ __device__ __forceinline__ void blend_wave_px2(const FrameParams& fp, const Buff
         store_stream(b.rgba + (size_t)(tyb * fp.tile_h + 8 * half + r) * fp.width + x, sp[k]);
     }
   }
-  if (va) store_bgr(fp, b, px, tyb * fp.tile_h + ly, qa);
-  if (vb) store_bgr(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
+  const bool dw = tile_x0 + 16 <= fp.width && ((uintptr_t)b.bgr & 3u) == 0u && (fp.bgr_pitch & 3) == 0;
+  if (dw) {
+    uint8_t* const sb = reinterpret_cast<uint8_t*>(&st[2][0]);  // 8 rows x 48 B (st[2] is idle)
+    const float4 oa = pixel_rgba(qa), ob = pixel_rgba(qb);
+    uint8_t* const d = sb + row * 48 + 3 * lx;
+    d[0] = to_u8(oa.z);  // RGBA2BGR
+    d[1] = to_u8(oa.y);
+    d[2] = to_u8(oa.x);
+    d[3] = to_u8(ob.z);
+    d[4] = to_u8(ob.y);
+    d[5] = to_u8(ob.x);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 64 * h + lane;  // dword k of the half tile's 96: row k / 12, dword k % 12
+      if (k < 96) {
+        const int r = k / 12, c = k - 12 * r;
+        if (tile_y0 + 8 * half + r < fp.height)
+          *reinterpret_cast<uint32_t*>(b.bgr + (size_t)(tyb * fp.tile_h + 8 * half + r) * fp.bgr_pitch +
+                                       3 * (size_t)tile_x0 + 4 * c) = reinterpret_cast<const uint32_t*>(sb)[k];
+      }
+    }
+  } else {
+    if (va) store_bgr(fp, b, px, tyb * fp.tile_h + ly, qa);
+    if (vb) store_bgr(fp, b, px + 1, tyb * fp.tile_h + ly, qb);
+  }
 }
 
 template <bool HWEXP>
@@ -3582,8 +3609,10 @@ __global__ __launch_bounds__(256) void gs_cov3d_kernel(FrameParams fp, Buffers b
   if (i >= fp.n) return;
   const size_t nn = (size_t)fp.n;
   const float4 sg = b.scale_gid[i];
-  b.cov3[9 * nn + i] = sg.w;
-  if (sg.w <= 0.0f) return;  // (an empty slot: the projection skips it)
+  if (sg.w <= 0.0f) {  // (an empty slot: the projection skips it)
+    b.cov3[8 * nn + i] = -1.0f;
+    return;
+  }
   const float4 rot = b.rot[i];
   const M3 C3 = cov3d(rot, div_p2<P2>(sg.x, fp.scale_div, fp.inv_sd), div_p2<P2>(sg.y, fp.scale_div, fp.inv_sd),
                       div_p2<P2>(sg.z, fp.scale_div, fp.inv_sd));
