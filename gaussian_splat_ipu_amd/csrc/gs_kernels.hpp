@@ -104,8 +104,9 @@ struct Buffers {
   const float4* scale_gid;  // sx sy sz gid
   const float4* cull;       // band cull: mean xyz + largest log-scale (NaN: empty slot, inf: never culled)
   const float4* mean_op;    // mean xyz + opacity (FrameParams::mean_w1: every mean's w is 1)
-  float* cov3;              // [10][n] per Gaussian: ComputeCov3D's 9 entries (m[c][r] at c * 3 + r)
-                            //   and its gid, SoA (FrameParams::cov_cache; static per fxy[1])
+  float* cov3;              // [9][n] per Gaussian: ComputeCov3D's 9 entries (m[c][r] at c * 3 + r),
+                            //   SoA (FrameParams::cov_cache; static per fxy[1]); an empty slot
+                            //   (gid <= 0) has m[2][2] = -1, a live one's is >= +0 or NaN
   // device order: record i is the input Gaussian perm[i] (3D Morton order by
   // default); the depth sort breaks ties by the input index, as the reference
   const uint32_t* perm;     // [n] device index -> input index

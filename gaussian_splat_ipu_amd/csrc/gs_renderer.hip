@@ -904,8 +904,8 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
   r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 76);
   // the 3D covariance cache: 9 entries + the gid per Gaussian (SoA)
-  if ((e = hipMalloc(&r->d_cov, nn * 40)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(covariances)"));
-  poison(r->d_cov, nn * 40, "cov");
+  if ((e = hipMalloc(&r->d_cov, nn * 36)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(covariances)"));
+  poison(r->d_cov, nn * 36, "cov");
   r->buf.cov3 = (float*)r->d_cov;
 
   const size_t T = (size_t)std::max(r->n_tiles, 1);
