@@ -238,8 +238,8 @@ def layout_bytes(kernel: str, T: int, P: int, n: int, px: int, rec: int, rec_con
     if band:  # band cull: every Gaussian's 16-B cull record and scales + gid, the band's Gaussians in
         # full (mean + opacity, the cached 3D covariance); rectangles, depth key, records
         project = n * (16 + 16) + rendered * (16 + 36 + 4 + 32) + n * rect_b
-    else:  # mean + opacity, the cached 3D covariance + gid (56 B); rectangles, depth key; the binned records
-        project = n * (56 + rect_b + 4) + rendered * 32
+    else:  # mean + opacity, the cached 3D covariance (52 B); rectangles, depth key; the binned records
+        project = n * (52 + rect_b + 4) + rendered * 32
     chunk_matrix = n_chunks * T * 4
     if pre or win:  # lazy big lists: the select reads every big-list key once,
         # writes the prefixes and windows, and the prefixes are sorted into the lists

@@ -55,7 +55,7 @@ def test_stage_bytes_from_the_layouts():
         return bench.layout_bytes(k, T, P, n, px, rec, 0, st, nc, 8, **kw)
 
     # mean + opacity, the cached 3D covariance + gid; two 4-B rectangles, depth key; 32-B records
-    assert ab("project") == n * (56 + 8 + 4) + n * 32
+    assert ab("project") == n * (52 + 8 + 4) + n * 32
     assert ab("scan") == n * 8 + 3 * nc * T * 4 + T * 12
     assert ab("emit") == n * (4 + 4) + nc * T * 4 + P * 8
     assert ab("sort") == P * 12  # no big lists: read the key, write the list entry
