@@ -295,7 +295,7 @@ __device__ __forceinline__ void sh_colour(const FrameParams& fp, const Buffers& 
 
 template <bool P2>
 __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i, uint2& rect_out,
-                                            uint2& crect_out) {
+                                            uint2& crect_out, float4* stage = nullptr) {
   bool rendered = false;
   // mean_w1: the mean's w is 1 and the colour's rgb is not needed (the blend
   // reads it from the scene): one 16-B load of xyz + opacity instead of 32 B
@@ -488,6 +488,10 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
       rec[0] = rec0;
       rec[1] = make_float4(k1, pcut, col.x, col.y);
       rec[2] = make_float4(col.z, k3, __uint_as_float(b01), __uint_as_float(b23));
+    } else if (stage) {  // (project_block stores the wave's records as whole lines)
+      stage[0] = rec0;
+      stage[1] = make_float4(k1, pcut, __uint_as_float(b01), __uint_as_float(b23));
+      if (fp.sh_degree >= 0 && b.sh) b.col_out[i] = col;
     } else if ((binned.x & 0xFFFFu) <= (binned.x >> 16)) {
       rec[0] = rec0;
       rec[1] = make_float4(k1, pcut, __uint_as_float(b01), __uint_as_float(b23));
@@ -687,7 +691,11 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
 }
 
 // one block of 256 Gaussians (every thread of the workgroup calls it)
-template <bool P2>
+// STAGE (whole frames' lean projection): the records go out as streaming
+// stores of whole 128-B lines -- each wave's 64 records (2 KB, contiguous)
+// through LDS, written for every Gaussian of the wave (a record that no tile
+// binned is never read, so its contents do not matter)
+template <bool P2, bool STAGE = false>
 __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffers& b, int blk) {
   const int i = blk * 256 + threadIdx.x;
   bool rendered = false;
@@ -714,6 +722,23 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
       b.depth_key[i] = 0xFFFFFFFFu;
     } else if (i < fp.n) {
       rendered = project_one<P2>(fp, b, i, rect, crect);
+    }
+  } else if constexpr (STAGE) {
+    __shared__ float4 s_rec[4][128];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float4 r2[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    if (i < fp.n) rendered = project_one<P2>(fp, b, i, rect, crect, r2);
+    float4* const sw = s_rec[wave];
+    sw[2 * lane] = r2[0];
+    sw[2 * lane + 1] = r2[1];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int i0 = blk * 256 + wave * 64;  // the wave's first Gaussian
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 64 * h + lane;  // float4 k of the wave's records: record i0 + k / 2
+      if (i0 + (k >> 1) < fp.n) store_stream(b.rec + 2 * (size_t)i0 + k, sw[k]);
     }
   } else if (i < fp.n) {
     rendered = project_one<P2>(fp, b, i, rect, crect);
@@ -744,7 +769,7 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
     fp.sh_degree = -1;
     fp.bin_global = 0;
   }
-  project_block<P2>(fp, b, blockIdx.x);
+  project_block<P2, MODE == kProjLean>(fp, b, blockIdx.x);
 }
 
 // --------------------------------------------------------------------- scan
