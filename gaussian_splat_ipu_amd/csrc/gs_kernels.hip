@@ -2961,8 +2961,10 @@ __device__ __forceinline__ void store_bgr(const FrameParams& fp, const Buffers& 
   dst[2] = to_u8(o.x);
 }
 
-// one pixel per lane: a wave's 16-B stores cover whole 128-B lines (8-pixel
-// rows of an 8x8 block), so the streaming stores write each line once
+// one pixel per lane: a wave's 16-B stores cover whole 128-B lines (the
+// 8-pixel rows of an 8x8 block, the 16-pixel rows of a 16x4 one), so the
+// streaming stores write each line once (the quad-row runs of other tile
+// shapes, BQW = 0, may start or end mid-line)
 __device__ __forceinline__ void store_pixel(const FrameParams& fp, const Buffers& b, int px, int row,
                                             const Px& q) {
   if (fp.write_rgba) store_stream(b.rgba + (size_t)row * fp.width + px, pixel_rgba(q));
