@@ -75,7 +75,8 @@ struct gs_renderer {
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
   void* d_lazy = nullptr;       // lazy big lists (16x16 tiles): per-tile tables + saved blend waves
   void* d_agg = nullptr;        // aggregated binning: per projection block its tile box and offsets
-  void* d_cov = nullptr;        // the scene's 3D covariances + gids (Buffers::cov3), 40 B per Gaussian
+  void* d_cov = nullptr;        // the scene's 3D covariances (Buffers::cov3): 9 float planes, 36 B per
+                                // Gaussian, an empty slot marked by Sigma[2][2] < 0; null: computed per frame
   float cov_sd = 0.0f;          // ... computed for this fxy[1]
   bool cov_valid = false;
   void* d_probe = nullptr;      // (GS_PROBE builds, GSPLAT_PROBE_FILE) the kernels' per-frame start / end ring

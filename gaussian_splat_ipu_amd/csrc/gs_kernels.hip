@@ -690,6 +690,14 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
   }
 }
 
+// GS_X_BAND (measurement builds only, tools/build_x.sh; wrong frames): what
+// a row band's projection spends where.  1: every block returns after the
+// cull pass; 2: no aggregated counting (and every block reports no rendered
+// Gaussian, so the emit places nothing).
+#ifndef GS_X_BAND
+#define GS_X_BAND 0
+#endif
+
 // one block of 256 Gaussians (every thread of the workgroup calls it)
 // STAGE (whole frames' lean projection): the records go out as streaming
 // stores of whole 128-B lines -- each wave's 64 records (2 KB, contiguous)
@@ -713,7 +721,7 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
       const float4 cr = b.cull[i];
       culled = !__builtin_isnan(cr.w) && band_culled_fast<P2>(fp, cr);
     }
-    if (__syncthreads_count(i < fp.n && !culled) == 0) {
+    if (__syncthreads_count(i < fp.n && !culled) == 0 || GS_X_BAND == 1) {
       if (threadIdx.x == 0) b.block_rendered[blk] = 0u;
       return;
     }
@@ -743,10 +751,10 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
   } else if (i < fp.n) {
     rendered = project_one<P2>(fp, b, i, rect, crect);
   }
-  if (fp.bin_agg) agg_count(fp, b, rect, crect, blk);
+  if (fp.bin_agg && GS_X_BAND != 2) agg_count(fp, b, rect, crect, blk);
   // V per workgroup (summed by the scan kernel): no single-address atomics
   const int v = __syncthreads_count(rendered);
-  if (threadIdx.x == 0) b.block_rendered[blk] = (uint32_t)v;
+  if (threadIdx.x == 0) b.block_rendered[blk] = (fp.band_cull && GS_X_BAND == 2) ? 0u : (uint32_t)v;
 }
 
 // one workgroup per block (a grid of workgroups walking the blocks held

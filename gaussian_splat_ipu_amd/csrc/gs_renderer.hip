@@ -48,7 +48,7 @@ int select_device(gs_renderer* r) {
 }
 
 // gs_test_set (include/gsplat.h): the test hooks gs_create reads
-std::atomic<int64_t> g_test_chunk_size{0}, g_test_bin_agg{-1}, g_test_poison{0};
+std::atomic<int64_t> g_test_chunk_size{0}, g_test_bin_agg{-1}, g_test_poison{0}, g_test_cov_cache{-1};
 
 // gs_test_set("debug_poison", 1): every device buffer is filled with 0xA5
 // bytes when it is allocated (before any initialisation the renderer does
@@ -903,10 +903,22 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.crect = (uint2*)((char*)r->d_gauss + nn * 64);
   r->buf.depth_key = (uint32_t*)((char*)r->d_gauss + nn * 72);
   r->buf.block_rendered = (uint32_t*)((char*)r->d_gauss + nn * 76);
-  // the 3D covariance cache: 9 entries + the gid per Gaussian (SoA)
-  if ((e = hipMalloc(&r->d_cov, nn * 36)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(covariances)"));
-  poison(r->d_cov, nn * 36, "cov");
-  r->buf.cov3 = (float*)r->d_cov;
+  // the 3D covariance cache: 9 float planes (SoA), 36 B per Gaussian; an empty
+  // slot is marked by a negative Sigma[2][2] (gs_cov3d_kernel).  An
+  // optimisation only: the lattice emulator never reads it, and when the
+  // allocation fails the projection keeps computing the covariances from the
+  // rotation and the scales (cov_cache = 0) instead of refusing the scene.
+  // (test hook: gs_test_set("cov_cache", 0) takes the fallback)
+  if (!lattice && g_test_cov_cache.load() != 0) {
+    if ((e = hipMalloc(&r->d_cov, nn * 36)) == hipSuccess) {
+      poison(r->d_cov, nn * 36, "cov");
+      r->buf.cov3 = (float*)r->d_cov;
+    } else {
+      (void)hipGetLastError();  // (clear the sticky error of the failed allocation)
+      r->d_cov = nullptr;
+      r->buf.cov3 = nullptr;
+    }
+  }
 
   const size_t T = (size_t)std::max(r->n_tiles, 1);
   r->zero_bytes = ((16 + T) * 4 + 15) / 16 * 16;
@@ -1319,6 +1331,8 @@ int gs_test_set(const char* key, int64_t value) {
     gsr::g_test_bin_agg.store(value);
   } else if (k == "debug_poison" && (value == 0 || value == 1)) {
     gsr::g_test_poison.store(value);
+  } else if (k == "cov_cache" && (value == -1 || value == 0)) {
+    gsr::g_test_cov_cache.store(value);
   } else {
     gsh::set_error("gs_test_set: unknown key or value");
     return GS_EINVAL;

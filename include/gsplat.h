@@ -503,6 +503,10 @@ int gs_cam_headless(const float* bb6, uint32_t width, uint32_t height, float fov
  *                     passes too (the path of bands wider than 16 384 tiles)
  *   "debug_poison"    1 = every device buffer starts as 0xA5 bytes instead
  *                     of zeros (reads of memory no stage wrote show up)
+ *   "cov_cache"       -1 = automatic; 0 = no 3D covariance cache (the
+ *                     projection computes them from the rotation and the
+ *                     scales every frame: the path a failed cache
+ *                     allocation takes)
  * Returns GS_EINVAL for an unknown key or value. */
 int gs_test_set(const char* key, int64_t value);
 

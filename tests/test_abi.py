@@ -172,6 +172,8 @@ def test_test_hooks_accept_only_their_keys(built):
     assert L.gs_test_set(b"bin_chunk_size", 0) == 0
     assert L.gs_test_set(b"bin_agg", -1) == 0
     assert L.gs_test_set(b"debug_poison", 0) == 0
+    assert L.gs_test_set(b"cov_cache", -1) == 0
+    assert L.gs_test_set(b"cov_cache", 1) == _lib.GS_EINVAL  # (only -1 / 0)
     assert L.gs_test_set(b"bin_agg", 1) == _lib.GS_EINVAL  # (only -1 / 0)
     assert L.gs_test_set(b"blend_px2", 0) == _lib.GS_EINVAL
     assert L.gs_test_set(None, 0) == _lib.GS_EINVAL

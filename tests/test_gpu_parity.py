@@ -477,15 +477,28 @@ def test_orbit_frames(pc12):
         assert_same_bits(s.get_rgba(), ref["rgba"], f"orbit frame {k}")
 
 
-def test_focal_changes_between_frames(pc12):
+@pytest.mark.parametrize("cov_cache", [-1, 0])
+def test_focal_changes_between_frames(pc12, test_hook, cov_cache):
     """One renderer, fxy[1] changed between frames: the projection's cached
     3D covariances (computed once per fxy[1]) follow it, frame for frame
-    against the oracle, including a frame in flight when it changes."""
+    against the oracle, including a frame in flight when it changes.
+    cov_cache = 0: no cache (the path a failed cache allocation takes: the
+    covariances from the rotation and the scales every frame), a whole frame
+    and a row band."""
     from gaussian_splat_ipu_amd import camera
     from gaussian_splat_ipu_amd.splatter import GpuSplatter
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
     from oracle import oracle as O
 
+    if cov_cache == 0:
+        test_hook("cov_cache", 0)
+        g, bb = pc12
+        view, proj = camera.headless(bb, 1920, 1080)
+        for band_count, band_index in [(1, 0), (8, 3)]:
+            s, f = _frame_pair(g, view, proj, 1920, 1080, 16, 16, 0.1, band_count=band_count,
+                               band_index=band_index)
+            _assert_parity(s, f, g, check_proj=band_count == 1)
+            s.close()
     g, bb = pc12
     view, proj = camera.headless(bb, 1280, 720)
     s = GpuSplatter(g, TiledFramebuffer(1280, 720, 16, 16), device=0)
@@ -744,10 +757,11 @@ def test_blend_px2_bit_exact(pc12, W, H, bin_global):
     """Two pixels per blend lane (whole frames of 16x16 tiles: a 16x8 half of
     the tile per wave, one mask per pixel pair, two independent chains per
     record, tiles longest list first) gives the oracle's frame bit for bit,
-    partial edge tiles included (1000x700).  The chunked binning has each
-    slot's tile and list segment written by the sort launch; the global-atomic
-    binning's frames read the queues and tile starts instead.  A row band
-    keeps one pixel per lane (the in-blend sort)."""
+    partial edge tiles included (1000x700).  Each slot's tile and list
+    segment come from the sort launch's segment table whenever the frame has
+    no big-list launches (pc12 has no list > 2048, so both binning paths take
+    it here; test_blend_px2_queues_with_big_lists covers the queue reads).  A
+    row band keeps one pixel per lane (the in-blend sort)."""
     from gaussian_splat_ipu_amd import camera
 
     g, bb = pc12
@@ -758,6 +772,37 @@ def test_blend_px2_bit_exact(pc12, W, H, bin_global):
         assert bool(s.stats()["paths"] & 4) == (band_count == 1)
         _assert_parity(s, f, g, check_proj=False)
         s.close()
+
+
+def test_blend_px2_queues_with_big_lists(built):
+    """The two-pixel blend reading its slots' tiles from the sort queues and
+    the tile starts (no segment table): a frame with big-list launches and no
+    lazy lists -- the global-atomic binning, whose frames keep every list
+    sorted before the blend.  A dense scene (lists > 2048 keys), the second
+    frame takes the big-list launches (the hint of the first); both frames
+    bit for bit."""
+    from gaussian_splat_ipu_amd import camera, scene
+
+    g, bb = scene.prepare_scene(scene.synthetic(scene.SynthSpec(n=20000, seed=5, sh_degree=0)))
+    a = np.ascontiguousarray(g).view(np.float32).reshape(-1, 16).copy()
+    rng = np.random.default_rng(3)
+    n = a.shape[0]
+    a[:, 0] = rng.uniform(-0.3, 0.3, n)
+    a[:, 1] = rng.uniform(-0.3, 0.3, n)
+    a[:, 2] = rng.uniform(0.0, 1.5, n)
+    a[:, 3] = 1.0
+    a[:, 7] = rng.uniform(0.02, 0.3, n)
+    a[:, 12:15] = -4.0 + rng.normal(0.0, 0.2, (n, 3))
+    _, proj = camera.headless(bb, 1280, 720)
+    view = np.float32([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, -4.0, 0, 0, 0, 1])
+    s, f = _frame_pair(a, view, proj, 1280, 720, 16, 16, 1.0, bin_global=True)
+    assert s.stats()["n_big_tiles"] > 0
+    _assert_parity(s, f, a, check_proj=False)
+    s.execute()
+    paths = s.stats()["paths"]
+    assert paths & 4 and paths & 16 and not paths & 8, paths  # px2, big-list launches, not lazy
+    _assert_parity(s, f, a, check_proj=False)
+    s.close()
 
 
 @pytest.mark.parametrize("tw,th", [(32, 8), (8, 32)])

@@ -28,7 +28,7 @@ def _files():
 def tool(built):
     if not os.path.isdir(REF):
         pytest.skip("/root/reference is not present (the reference parser is built here only)")
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref-tools"], check=True)
     if not os.path.exists(TOOL):
         pytest.skip("oracle/_ref/ply_dump was not built (happly.h absent)")
     return TOOL

@@ -1,6 +1,6 @@
 """A scene past 256 binning chunks (default 20 M Gaussians, 306 chunks of
 65535) at 1080p: the chunked binning (gs_colscan_kernel's extra rows) against
-the global-atomic binning forced by GSPLAT_BIN_MAX_CHUNKS -- two independent
+the global-atomic binning (GS_FLAG_BIN_GLOBAL) -- two independent
 GPU paths whose frames, histograms and stats must be identical -- and both
 paths' frame times.  Prints one JSON line.
 
@@ -34,11 +34,8 @@ def main():
     view, proj = camera.headless(bb, W, H)
     out = {"workload": f"synthetic {a.n} Gaussians, {W}x{H}, {T}x{T} tiles, headless camera"}
     frames = {}
-    for name, env in (("chunked", None), ("global", "1")):
-        if env:
-            os.environ["GSPLAT_BIN_MAX_CHUNKS"] = env
-        s = GpuSplatter(g, TiledFramebuffer(W, H, T, T), device=0)
-        os.environ.pop("GSPLAT_BIN_MAX_CHUNKS", None)
+    for name, bin_global in (("chunked", False), ("global", True)):
+        s = GpuSplatter(g, TiledFramebuffer(W, H, T, T), device=0, bin_global=bin_global)
         s.set_view_wire(view)
         s.set_projection_wire(proj)
         s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
