@@ -107,6 +107,7 @@ def parse():
 
 # gs_frame_stats.paths bits (include/gsplat.h)
 PATH_BIN_AGG, PATH_BLEND_SORT, PATH_BLEND_PX2, PATH_LAZY, PATH_BIG_LISTS = 1, 2, 4, 8, 16
+PATH_PROJ_BAND, PATH_PROJ_ANY = 32, 64  # (ABI 13: which projection instantiation ran)
 
 
 def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
@@ -119,7 +120,9 @@ def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
                                                             PATH_LAZY, PATH_BIG_LISTS))
     buckets = [("gs_big_count", 1), ("gs_big_bscan", 1), ("gs_big_scatter", 1), ("gs_big_bsort", 1)]
     if stage == "project":
-        return [("gs_project", 1)]
+        if paths & PATH_PROJ_BAND:
+            return [("gs_project_band", 1)]
+        return [("gs_project_any" if paths & PATH_PROJ_ANY else "gs_project", 1)]
     if stage == "scan":
         if agg:
             return [("gs_agg_scan", 1)]
@@ -137,6 +140,30 @@ def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
     if stage == "blend_cont":  # lazy big lists: window sort + continued blend, pass 2 (launch_blend_cont)
         return [("gs_big_cont", 1), ("gs_blend_cont", 2), ("gs_big_prefix", 1)] + buckets
     raise KeyError(stage)
+
+
+def pmc_key_of(workload: str, n: int, W: int, H: int, TW: int, bands: int, band: int) -> str:
+    """The PMC summary key of a renderer's launches: the workload and the band
+    shape -- "whole" for a plain whole-frame renderer, "bands{B}/band{k}" for
+    band k of a B-way row split (a group member; B = 1: the whole frame as a
+    band, bench.py --gather).  Per-launch counters are kernel properties of
+    that shape, not of the launch mode or the frames in flight."""
+    shape = "whole" if bands <= 0 else f"bands{bands}/band{band}"
+    return f"{workload}:{n}@{W}x{H}/t{TW}/{shape}"
+
+
+def pmc_lookup(path: str, key: str):
+    """The per-kernel PMC summary for `key` from a tools/pmc_summary.py file:
+    {"summaries": {key: {"kernels": ...}}} (several band shapes), or the
+    one-summary form {"config": key, "kernels": ...}; None when absent."""
+    try:
+        d = json.load(open(path))
+    except Exception:
+        return None
+    if "summaries" in d:
+        e = d["summaries"].get(key)
+        return {"config": key, **e} if e else None
+    return d if d.get("config") == key else None
 
 
 def stage_pmc(stage: str, paths: int, kernels: dict, bin_global: bool = False):
@@ -597,17 +624,13 @@ def main():
     dom = max(stage, key=lambda k: stage[k]["avg_ms"])
     # PMC counters are per launch (kernel properties): the key names the
     # workload, the split and the band, not the frames in flight
-    pmc_key = f"{'c5' if a.config5 else 'c3'}:{a.n}@{W}x{H}/t{TW}/world{ngpu}/split{split}/band{rank}"
+    # (the band shape, not the launch: a --gpus N line's rank 0 renders band 0
+    # of N, as band 0 of an N-way split emulated on one GPU does)
+    pmc_key = pmc_key_of("c5" if a.config5 else "c3", a.n, W, H, TW, split if group else 0, 0)
     # HBM bytes per launch of the same stage, from the committed PMC summary of
-    # this exact workload (tools/profile.sh + tools/pmc_summary.py), if any
-    pm = None
-    if os.path.exists(a.pmc_json):
-        try:
-            pm = json.load(open(a.pmc_json))
-            if pm.get("config") != pmc_key:
-                pm = None
-        except Exception:
-            pm = None
+    # this exact workload and band shape (tools/profile.sh, tools/r6/pmc_bands.sh
+    # + tools/pmc_summary.py), if any
+    pm = pmc_lookup(a.pmc_json, pmc_key)
 
     paths = int(st_view.get("paths", 0))
     bin_global = bool(st_view.get("bin_global", 0))
@@ -620,7 +643,7 @@ def main():
 
     def roof(name):
         k = kern[name]
-        pmc = valu = valu_cpi = valu_note = None
+        pmc = valu = valu2 = valu_cpi = valu_note = None
         launched = [x for x, _ in stage_kernels(name, paths, bin_global)]
         if pm is None:
             note = f"no PMC summary for {pmc_key} in {os.path.relpath(a.pmc_json, ROOT)}"
@@ -635,6 +658,11 @@ def main():
                 # stage's wave64 VALU instructions x their hot loops' measured
                 # cycles per instruction over 1024 SIMDs x 2.4 GHz x the launch
                 cyc, used = stage_valu_cycles(name, paths, pm.get("kernels", {}), cpi, bin_global)
+                if vi:
+                    # ... and at a flat 2 SIMD cycles per wave64 instruction
+                    # (MI355X_MICROARCH.md's v_fma_f32 row; DESIGN §4 on why
+                    # the measured costs differ)
+                    valu2 = round(min(1.0, vi * 2.0 / (1024 * 2.4e9 * k["avg_ms"] * 1e-3)), 3)
                 if cyc is not None:
                     valu = round(min(1.0, cyc / (1024 * 2.4e9 * k["avg_ms"] * 1e-3)), 3)
                     valu_cpi = used
@@ -654,6 +682,7 @@ def main():
             if k["avg_ms"] > 0 else None,
             "avg_launch_ms": k["avg_ms"],
             "valu_issue_frac": valu,
+            "valu_issue_frac_2cyc": valu2,
             "valu_cpi": valu_cpi,
         }
         if note:
@@ -683,10 +712,12 @@ def main():
                               "record = list entry + 32-B record + 16-B colour)",
         "avg_launch_ms": rd["avg_launch_ms"],
         "valu_issue_frac": rd["valu_issue_frac"],
+        "valu_issue_frac_2cyc": rd["valu_issue_frac_2cyc"],
         "valu_cpi": rd["valu_cpi"],
         "valu_model": "SQ_INSTS_VALU of the launched kernels x their hot loops' SIMD cycles per wave64 instruction "
                       "(tools/valu_cpi.py from the measured per-instruction costs, tools/hip/valu_rate.hip: "
-                      "v_mul/v_add 2, v_fma/v_cmp/v_cvt/v_pk 4, v_exp 8) over 1024 SIMDs x 2.4 GHz x the launch",
+                      "v_mul/v_add 2, v_fma/v_cmp/v_cvt/v_pk 4, v_exp 8) over 1024 SIMDs x 2.4 GHz x the launch; "
+                      "valu_issue_frac_2cyc: the same instructions at a flat 2 cycles (the guide's v_fma_f32 row)",
         "traffic_model": "PMC HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) and VALU of the kernels this stage launched in "
                          "the timed frames (gs_frame_stats.paths -> bench.stage_kernels), per launch x launches per "
                          "frame; null with traffic_note when the summary lacks one of them",

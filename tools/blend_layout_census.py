@@ -159,13 +159,14 @@ def main():
                 # a window of K staged batches: each step, every lane with a record
                 # left in the window takes one; when no lane has one left in the
                 # window's first batch, the window slides (the next batch staged)
-                for K in a.window:
-                    key = f"win{K}"
+                relw = np.nonzero(union.any(axis=1))[0]
+                for K, wk, key in [(K, walk, f"win{K}") for K in a.window] + \
+                                  [(K, walk[relw], f"cwin{K}") for K in a.window]:
                     A.setdefault(key, 0)
-                    nb = -(-L // B)
-                    cnt = np.zeros((nb, walk.shape[1]), np.int64)
+                    nb = -(-wk.shape[0] // B)
+                    cnt = np.zeros((nb, wk.shape[1]), np.int64)
                     for bb in range(nb):
-                        cnt[bb] = walk[bb * B:(bb + 1) * B].sum(axis=0)
+                        cnt[bb] = wk[bb * B:(bb + 1) * B].sum(axis=0)
                     rem = cnt.copy()
                     steps = 0
                     w = 0
@@ -194,6 +195,18 @@ def main():
                     A["evals"] += int(w.sum()) * k
                 A["iters"] += wave_iters
                 A["tail"] = max(A["tail"], wave_iters)
+                # compacted staging (round 6): the wave stages only the records
+                # whose box meets one of its pixels, in list order, 64 a batch
+                rel = np.nonzero(union.any(axis=1))[0]
+                wc = walk[rel]
+                endc = np.searchsorted(rel, lane_end.max(), side="right")  # records up to the wave's end
+                for k_, key in (("cmp_iters", "cmp_iters"), ("cmp_batches", "cmp_batches"), ("cmp_staged", "cmp_staged")):
+                    A.setdefault(key, 0)
+                for base in range(0, int(endc), B):
+                    w = wc[base:base + B]
+                    A["cmp_batches"] += 1
+                    A["cmp_staged"] += w.shape[0]
+                    A["cmp_iters"] += int(w.sum(axis=0).max())
                 A["useful"] += int(live[:, P.reshape(-1)].sum())
     scale = T / pick.size
     print(f"tiles sampled {pick.size} of {T}, longest list {lens.max()} (sampled)")
@@ -203,7 +216,10 @@ def main():
     for name, A in acc.items():
         print(f"{name}: wave steps with a barrier per batch {A['iters'] * scale:.0f}, "
               f"without (lanes at their own pace) {A.get('free', 0) * scale:.0f}, " +
-              ", ".join(f"window {K}: {A.get(f'win{K}', 0) * scale:.0f}" for K in a.window))
+              ", ".join(f"window {K}: {A.get(f'win{K}', 0) * scale:.0f}" for K in a.window) +
+              "; compacted, " + ", ".join(f"window {K}: {A.get(f'cwin{K}', 0) * scale:.0f}" for K in a.window))
+        print(f"{name}: compacted staging (the wave's own records only): wave steps {A.get('cmp_iters', 0) * scale:.0f}, "
+              f"batches {A.get('cmp_batches', 0) * scale:.0f}, staged {A.get('cmp_staged', 0) * scale:.0f}")
     for name, A in acc.items():
         nw = len(lay[name]) * T
         print(f"{name:6s} {nw:6d} {A['iters'] * scale:10.0f} {A['staged'] * scale:10.0f} {A['batches'] * scale:9.0f} "

@@ -149,6 +149,34 @@ OPK2(v_pk_add_f32, "v_pk_add_f32 %0, %0, %1")
 OPK2(v_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1")
 OPK2(v_cmp_eq_u64, "v_cmp_eq_u64 s[0:1], %0, %1")
 
+// Compiler-emitted forms (no inline-asm instruction, so no per-instruction
+// s_nop pad after it: the asm OPK kernels above get an `s_nop 0` after every
+// instruction, these one per 8-chain step, the same for every op): the four
+// plain ops of the blend's record step, and fma / mul (add) alternating, at 8 waves per
+// SIMD.  Round 6: settles whether a v_fma_f32 costs twice a v_mul_f32.
+#define BIK(NAME, EXPR)                                                                \
+  __global__ __launch_bounds__(256) void bi_##NAME(float* out, unsigned long long* clk, int iters, float s) { \
+    float a[8];                                                                        \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) a[c] = (float)threadIdx.x * 1e-7f + c; \
+    const float k = s * 1e-7f;                                                         \
+    for (int i = 0; i < iters; ++i) {                                                  \
+      _Pragma("unroll") for (int u = 0; u < 16; ++u)                                   \
+      _Pragma("unroll") for (int c = 0; c < 8; ++c) {                                  \
+        const float x = a[c];                                                          \
+        a[c] = (EXPR);                                                                 \
+        asm volatile("" : "+v"(a[c]));                                                 \
+      }                                                                                \
+    }                                                                                  \
+    float r = 0.f;                                                                     \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) r += a[c];                           \
+    if (r == 12345.678f) out[threadIdx.x] = r;                                         \
+  }
+BIK(fma, __builtin_fmaf(x, s, k))
+BIK(mul, x * s)
+BIK(add, x + s)
+BIK(fma_mul, ((c & 1) ? x * s : __builtin_fmaf(x, s, k)))
+BIK(fma_add, ((c & 1) ? x + s : __builtin_fmaf(x, s, k)))
+
 template <int CH, bool PK>
 static void run(const char* name, int waves_per_simd, int iters, float* out, unsigned long long* clk, bool first) {
   const int blocks = 256 * waves_per_simd;  // 4 waves per block: one per SIMD
@@ -244,6 +272,11 @@ int main() {
   RUN_OP(v_pk_add_f32);
   RUN_OP(v_lshl_add_u64);
   RUN_OP(v_cmp_eq_u64);
+  run_op("bi_v_fma_f32", bi_fma, out, clk);
+  run_op("bi_v_mul_f32", bi_mul, out, clk);
+  run_op("bi_v_add_f32", bi_add, out, clk);
+  run_op("bi_fma_mul_alternating", bi_fma_mul, out, clk);
+  run_op("bi_fma_add_alternating", bi_fma_add, out, clk);
   std::printf("\n]\n");
   return 0;
 }

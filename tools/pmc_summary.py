@@ -2,8 +2,10 @@
 
     python tools/pmc_summary.py gpurun_out/prof [--config KEY] [--json out.json]
 
-KEY is the bench line's config.pmc_key (workload, split, band); by default it
-is read from the bench lines the profiled runs printed (<dir>/*.log).
+KEY is the bench line's config.pmc_key (workload and band shape,
+bench.pmc_key_of); by default it is read from the bench lines the profiled
+runs printed (<dir>/*.log).  The output holds {"summaries": {KEY: ...}};
+--append adds the key to an existing file (several band shapes in one).
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half of the bytes of a
@@ -54,6 +56,9 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--config", default=None)
     ap.add_argument("--json")
+    ap.add_argument("--append", action="store_true",
+                    help="add (or replace) this key's summary in an existing --json file of several "
+                         "band shapes ({\"summaries\": {key: ...}}, bench.pmc_lookup)")
     a = ap.parse_args()
     if a.config is None:
         keys = set()
@@ -89,7 +94,14 @@ def main():
             e["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
             e["smem_insts_per_wave"] = c.get("SQ_INSTS_SMEM", 0) / c["SQ_WAVES"]
         kernels[k] = e
-    out = {"config": a.config, "source": os.path.abspath(a.dir), "kernels": kernels}
+    entry = {"source": os.path.relpath(os.path.abspath(a.dir), os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+             "kernels": kernels}
+    out = {"summaries": {a.config: entry}}
+    if a.append and a.json and os.path.exists(a.json):
+        old = json.load(open(a.json))
+        prev = old.get("summaries", {old["config"]: {"kernels": old["kernels"]}} if "config" in old else {})
+        prev[a.config] = entry
+        out = {"summaries": prev}
     for k, e in kernels.items():
         keys = ["avg_us", "hbm_bytes_per_launch", "frac_wait_any", "frac_valu_active", "valu_insts_per_wave"]
         print(k, {x: (round(e[x], 3) if isinstance(e.get(x), float) else e.get(x)) for x in keys if x in e})
