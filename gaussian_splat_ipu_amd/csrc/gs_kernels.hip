@@ -26,6 +26,9 @@
 // Arithmetic: fp32 everywhere, compiled with -ffp-contract=off and the default
 // correctly rounded divide / sqrt, so every expression below performs exactly
 // the IEEE operations written (and matches the CPU oracle bit for bit).
+#include <algorithm>
+#include <vector>
+
 #include "gs_kernels.hpp"
 #include "gs_math.hpp"
 
@@ -693,7 +696,10 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
 // GS_X_BAND (measurement builds only, tools/build_x.sh; wrong frames): what
 // a row band's projection spends where.  1: every block returns after the
 // cull pass; 2: no aggregated counting (and every block reports no rendered
-// Gaussian, so the emit places nothing).
+// Gaussian, so the emit places nothing); 3: a band renderer projects only its
+// first frame, later frames reuse its records, rectangles and counters (the
+// aggregated scan keeps them): right frames for a fixed camera at no
+// projection cost -- what the projection costs the pipelined band frame.
 #ifndef GS_X_BAND
 #define GS_X_BAND 0
 #endif
@@ -768,7 +774,7 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
 // kProjAny: every path, chosen at run time.
 enum { kProjAny = 0, kProjLean = 1, kProjBand = 2 };
 template <bool P2, int MODE>
-__global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
+__device__ __forceinline__ void project_entry(FrameParams fp, const Buffers& b) {
   GS_PROBE_SCOPE(kPrProject);
   if constexpr (MODE != kProjAny) {
     fp.band_cull = MODE == kProjBand ? 1 : 0;
@@ -778,6 +784,20 @@ __global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers
     fp.bin_global = 0;
   }
   project_block<P2, MODE == kProjLean>(fp, b, blockIdx.x);
+}
+// one kernel name per kind, so a profile's per-kernel counters are the
+// kind's own (gs_frame_stats.paths bits GS_PATH_PROJ_BAND / _ANY)
+template <bool P2>
+__global__ __launch_bounds__(256) void gs_project_kernel(FrameParams fp, Buffers b) {
+  project_entry<P2, kProjLean>(fp, b);
+}
+template <bool P2>
+__global__ __launch_bounds__(256) void gs_project_band_kernel(FrameParams fp, Buffers b) {
+  project_entry<P2, kProjBand>(fp, b);
+}
+template <bool P2>
+__global__ __launch_bounds__(256) void gs_project_any_kernel(FrameParams fp, Buffers b) {
+  project_entry<P2, kProjAny>(fp, b);
 }
 
 // --------------------------------------------------------------------- scan
@@ -998,8 +1018,10 @@ __global__ __launch_bounds__(NT) void gs_agg_scan_kernel(FrameParams fp, Buffers
         s_c[j * NT + tid] = (uint32_t)vs[j] + fb[j];  // the tile's binned pairs
         s_a[j * NT + tid] = (uint32_t)vs[j];          // ... of which the aggregated workgroups'
         if (i < T) {
-          b.tile_cnt64[i] = 0ull;  // zero for the next frame's projection
-          b.tile_fb[i] = 0u;
+          if (GS_X_BAND != 3) {
+            b.tile_cnt64[i] = 0ull;  // zero for the next frame's projection
+            b.tile_fb[i] = 0u;
+          }
           b.tile_ref[i] = rf;      // the histogram (reference list lengths; the host reads it at sync)
           if (b.footer) b.footer[16 + i] = rf;
         }
@@ -3590,6 +3612,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
 // its own symbol, so the whole-frame blend does not carry the sort's ~20 KB
 // of code (the CU pair's instruction cache is shared with the other frames'
 // kernels: config 3 7 703 -> 7 839 frames/s, blend 79.2 -> 76.7 us without it)
+#ifndef GS_X_BSORT
+#define GS_X_BSORT 0
+#endif
+#if GS_X_BSORT
+__device__ uint32_t g_x_bsort_frames = 0;
+#endif
 template <bool HWEXP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WPE, 8))) void gs_blend_sort_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrBlend);
@@ -3597,10 +3625,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int slot = (int)blockIdx.x;  // (chunks_per_tile == GS_BLEND_WPG)
   if (slot >= fp.n_tiles) return;
+#if GS_X_BSORT
+  // (measurement builds: 1 = no sort after a renderer's first frames -- a
+  // fixed camera's lists are the previous frame's -- 2 = no blend walk)
+  const bool x_sort = GS_X_BSORT == 2 || __hip_atomic_load(&g_x_bsort_frames, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8u;
+  if (x_sort)
+#endif
   blend_sort_tile(fp, b, blend_tile_of(fp, b, slot), reinterpret_cast<unsigned long long*>(lds));
   // the list's stores are done (s_waitcnt in the barrier) before any wave
   // reads it, and the sort's LDS is free for the staging
   __syncthreads();
+#if GS_X_BSORT
+  if (slot == 0 && threadIdx.x == 0) atomicAdd(&g_x_bsort_frames, 1u);
+  if (GS_X_BSORT == 2) return;
+#endif
   blend_wave<4, HWEXP>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
 }
 
@@ -3667,18 +3705,30 @@ void launch_cov3d(const FrameParams& fp, const Buffers& b, hipStream_t s) {
     gs_cov3d_kernel<false><<<nb, 256, 0, s>>>(fp, b);
 }
 
+int project_kind(const FrameParams& fp, const Buffers& b) {
+  const bool plain = !fp.full_record && !(fp.sh_degree >= 0 && b.sh) && !fp.bin_global;
+  if (fp.pow2 && plain && !fp.band_cull && !fp.bin_agg) return kProjLean;
+  if (fp.pow2 && plain && fp.band_cull && fp.bin_agg) return kProjBand;
+  return kProjAny;
+}
+
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
   const int nb = (fp.n + 255) / 256;
-  const bool plain = !fp.full_record && !(fp.sh_degree >= 0 && b.sh) && !fp.bin_global;
-  if (fp.pow2 && plain && !fp.band_cull && !fp.bin_agg) {
-    gs_project_kernel<true, kProjLean><<<nb, 256, 0, s>>>(fp, b);
-  } else if (fp.pow2 && plain && fp.band_cull && fp.bin_agg) {
-    gs_project_kernel<true, kProjBand><<<nb, 256, 0, s>>>(fp, b);
+  const int kind = project_kind(fp, b);
+  if (kind == kProjLean) {
+    gs_project_kernel<true><<<nb, 256, 0, s>>>(fp, b);
+  } else if (kind == kProjBand) {
+    if (GS_X_BAND == 3) {  // (measurement builds: one projection per renderer)
+      static std::vector<const void*> seen;
+      if (std::find(seen.begin(), seen.end(), (const void*)b.rec) != seen.end()) return;
+      seen.push_back(b.rec);
+    }
+    gs_project_band_kernel<true><<<nb, 256, 0, s>>>(fp, b);
   } else if (fp.pow2) {
-    gs_project_kernel<true, kProjAny><<<nb, 256, 0, s>>>(fp, b);
+    gs_project_any_kernel<true><<<nb, 256, 0, s>>>(fp, b);
   } else {
-    gs_project_kernel<false, kProjAny><<<nb, 256, 0, s>>>(fp, b);
+    gs_project_any_kernel<false><<<nb, 256, 0, s>>>(fp, b);
   }
 }
 

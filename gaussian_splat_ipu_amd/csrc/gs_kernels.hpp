@@ -213,6 +213,9 @@ size_t bin_lds_bytes(int n_tiles);
 bool bin_lds_fits(int n_tiles);
 hipError_t init_kernel_attributes();
 
+// the projection's instantiation for fp: 1 = a whole frame's lean one
+// (gs_project), 2 = a row band's (gs_project_band), 0 = every path (gs_project_any)
+int project_kind(const FrameParams& fp, const Buffers& b);
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s);
 // the 3D covariances of the scene for fp's fxy[1] into Buffers::cov3
 void launch_cov3d(const FrameParams& fp, const Buffers& b, hipStream_t s);

@@ -597,7 +597,9 @@ int finish_frame(gs_renderer* r) {
                                  (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u) |
                                  (r->last_fp.blend_px2 ? GS_PATH_BLEND_PX2 : 0u) |
                                  (r->last_fp.lazy ? GS_PATH_LAZY : 0u) |
-                                 (r->last_fp.big_separate ? GS_PATH_BIG_LISTS : 0u))
+                                 (r->last_fp.big_separate ? GS_PATH_BIG_LISTS : 0u) |
+                                 (gsk::project_kind(r->last_fp, r->buf) == 2 ? GS_PATH_PROJ_BAND : 0u) |
+                                 (gsk::project_kind(r->last_fp, r->buf) == 0 ? GS_PATH_PROJ_ANY : 0u))
                               : 0u;
   r->stats.blend_records = r->stats.blend_cont_records = r->stats.cont_keys = 0;
   r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = r->stats.cont_full_sorts = 0;
