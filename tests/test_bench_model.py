@@ -185,8 +185,12 @@ def test_round_pmc_holds_the_default_kernels(pmc, paths):
     if not os.path.exists(pp):
         pytest.skip("round-end profiles not present")
     files = [pp] + ([os.path.join(ROOT, "profiles", "pmc_latest.json")] if pmc == "pmc_c3.json" else [])
+    key = bench.pmc_key_of("c3" if pmc == "pmc_c3.json" else "c5", 1_000_000 if pmc == "pmc_c3.json" else 8_000_000,
+                           1920 if pmc == "pmc_c3.json" else 3840, 1080 if pmc == "pmc_c3.json" else 2160, 16, 0, 0)
     for f in files:
-        kernels = json.load(open(f))["kernels"]
+        d = json.load(open(f))
+        # (the several-shape form keyed by bench.pmc_key_of, or round 5's one-summary form)
+        kernels = bench.pmc_lookup(f, key)["kernels"] if "summaries" in d else d["kernels"]
         for stage in ("project", "scan", "emit", "sort", "blend") + (("blend_cont",) if paths & bench.PATH_LAZY else ()):
             _, _, missing = bench.stage_pmc(stage, paths, kernels)
             assert not missing, (f, stage, missing)

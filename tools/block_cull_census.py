@@ -1,11 +1,11 @@
-"""Band block-list census (CPU, oracle data): how many 256-Gaussian blocks
-(device = 3D Morton order) gs_block_list_kernel's per-block bound keeps for
-each row band, and a soundness check of that bound against the oracle's
-rectangles (no Gaussian of a culled block may have a tile row in the band).
-The bound is restated in float64 as the (measured and dropped)
-gs_block_list_kernel had it.
+"""Band group-cull census (CPU, oracle data): how many groups of Gaussians
+(device = 3D Morton order; 64 = a projection wave's, gs_kernels.hip
+group_culled) the per-group bound keeps for each row band, and a soundness
+check of that bound against the oracle's rectangles (no Gaussian of a culled
+group may have a tile row in the band).  The bound is restated in float64 as
+group_culled has it.
 
-  python tools/block_cull_census.py [--n 1000000] [--bands 8]
+  python tools/block_cull_census.py [--n 1000000] [--group 64] [--bands ...]
 """
 import argparse
 import json
@@ -32,16 +32,34 @@ def morton_perm(mean):
     return np.lexsort((np.arange(mean.shape[0]), key))
 
 
+def spectral_norm2_bound(m):
+    """gs_renderer.hip spectral_norm2_bound: >= ||W||_2^2, W the mvp's upper 3x3."""
+    W = np.array([[m[i * 4 + k] for k in range(3)] for i in range(3)], np.float64)
+    A = W @ W.T
+    tr = np.trace(A)
+    L = math.log(tr)
+    A = A / tr
+    for _ in range(6):
+        B = A @ A
+        t = np.trace(B)
+        L = 2 * L + math.log(t)
+        A = B / t
+    return float(np.nextafter(np.float32(math.exp(L / 64) * (1 + 1e-9)), np.float32(np.inf)))
+
+
 def block_culled(m, lo, hi, fp):
-    """m: the mvp as 16 floats, glm column-major (m[c * 4 + r])."""
+    """gs_kernels.hip group_culled, restated in float64 (the kernel's float
+tail with its margins).  m: the mvp as 16 floats, glm
+    column-major (m[c * 4 + r])."""
     if not (hi[3] < math.inf) or not (fp["scale_div"] > 0):
         return False
-    vmin, vmax, tzmin = 1e300, -1e300, 1e300
+    vmin, vmax, tzmin, rx, ry = 1e300, -1e300, 1e300, 0.0, 0.0
     pos = neg = True
     for c in range(8):
         x = hi[0] if c & 1 else lo[0]
         y = hi[1] if c & 2 else lo[1]
         z = hi[2] if c & 4 else lo[2]
+        tx = (m[0] * x + m[4] * y) + (m[8] * z + m[12])
         cy = (m[1] * x + m[5] * y) + (m[9] * z + m[13])
         cw = (m[3] * x + m[7] * y) + (m[11] * z + m[15])
         tz = (m[2] * x + m[6] * y) + (m[10] * z + m[14])
@@ -53,16 +71,20 @@ def block_culled(m, lo, hi, fp):
         pos = pos and tz > 0
         neg = neg and tz < 0
         tzmin = min(tzmin, abs(tz))
+        if tz != 0:
+            rx, ry = max(rx, abs(tx) / abs(tz)), max(ry, abs(cy) / abs(tz))
     if not (pos or neg) or not tzmin > 0:
         return False
     lim = 1.3 * fp["tanfov"]
     fx, fy = fp["focal_x"], fp["focal_y"]
-    j2 = (fx * fx + fy * fy) * (1 + lim * lim) / (tzmin * tzmin)
-    lc = math.exp(2.0 * (hi[3] / fp["scale_div"])) * 1.01
-    r = 3.0 * math.sqrt(1.05 * (2.0 * lc * fp["wnorm2"] * j2) + 1.0) + 2.0
+    cx, cyy = min(lim, rx * 1.001), min(lim, ry * 1.001)
+    j2 = (fx * fx * (1 + cx * cx) + fy * fy * (1 + cyy * cyy)) / (tzmin * tzmin)
+    lc = math.exp(2.0 * (hi[3] / fp["scale_div"])) * 1.02
+    r = 3.0 * math.sqrt(1.05 * (lc * fp["wnorm2"] * j2) + 1.0) + 2.0
     av = max(abs(vmin), abs(vmax))
-    r = r * 1.02 + 1.0 + 1e-4 * av + 1.0
-    if not (r < 1e12 and av < 1e12):
+    r = r * fp.get("rscale", 1.0)
+    r = r * 1.02 + 2.0 + 1e-4 * av + 1.0
+    if not (r < 1e6 and av < 1e6):
         return False
     th = fp["th"]
     fy0 = math.floor(math.floor(vmin - r) / th)
@@ -77,6 +99,8 @@ def block_culled(m, lo, hi, fp):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--group", type=int, default=64, help="Gaussians per bound (256: a projection block, 64: a wave)")
+    ap.add_argument("--rscale", type=float, default=1.0, help="(estimates only, unsound below 1) radius bound scale")
     ap.add_argument("--bands", default="0,18,23,29,34,39,44,50,68",
                     help="band boundaries in tile rows (default: round 5's balanced 8-band split)")
     a = ap.parse_args()
@@ -99,16 +123,17 @@ def main():
                 s = np.float32(s + np.float32(pj[k][r_] * vw[c][k]))
             mvp[c][r_] = s
     m = [float(x) for x in mvp.reshape(16)]
-    w2 = sum(m[c * 4 + r_] ** 2 for c in range(3) for r_ in range(3)) * 1.0001
+    w2 = spectral_norm2_bound(m)
     tf = math.tan(camera.FOV_DEFAULT / 2)
     fp = dict(H=float(H), th=float(TW), tiles_y=-(-H // TW), scale_div=1.0, tanfov=math.tan(0.5 * camera.FOV_DEFAULT),
-              focal_x=W / (2 * tf), focal_y=H / (2 * tf), wnorm2=w2)
+              focal_x=W / (2 * tf), focal_y=H / (2 * tf), wnorm2=w2, rscale=a.rscale)
     cr_w = np.where(G[:, 15] <= 0, np.nan, np.where(G[:, 3] != 1.0, np.inf, G[:, 12:15].max(axis=1)))
-    nb = (a.n + 255) // 256
+    G_ = a.group
+    nb = (a.n + G_ - 1) // G_
     lo = np.zeros((nb, 3))
     hi = np.zeros((nb, 4))
     for k in range(nb):
-        idx = perm[k * 256:(k + 1) * 256]
+        idx = perm[k * G_:(k + 1) * G_]
         mm = G[idx, 0:3]
         sw = cr_w[idx]
         lo[k] = mm.min(axis=0)
@@ -124,12 +149,12 @@ def main():
         bad = 0
         for k in range(nb):
             if block_culled(m, lo[k], hi[k], fp):
-                idx = perm[k * 256:(k + 1) * 256]
+                idx = perm[k * G_:(k + 1) * G_]
                 hit = live[idx] & (rows0[idx] <= b[i + 1] - 1) & (rows1[idx] >= b[i])
                 bad += int(hit.sum())
             else:
                 kept += 1
-        out.append(dict(band=[b[i], b[i + 1]], blocks_kept=kept, frac_kept=round(kept / nb, 3), unsound=bad))
+        out.append(dict(band=[b[i], b[i + 1]], group=G_, blocks_kept=kept, frac_kept=round(kept / nb, 3), unsound=bad))
         print(json.dumps(out[-1]), flush=True)
 
 

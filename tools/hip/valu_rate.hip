@@ -176,6 +176,32 @@ BIK(mul, x * s)
 BIK(add, x + s)
 BIK(fma_mul, ((c & 1) ? x * s : __builtin_fmaf(x, s, k)))
 BIK(fma_add, ((c & 1) ? x + s : __builtin_fmaf(x, s, k)))
+// the operand kinds (round 6): a per-lane (VGPR) multiplier, an inline
+// constant, a literal; fma with every source a VGPR
+#define BIV(NAME, EXPR)                                                                \
+  __global__ __launch_bounds__(256) void bv_##NAME(float* out, unsigned long long* clk, int iters, float s) { \
+    float a[8];                                                                        \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) a[c] = (float)threadIdx.x * 1e-7f + c; \
+    float v = s * (1.0f + (float)threadIdx.x * 1e-9f), w = v * 1e-7f;                   \
+    asm volatile("" : "+v"(v), "+v"(w));                                               \
+    for (int i = 0; i < iters; ++i) {                                                  \
+      _Pragma("unroll") for (int u = 0; u < 16; ++u)                                   \
+      _Pragma("unroll") for (int c = 0; c < 8; ++c) {                                  \
+        const float x = a[c];                                                          \
+        a[c] = (EXPR);                                                                 \
+        asm volatile("" : "+v"(a[c]));                                                 \
+      }                                                                                \
+    }                                                                                  \
+    float r = 0.f;                                                                     \
+    _Pragma("unroll") for (int c = 0; c < 8; ++c) r += a[c];                           \
+    if (r == 12345.678f) out[threadIdx.x] = r;                                         \
+  }
+BIV(mul_vgpr, x * v)
+BIV(add_vgpr, x + v)
+BIV(mul_inline, x * 0.5f)
+BIV(mul_literal, x * 0.99987f)
+BIV(fma_vgpr, __builtin_fmaf(x, v, w))
+BIV(min_vgpr, __builtin_fminf(x, v))
 
 template <int CH, bool PK>
 static void run(const char* name, int waves_per_simd, int iters, float* out, unsigned long long* clk, bool first) {
@@ -277,6 +303,12 @@ int main() {
   run_op("bi_v_add_f32", bi_add, out, clk);
   run_op("bi_fma_mul_alternating", bi_fma_mul, out, clk);
   run_op("bi_fma_add_alternating", bi_fma_add, out, clk);
+  run_op("bv_v_mul_f32_vgpr", bv_mul_vgpr, out, clk);
+  run_op("bv_v_add_f32_vgpr", bv_add_vgpr, out, clk);
+  run_op("bv_v_mul_f32_inline", bv_mul_inline, out, clk);
+  run_op("bv_v_mul_f32_literal", bv_mul_literal, out, clk);
+  run_op("bv_v_fma_f32_vgpr", bv_fma_vgpr, out, clk);
+  run_op("bv_v_min_f32_vgpr", bv_min_vgpr, out, clk);
   std::printf("\n]\n");
   return 0;
 }
