@@ -189,11 +189,6 @@ __device__ __forceinline__ void band_rows_of(const FrameParams& fp, float fy0, f
 // The bound is inflated by 5 % + 2 px against fp32 rounding, and the tile-row
 // range is computed with the rectangle's own (monotone) formulas from the same
 // vy, so it contains the true rows.  Non-finite values never cull.
-// GS_X_GROUP (measurement builds only, tools/build_x.sh): 1 = no per-group
-// cull in the band projection; 2 = that and the rounds 2-5 factor 2
-#ifndef GS_X_GROUP
-#define GS_X_GROUP 0
-#endif
 template <bool P2>
 __device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, const M3& T, float4 sg,
                                             float extra = 0.0f) {
@@ -204,7 +199,7 @@ __device__ __forceinline__ bool band_culled(const FrameParams& fp, float vy, con
     for (int r = 0; r < 3; ++r) t2 += T.m[c][r] * T.m[c][r];
   const float smax = div_p2<P2>(fmaxf(fmaxf(sg.x, sg.y), sg.z), fp.scale_div, fp.inv_sd);
   const float lc = __expf(2.0f * smax) * 1.01f;
-  const float r = 3.0f * __builtin_sqrtf(1.05f * ((GS_X_GROUP == 2 ? 2.0f : 1.0f) * lc * t2) + 1.0f) + 2.0f + extra;
+  const float r = 3.0f * __builtin_sqrtf(1.05f * (lc * t2) + 1.0f) + 2.0f + extra;
   if (!(__builtin_fabsf(vy) < 1e30f) || !(r < 1e30f)) return false;
   const float fy0 = __builtin_floorf(div_p2<P2>(__builtin_floorf(vy - r), fp.th, fp.inv_th));
   const float fy1 = __builtin_floorf(div_p2<P2>(__builtin_ceilf(vy + r), fp.th, fp.inv_th));
@@ -253,72 +248,6 @@ __device__ __forceinline__ bool band_culled_fast(const FrameParams& fp, float4 c
 #pragma unroll
     for (int r = 0; r < 3; ++r) W.m[c][r] = m[c * 4 + r];
   return band_culled<P2>(fp, vy, m3_mul(W, J), sg, 1e-5f * __builtin_fabsf(vy) + 0.05f);
-}
-
-// The band cull per group of 64 Gaussians (a projection wave's, device order),
-// before any of them is read: true when none of them can have a tile row in
-// this band.  From Buffers::group_bounds (the box of the group's means, its
-// largest log-scale; +inf: never culled) and band_culled's bound taken over
-// the box.  Over a box with clip w > 0 at every corner, vy = cy / cw and
-// tx / tz, ty / tz are linear-fractional in the mean, so their extremes are
-// corners'; with one sign of the clip-space t_z at every corner its smallest
-// |t_z| is a corner's too.  ||T||_F = ||W J||_F <= ||W||_2 ||J||_F
-// (FrameParams::wnorm2 >= ||W||_2^2, from the host) and
-// ||J||_F^2 = (fx^2 (1 + clamp(tx/tz)^2) + fy^2 (1 + clamp(ty/tz)^2)) / t_z^2.
-// The corners' clip coordinates in double (no cancellation), rounded to
-// float (2^-24 relative each); the rest in float with v_rcp / v_exp / v_sqrt
-// (a few ulp each), covered by inflating the radius by 2 % + 2 px and vy by
-// 1e-4 |vy| + 1 px.  A box with a corner at w <= 0 or a t_z sign change, or
-// beyond 1e6 px, is never culled.  Each lane evaluates corner lane & 7; the
-// result is wave-uniform.  (tools/block_cull_census.py checks the bound
-// against the oracle's rectangles; round 6's first, all-double version cost
-// the band projection 18.7 -> 25.3 us.)
-__device__ __forceinline__ bool group_culled(const FrameParams& fp, float4 lo, float4 hi) {
-  if (!(hi.w < __builtin_huge_valf()) || !(fp.scale_div > 0.0f) || !(fp.wnorm2 > 0.0f)) return false;
-  const int c = threadIdx.x & 7;
-  const float* m = fp.mvp;
-  const double x = (c & 1) ? hi.x : lo.x, y = (c & 2) ? hi.y : lo.y, z = (c & 4) ? hi.z : lo.z;
-  const double dw = __builtin_fma((double)m[3], x, __builtin_fma((double)m[7], y, __builtin_fma((double)m[11], z, (double)m[15])));
-  const double wmag = __builtin_fma(__builtin_fabs((double)m[3]), __builtin_fabs(x),
-                      __builtin_fma(__builtin_fabs((double)m[7]), __builtin_fabs(y),
-                      __builtin_fma(__builtin_fabs((double)m[11]), __builtin_fabs(z), __builtin_fabs((double)m[15]))));
-  const float tx = (float)__builtin_fma((double)m[0], x, __builtin_fma((double)m[4], y, __builtin_fma((double)m[8], z, (double)m[12])));
-  const float ty = (float)__builtin_fma((double)m[1], x, __builtin_fma((double)m[5], y, __builtin_fma((double)m[9], z, (double)m[13])));
-  const float tz = (float)__builtin_fma((double)m[2], x, __builtin_fma((double)m[6], y, __builtin_fma((double)m[10], z, (double)m[14])));
-  const float cw = (float)dw;
-  const bool bad = !(dw > 1e-9 * wmag) || !(cw > 1e-30f);
-  const unsigned long long c8 = 0xFFull;
-  if ((ballot64(bad) & c8) != 0ull) return false;
-  const bool pos = (ballot64(tz > 1e-30f) & c8) == c8, neg = (ballot64(tz < -1e-30f) & c8) == c8;
-  if (!(pos || neg)) return false;
-  float v0 = (ty * __builtin_amdgcn_rcpf(cw) * 0.5f + 0.5f) * fp.H, v1 = v0;
-  float az = __builtin_fabsf(tz);
-  const float iz = __builtin_amdgcn_rcpf(az);
-  float rx = __builtin_fabsf(tx) * iz, ry = __builtin_fabsf(ty) * iz;
-#pragma unroll
-  for (int d = 1; d < 8; d <<= 1) {
-    v0 = fminf(v0, __shfl_xor(v0, d, 64));
-    v1 = fmaxf(v1, __shfl_xor(v1, d, 64));
-    az = fminf(az, __shfl_xor(az, d, 64));
-    rx = fmaxf(rx, __shfl_xor(rx, d, 64));
-    ry = fmaxf(ry, __shfl_xor(ry, d, 64));
-  }
-  const float lim = 1.3f * fp.tanfov;
-  const float cx = fminf(lim, rx * 1.001f), cy = fminf(lim, ry * 1.001f);
-  const float iaz = __builtin_amdgcn_rcpf(az);
-  const float j2 = (fp.focal_x * fp.focal_x * (1.0f + cx * cx) + fp.focal_y * fp.focal_y * (1.0f + cy * cy)) * (iaz * iaz);
-  const float lc = __expf(2.0f * (hi.w * __builtin_amdgcn_rcpf(fp.scale_div))) * 1.02f;
-  float r = 3.0f * __builtin_sqrtf(1.05f * (lc * fp.wnorm2 * j2) + 1.0f) + 2.0f;
-  const float av = fmaxf(__builtin_fabsf(v0), __builtin_fabsf(v1));
-  r = r * 1.02f + 2.0f + 1e-4f * av + 1.0f;
-  if (!(r < 1e6f) || !(av < 1e6f)) return false;
-  const float ith = __builtin_amdgcn_rcpf(fp.th);
-  const float fy0 = __builtin_floorf(__builtin_floorf(v0 - r) * ith);
-  const float fy1 = __builtin_floorf(__builtin_ceilf(v1 + r) * ith);
-  if (fy1 < 0.0f || fy0 > (float)(fp.tiles_y - 1)) return true;  // off the frame's tile rows
-  int yb0, yb1;
-  band_rows_of<false>(fp, fy0, fy1, yb0, yb1);
-  return yb0 > yb1;
 }
 
 // gs_set_sh (opt-in, not in the reference: its loader reads
@@ -796,13 +725,10 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
     // (Per-block bounds before any Gaussian is read did not pay: DESIGN.md
     // §4 "Tried and dropped", the two round-2 block-test entries, and §0's
     // round-5 block list -- a launch projecting only the listed blocks)
-    // first the wave's 64 Gaussians at once (group_culled, from the group's
-    // bound: no per-Gaussian read), then each of a live group's
-    const int g = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    // (a per-wave test of the 64 Gaussians' bound before any of them is read,
+    // round 6: slower -- DESIGN.md section 4 "Tried and dropped")
     bool culled = true;
-    if (g * 64 < fp.n && !(GS_X_GROUP == 0 && b.group_bounds &&
-                           group_culled(fp, b.group_bounds[2 * g], b.group_bounds[2 * g + 1])) &&
-        i < fp.n) {
+    if (i < fp.n) {
       // one 16-B load (the mean and the largest scale) instead of two
       const float4 cr = b.cull[i];
       culled = !__builtin_isnan(cr.w) && band_culled_fast<P2>(fp, cr);

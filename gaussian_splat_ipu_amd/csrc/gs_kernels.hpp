@@ -45,7 +45,6 @@ struct FrameParams {
   int tiles_y;        // tile rows of the whole frame
   int band_rows;      // pixel rows of this band's output
   int band_cull;      // skip Gaussians whose extent bound misses the band (GS_FLAG_BAND_CULL)
-  float wnorm2;       // >= ||W||_2^2, W the mvp's upper 3x3 (the band cull's per-group bound)
   int n;              // Gaussians
   int n_tiles;        // tiles_x * (band_ty1 - band_ty0)
   int chunks_per_tile;  // blend waves per tile (16 pixel quads each)
@@ -105,9 +104,6 @@ struct Buffers {
   const float4* scale_gid;  // sx sy sz gid
   const float4* cull;       // band cull: mean xyz + largest log-scale (NaN: empty slot, inf: never culled)
   const float4* mean_op;    // mean xyz + opacity (FrameParams::mean_w1: every mean's w is 1)
-  const float4* group_bounds;  // [2 x ceil(n / 64)] per 64 Gaussians (device order): the box of
-                               //   their means (lo xyz, 0 | hi xyz, largest log-scale; +inf: the
-                               //   group is never culled) -- the band cull's group_culled
   float* cov3;              // [9][n] per Gaussian: ComputeCov3D's 9 entries (m[c][r] at c * 3 + r),
                             //   SoA (FrameParams::cov_cache; static per fxy[1]); an empty slot
                             //   (gid <= 0) has m[2][2] = -1, a live one's is >= +0 or NaN

@@ -30,47 +30,8 @@ namespace {
 // scene allocation: the 64-B records (SoA), the permutation both ways, then
 // the band cull's 16-B records (16-B aligned)
 size_t cull_offset(size_t nn) { return (nn * (64 + 8) + 15) / 16 * 16; }
-// + the band cull's records (16 B) + mean xyz with the opacity (16 B), then
-// the band cull's group bounds (32 B per 64 Gaussians)
-size_t bounds_offset(size_t nn) { return cull_offset(nn) + nn * 32; }
-size_t scene_bytes(size_t nn) { return bounds_offset(nn) + (nn + 63) / 64 * 32; }
-
-// An upper bound on ||W||_2^2, W the upper 3x3 of the mvp (column-major,
-// m[c * 4 + r]): lambda_max(A) <= trace(A^64)^(1/64) for A = W^T W >= 0, at
-// most 3^(1/64) = 1.7 % above it (six squarings of A / trace(A) in double),
-// rounded up.  The band cull's group bound (gs_kernels.hip group_culled).
-float spectral_norm2_bound(const float* m) {
-  double A[3][3];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      double t = 0.0;
-      for (int k = 0; k < 3; ++k) t += (double)m[i * 4 + k] * (double)m[j * 4 + k];
-      A[i][j] = t;
-    }
-  const double tr = A[0][0] + A[1][1] + A[2][2];
-  if (!(tr > 0.0) || !(tr < 1e30)) return 0.0f;  // (0: the group cull stays off)
-  double log_scale = std::log(tr);
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) A[i][j] /= tr;
-  for (int s = 0; s < 6; ++s) {  // A <- (A / trace(A))^2, the trace's log kept
-    double B[3][3];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        double t = 0.0;
-        for (int k = 0; k < 3; ++k) t += A[i][k] * A[k][j];
-        B[i][j] = t;
-      }
-    const double t = B[0][0] + B[1][1] + B[2][2];
-    if (!(t > 0.0)) return 0.0f;
-    log_scale = 2.0 * log_scale + std::log(t);
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) A[i][j] = B[i][j] / t;
-  }
-  // trace(A_0^64) = exp(log_scale) (the last normalised A has trace 1)
-  const double l = std::exp(log_scale / 64.0) * (1.0 + 1e-9);
-  const float f = (float)l;
-  return std::nextafter(f, INFINITY);
-}
+// + the band cull's records (16 B) + mean xyz with the opacity (16 B)
+size_t scene_bytes(size_t nn) { return cull_offset(nn) + nn * 32; }
 }  // namespace
 
 namespace gsr {
@@ -289,7 +250,6 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   fp.tiles_y = r->tiles_y;
   fp.band_rows = r->band_rows;
   fp.band_cull = ((r->cfg.flags & GS_FLAG_BAND_CULL) && r->band_nrows < r->tiles_y) ? 1 : 0;
-  fp.wnorm2 = fp.band_cull ? spectral_norm2_bound(fp.mvp) : 0.0f;
   fp.n = (int)r->n;
   fp.n_tiles = r->n_tiles;
   // blend: one wave per 16 pixel quads -- an 8x8 or 16x4 pixel block when the
@@ -915,39 +875,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
         w1 = w1 && s[3] == 1.0f;
       }
       r->scene_w1 = w1;
-      // the band cull's group bounds (group_culled): per 64 consecutive
-      // Gaussians of the device order, the box of their means and their
-      // largest log-scale, from the cull records; an empty slot (NaN) is never
-      // rendered and stays out of the box, a mean with w != 1 (+inf) or a
-      // non-finite value makes the group never culled (+inf)
-      for (size_t k = 0; k < (nn + 63) / 64; ++k) {
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        bool never = false;
-        for (size_t i = k * 64; i < std::min(n, k * 64 + 64); ++i) {
-          const float* cr = soa + cull_offset(nn) / 4 + 4 * i;
-          if (std::isnan(cr[3])) continue;
-          if (!(std::isfinite(cr[0]) && std::isfinite(cr[1]) && std::isfinite(cr[2]) && std::isfinite(cr[3]))) {
-            never = true;
-            break;
-          }
-          for (int c = 0; c < 3; ++c) {
-            lo[c] = std::min(lo[c], cr[c]);
-            hi[c] = std::max(hi[c], cr[c]);
-          }
-          hi[3] = std::max(hi[3], cr[3]);
-        }
-        float* bb = soa + bounds_offset(nn) / 4 + 8 * k;
-        if (!never && !(hi[3] > -INFINITY)) {  // only empty slots: a point box, the smallest scale
-          for (int c = 0; c < 3; ++c) lo[c] = hi[c] = 0.0f;
-          hi[3] = -INFINITY;
-        }
-        for (int c = 0; c < 3; ++c) {
-          bb[c] = lo[c];
-          bb[4 + c] = hi[c];
-        }
-        bb[3] = 0.0f;
-        bb[7] = never ? INFINITY : hi[3];
-      }
       e = hipMemcpy(r->d_scene, soa, scene_bytes(nn), hipMemcpyHostToDevice);
       (void)hipHostFree(soa);
       if (e != hipSuccess) return fail(hip_fail(e, "hipMemcpy(scene)"));
@@ -961,7 +888,6 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   r->buf.perm = (const uint32_t*)(sc + 4 * nn);
   r->buf.cull = (const float4*)((const char*)r->d_scene + cull_offset(nn));
   r->buf.mean_op = r->buf.cull + nn;
-  r->buf.group_bounds = (const float4*)((const char*)r->d_scene + bounds_offset(nn));
   r->buf.inv_perm = r->buf.perm + nn;
 
   // per Gaussian: 48 B of record (frames: the 32-B record the blend reads and,
