@@ -8,7 +8,7 @@
 namespace gsk {
 
 // Per-frame constants, passed by value as kernel arguments.
-// Timeline probe builds (-DGS_PROBE=1, tools/build_variant.sh; never the
+// Timeline probe builds (-DGS_PROBE=1, tools/build_x.sh; never the
 // default library): every kernel records, per frame, its first wave's start
 // and its last wave's end (wall_clock64, 100 MHz), for tools/probe_timeline.py
 #ifndef GS_PROBE

@@ -227,3 +227,28 @@ def test_committed_lines_use_the_survey_terms():
         dk = d["kernels"][r["kernel"]]
         assert r["alg_bytes_per_launch"] == dk["alg_bytes"], p
         assert abs(r["frac"] - dk["alg_bytes"] / (dk["avg_ms"] * 1e-3) / 8e12) < 2e-3, p
+
+
+@pytest.mark.parametrize("bands,paths", [
+    (8, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_PROJ_BAND),
+    (4, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_PROJ_BAND),
+    (2, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_PROJ_BAND),
+    (1, bench.PATH_BLEND_PX2),  # bench.py --gather: the one-GPU group renders the whole frame as band 0 of 1
+])
+def test_group_line_shapes_resolve_traffic_and_valu(bands, paths):
+    """A --gpus N line (rank 0 renders band 0 of N) and the one-GPU group line
+    (--gather) find their band shape's PMC summary in the bench's default file
+    (bench.pmc_key_of, profiles/pmc_latest.json from tools/r6/pmc_bands.sh), so
+    every launched stage has non-null traffic and the blend a VALU fraction."""
+    key = bench.pmc_key_of("c3", 1_000_000, 1920, 1080, 16, bands, 0)
+    pm = bench.pmc_lookup(os.path.join(ROOT, "profiles", "pmc_latest.json"), key)
+    assert pm is not None, key
+    kernels = pm["kernels"]
+    for stage in ("project", "scan", "emit", "sort", "blend"):
+        if not bench.stage_kernels(stage, paths):
+            continue  # (a band's tile sort runs inside its blend)
+        hb, vi, missing = bench.stage_pmc(stage, paths, kernels)
+        assert not missing and hb and hb > 0 and vi, (key, stage, missing)
+    cpi = json.load(open(os.path.join(ROOT, "profiles", "valu_cpi.json")))
+    cyc, used = bench.stage_valu_cycles("blend", paths, kernels, cpi)
+    assert cyc is not None and cyc > 0, (key, used)

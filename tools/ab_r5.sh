@@ -1,6 +1,6 @@
 #!/bin/bash
 # Interleaved A/B of the in-tree library against tmp_ab/<name>/libgsplat.so
-# variants (tools/build_variant.sh): the GPU parity tests once per variant
+# variants (tools/build_x.sh <name> "-D..."): the GPU parity tests once per variant
 # (first failure stops it), then REPEATS rounds of a bench line per library,
 # libraries interleaved within a round.  BENCH_ARGS adds bench.py flags.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1

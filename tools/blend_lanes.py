@@ -1,7 +1,7 @@
 """Kernel-counted blend lane utilisation (GPU; a GS_LANES build, never the
 default library).  Builds nothing itself: build the counting library here with
 
-  ABDIR=tmp_ab_l bash tools/build_variant.sh lanes tools/lanes_edit.py
+  ABDIR=tmp_ab_l bash tools/build_x.sh lanes "-DGS_LANES=1"
 
 then on the GPU box
 

@@ -1,4 +1,4 @@
-"""Kernel timeline of a probe build (tools/edit_probe.py): per frame and
+"""Kernel timeline of a probe build (bash tools/build_x.sh probe "-DGS_PROBE=1"): per frame and
 kernel, the first wave's start and the last wave's end on the GPU's 100 MHz
 wall clock -- without a profiler in the process, so frames in flight overlap
 as they do in the bench.
