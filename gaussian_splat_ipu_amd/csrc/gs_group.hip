@@ -1092,7 +1092,9 @@ int read_tile_histogram(Group* g, uint32_t* dst, size_t n) {
 int get_stats(Group* g, gs_frame_stats* st) {
   std::lock_guard<std::mutex> lk(g->hist_mu);
   *st = g->stats;
-  // the profiled band renderer's own counts (this rank's band)
+  // the profiled band renderer's own counts (this rank's band), and the
+  // kernels its frames launch (the footers carry no paths)
+  st->paths = gsr::frame_paths(g->mem[0].slot[0]);
   st->blend_records = g->mem[0].slot[0]->stats.blend_records;
   st->blend_cont_records = g->mem[0].slot[0]->stats.blend_cont_records;
   st->cont_keys = g->mem[0].slot[0]->stats.cont_keys;

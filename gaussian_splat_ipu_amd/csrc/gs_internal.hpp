@@ -124,6 +124,7 @@ struct gs_renderer {
   size_t bcount_words = 0;
   bool last_counted = false;   // the last enqueued frame counted its blend records
   uint64_t frame_seq = 0;
+  uint64_t x_frames = 0;  // (GS_X_BAND measurement builds only: this renderer's frames)
   gsr::ProfileSlot ring[gsr::kProfileRing];
   int ring_head = 0;
   double k_ms[GS_K_COUNT] = {0};
@@ -152,6 +153,7 @@ void destroy(gs_renderer* r);
 int set_band_rows(gs_renderer* r, int ty0, int ty1, int pad_rows);
 int enqueue_frame(gs_renderer* r);
 int finish_frame(gs_renderer* r);
+uint32_t frame_paths(const gs_renderer* r);  // gs_frame_stats.paths of the last enqueued frame
 // after GS_EOVERFLOW: grow the pair buffers to hold the last frame's pairs
 // (force: at least double them, even if the last frame fit)
 int grow_pairs(gs_renderer* r, bool force);

@@ -2906,10 +2906,27 @@ struct Px {
   bool done;
 };
 
+// GS_X_EXPM (measurement builds, tools/build_x.sh): 1 = rint and the integer
+// exponent from the magic-number addition
+#ifndef GS_X_EXPM
+#define GS_X_EXPM 0
+#endif
 __device__ __forceinline__ float gs_expf_inrange(float x) {
   // gs_expf for x in [-80, 0]: the same ops minus the clamps / selects, which
   // are no-ops there.  Outside that range the result is unused (selected away).
+#if GS_X_EXPM
+  // rint by the 1.5 * 2^23 addition (exact for |t| < 2^22, ties to even as
+  // v_rndne_f32), and the integer k from the sum's low mantissa bits: two
+  // full-rate adds and an integer add instead of v_rndne and v_cvt_i32
+  // (~4.1 SIMD cycles each), the same values
+  const float t = x * 1.44269502162933349609f;
+  const float sm = t + 12582912.0f;
+  const float k = sm - 12582912.0f;
+  const int ki = (int)(__float_as_uint(sm) - 0x4B400000u);
+#else
   const float k = __builtin_rintf(x * 1.44269502162933349609f);
+  const int ki = (int)k;
+#endif
   float r = __builtin_fmaf(k, -0.693145751953125f, x);
   r = __builtin_fmaf(k, -1.428606765330187045e-06f, r);
   float p = 1.9875691500e-4f;
@@ -2921,7 +2938,7 @@ __device__ __forceinline__ float gs_expf_inrange(float x) {
   const float r2 = r * r;
   p = __builtin_fmaf(p, r2, r);
   p = p + 1.0f;
-  return __builtin_amdgcn_ldexpf(p, (int)k);  // == p * 2^k: k in [-115, 0], p in [0.7, 1.5]
+  return __builtin_amdgcn_ldexpf(p, ki);  // == p * 2^k: k in [-115, 0], p in [0.7, 1.5]
 }
 
 // GS_FLAG_FAST_EXP: e^x = 2^t with t = x log2(e) split into t + lo by an fma

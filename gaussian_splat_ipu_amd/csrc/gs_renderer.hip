@@ -34,6 +34,10 @@ size_t cull_offset(size_t nn) { return (nn * (64 + 8) + 15) / 16 * 16; }
 size_t scene_bytes(size_t nn) { return cull_offset(nn) + nn * 32; }
 }  // namespace
 
+#ifndef GS_X_BAND
+#define GS_X_BAND 0
+#endif
+
 namespace gsr {
 
 int hip_fail(hipError_t e, const char* what) {
@@ -534,9 +538,13 @@ int enqueue_frame(gs_renderer* r) {
   if (slot) GS_HIP(hipEventRecord(slot->ev[0], s));
   gsk::launch_project(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[1], s));
-  gsk::launch_scan(fp, r->buf, s);
+  // (GS_X_BAND == 5, measurement builds only, wrong frames: a band renderer
+  // launches the aggregated scan and emit for its first 4 frames only; later
+  // frames blend those lists again -- what the two launches cost the chain)
+  const bool x_skip = GS_X_BAND == 5 && fp.bin_agg && fp.band_cull && ++r->x_frames > 4;
+  if (!x_skip) gsk::launch_scan(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[2], s));
-  gsk::launch_emit(fp, r->buf, s);
+  if (!x_skip) gsk::launch_emit(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[3], s));
   gsk::launch_sort(fp, r->buf, s);
   if (slot) GS_HIP(hipEventRecord(slot->ev[4], s));
@@ -563,6 +571,16 @@ int enqueue_frame(gs_renderer* r) {
   }
   r->frame_pending = true;
   return GS_OK;
+}
+
+// gs_frame_stats.paths of the renderer's last enqueued frame
+uint32_t frame_paths(const gs_renderer* r) {
+  if (!r->have_fp) return 0u;
+  const int kind = gsk::project_kind(r->last_fp, r->buf);
+  return (r->last_fp.bin_agg ? GS_PATH_BIN_AGG : 0u) | (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u) |
+         (r->last_fp.blend_px2 ? GS_PATH_BLEND_PX2 : 0u) | (r->last_fp.lazy ? GS_PATH_LAZY : 0u) |
+         (r->last_fp.big_separate ? GS_PATH_BIG_LISTS : 0u) | (kind == 2 ? GS_PATH_PROJ_BAND : 0u) |
+         (kind == 0 ? GS_PATH_PROJ_ANY : 0u);
 }
 
 int finish_frame(gs_renderer* r) {
@@ -593,14 +611,7 @@ int finish_frame(gs_renderer* r) {
   r->stats.max_list = mx;
   r->stats.pair_capacity = r->pair_cap;
   r->stats.n_big_tiles = c[0];
-  r->stats.paths = r->have_fp ? ((r->last_fp.bin_agg ? GS_PATH_BIN_AGG : 0u) |
-                                 (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u) |
-                                 (r->last_fp.blend_px2 ? GS_PATH_BLEND_PX2 : 0u) |
-                                 (r->last_fp.lazy ? GS_PATH_LAZY : 0u) |
-                                 (r->last_fp.big_separate ? GS_PATH_BIG_LISTS : 0u) |
-                                 (gsk::project_kind(r->last_fp, r->buf) == 2 ? GS_PATH_PROJ_BAND : 0u) |
-                                 (gsk::project_kind(r->last_fp, r->buf) == 0 ? GS_PATH_PROJ_ANY : 0u))
-                              : 0u;
+  r->stats.paths = frame_paths(r);
   r->stats.blend_records = r->stats.blend_cont_records = r->stats.cont_keys = 0;
   r->stats.cont_lists = r->stats.cont_max = r->stats.prefix_overflows = r->stats.cont_full_sorts = 0;
   r->stats.big_pairs = r->stats.big_prefix_keys = r->stats.big_window_keys = 0;

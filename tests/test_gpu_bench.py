@@ -40,6 +40,10 @@ def test_bench_in_process_group_over_rccl():
     assert gr["gather_ms"][0] >= 0
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["frac"] > 0 and r["alg_bytes_per_launch"] > 0
+    # the group's stats carry the kernels its band renderer launched (a
+    # one-band group renders the whole frame: the two-pixel blend), so the
+    # line's PMC lookup asks for the right kernels
+    assert r["traffic_kernels"] == ["gs_blend_px2"], r
 
 
 def test_bench_refuses_more_gpus_than_visible():

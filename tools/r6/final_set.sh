@@ -38,5 +38,5 @@ PY
 done
 timeout -k 10 400 python3 tools/band_emulate.py --balanced --inflight 3 > $O/bands_c4.jsonl 2> $O/bands_c4.err
 tail -n 1 $O/bands_c4.jsonl | cut -c1-400
-timeout -k 10 500 python3 tools/band_emulate.py --config5 --rebalance --bands 1,8 --inflight 3 --steps 60 > $O/bands_c5.jsonl 2> $O/bands_c5.err
+timeout -k 10 500 python3 tools/band_emulate.py --config5 --balanced --rebalance --bands 1,8 --inflight 3 --steps 60 > $O/bands_c5.jsonl 2> $O/bands_c5.err
 tail -n 1 $O/bands_c5.jsonl | cut -c1-400
