@@ -108,6 +108,7 @@ def parse():
 # gs_frame_stats.paths bits (include/gsplat.h)
 PATH_BIN_AGG, PATH_BLEND_SORT, PATH_BLEND_PX2, PATH_LAZY, PATH_BIG_LISTS = 1, 2, 4, 8, 16
 PATH_PROJ_BAND, PATH_PROJ_ANY = 32, 64  # (ABI 13: which projection instantiation ran)
+PATH_BIN_DIRECT = 128  # (ABI 14: a row band's direct binning -- no scan, no emit launch)
 
 
 def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
@@ -123,6 +124,8 @@ def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
         if paths & PATH_PROJ_BAND:
             return [("gs_project_band", 1)]
         return [("gs_project_any" if paths & PATH_PROJ_ANY else "gs_project", 1)]
+    if stage in ("scan", "emit") and paths & PATH_BIN_DIRECT:
+        return []  # (the projection placed the pairs; the blend's workgroups wrote the counters)
     if stage == "scan":
         if agg:
             return [("gs_agg_scan", 1)]
@@ -579,6 +582,8 @@ def main():
     sib = bool(st_view.get("paths", 0) & 2)
     kern = {}
     for name, (avg_ms, cnt) in kt.items():
+        if name in ("scan", "emit") and int(st_view.get("paths", 0)) & PATH_BIN_DIRECT:
+            continue  # (direct binning: no such launch; its stage events are back to back)
         if name == "gather":
             if group:
                 kern[name] = {"avg_ms": round(avg_ms, 5), "launches": int(cnt),

@@ -302,7 +302,7 @@ __device__ __forceinline__ void sh_colour(const FrameParams& fp, const Buffers& 
 
 template <bool P2>
 __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers& b, int i, uint2& rect_out,
-                                            uint2& crect_out, float4* stage = nullptr) {
+                                            uint2& crect_out, float4* stage = nullptr, uint32_t* dkey_out = nullptr) {
   bool rendered = false;
   // mean_w1: the mean's w is 1 and the colour's rgb is not needed (the blend
   // reads it from the scene): one 16-B load of xyz + opacity instead of 32 B
@@ -512,6 +512,7 @@ __device__ __forceinline__ bool project_one(const FrameParams& fp, const Buffers
   }
   store_rects(fp, b, i, rect, crect);
   b.depth_key[i] = dkey;
+  if (dkey_out) *dkey_out = dkey;
   rect_out = rect;
   crect_out = fp.pair_cull ? crect : rect;
   return rendered;
@@ -697,6 +698,121 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
   }
 }
 
+// FrameParams::bin_direct (row bands): the projection workgroup places its
+// own pairs.  Tile t owns the fixed pair segment [t * tile_cap, (t + 1) *
+// tile_cap); the workgroup's reservation -- the returning add on the tile's
+// counter that agg_count makes (binned | reference << 32) -- is its offset in
+// that segment, so no scan has to run before any pair can be placed and no
+// emit launch follows.  The same three box cases as agg_count (ballots for
+// <= kAggBallot tiles, LDS cursors for <= kAggCap, a returning add per pair
+// beyond), the emit's placement rules (agg_emit_block) inside each.  A pair
+// past its segment is not written and flags the frame (dir_word[1]): the
+// blend's last workgroup reports it as the pair-capacity overflow, and the
+// host then bins that renderer's next frames with the scan and emit again.
+// The order of a tile's pairs is set by the atomics, as with agg_emit: the
+// in-blend sort puts every list in its total (z, input index) order.
+__device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers& b, uint2 r, uint2 q,
+                                           unsigned long long key) {
+  __shared__ uint32_t dcnt[kAggCap];
+  __shared__ uint32_t d_lo[4], d_hi[4];
+  __shared__ uint32_t d_wc[4][kAggBallot];
+  const AggBox bx = agg_box(r, d_lo, d_hi);
+  if (bx.area == 0) return;  // (uniform)
+  const uint32_t cap = fp.tile_cap;
+  const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
+  const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  bool ovf = false;
+  auto put = [&](uint32_t t, uint32_t off) {
+    if (off < cap) b.pairs[(size_t)t * cap + off] = key;
+    else ovf = true;
+  };
+  if (bx.area <= kAggBallot) {  // (uniform) per tile: ballots of the rectangles covering it
+    for (int k = 0; k < bx.area; ++k) {
+      const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
+      const bool in_r = x0 <= tx && tx <= x1 && y0 <= ty && ty <= y1;
+      const bool in_q = u0 <= tx && tx <= u1 && v0 <= ty && ty <= v1;
+      const uint32_t cr = (uint32_t)__popcll(ballot64(in_r)), cq = (uint32_t)__popcll(ballot64(in_q));
+      if (lane == 0) d_wc[wave][k] = (cr << 16) | cq;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < bx.area) {  // the workgroup's offset in the tile, split over its waves
+      const int k = threadIdx.x;
+      const uint32_t w0 = d_wc[0][k], w1 = d_wc[1][k], w2 = d_wc[2][k], w3 = d_wc[3][k];
+      const uint32_t v = w0 + w1 + w2 + w3;
+      uint32_t base = 0u;
+      if (v) {
+        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
+        base = (uint32_t)atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x],
+                                   ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
+      }
+      const uint32_t c0 = w0 & 0xFFFFu, c1 = w1 & 0xFFFFu, c2 = w2 & 0xFFFFu;
+      d_wc[0][k] = base;
+      d_wc[1][k] = base + c0;
+      d_wc[2][k] = base + c0 + c1;
+      d_wc[3][k] = base + c0 + c1 + c2;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int k = 0; k < bx.area; ++k) {
+      const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
+      const bool in_q = u0 <= tx && tx <= u1 && v0 <= ty && ty <= v1;
+      const unsigned long long m = ballot64(in_q);
+      if (in_q) put(ty * (uint32_t)fp.tiles_x + tx, d_wc[wave][k] + (uint32_t)__popcll(m & lt));
+    }
+  } else if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: a returning add per pair
+    if (x0 <= x1)
+      for (uint32_t y = y0; y <= y1; ++y) {
+        const bool yin = v0 <= y && y <= v1;
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const uint32_t t = y * fp.tiles_x + x;
+          if (yin && u0 <= x && x <= u1) put(t, (uint32_t)atomicAdd(&b.tile_cnt64[t], (1ull << 32) | 1ull));
+          else atomicAdd(&b.tile_cnt64[t], 1ull << 32);
+        }
+      }
+  } else {  // LDS histogram of the box, one returning add per (workgroup, tile), LDS cursors
+    for (int k = threadIdx.x; k < bx.area; k += 256) dcnt[k] = 0u;
+    uint32_t len;
+    const bool start = rect_run(r, q, len);
+    __syncthreads();
+    if (start && x0 <= x1)
+      for (uint32_t y = y0; y <= y1; ++y) {
+        const bool yin = v0 <= y && y <= v1;
+        const int row = ((int)y - bx.y0) * bx.w - bx.x0;
+        for (uint32_t x = x0; x <= x1; ++x)
+          atomicAdd(&dcnt[row + (int)x], (len << 16) | ((yin && u0 <= x && x <= u1) ? len : 0u));
+      }
+    __syncthreads();
+    for (int k = threadIdx.x; k < bx.area; k += 256) {
+      const uint32_t v = dcnt[k];
+      uint32_t base = 0u;
+      if (v) {
+        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
+        base = (uint32_t)atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x],
+                                   ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
+      }
+      dcnt[k] = base;  // the workgroup's cursor in the tile's segment
+    }
+    __syncthreads();
+    // a run of equal (reference, binned) rectangles takes its slots of each
+    // binned tile with one LDS atomic by its first lane
+    const unsigned long long st = ballot64(start);
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const int lead = 63 - __builtin_clzll(st & upto);
+    const uint32_t rank = (uint32_t)(lane - lead);
+    if (u0 <= u1)
+      for (uint32_t y = v0; y <= v1; ++y) {
+        const int row = ((int)y - bx.y0) * bx.w - bx.x0;
+        for (uint32_t x = u0; x <= u1; ++x) {
+          uint32_t base = 0u;
+          if (start) base = atomicAdd(&dcnt[row + (int)x], len);
+          put(y * (uint32_t)fp.tiles_x + x, (uint32_t)__shfl((int)base, lead, 64) + rank);
+        }
+      }
+  }
+  if (ovf) atomicOr(&b.dir_word[1], 1u);
+}
+
 // GS_X_BAND (measurement builds only, tools/build_x.sh; wrong frames): what
 // a row band's projection spends where.  1: every block returns after the
 // cull pass; 2: no aggregated counting (and every block reports no rendered
@@ -718,6 +834,7 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
   const int i = blk * 256 + threadIdx.x;
   bool rendered = false;
   uint2 rect = kEmptyRect, crect = kEmptyRect;
+  uint32_t dkey = 0xFFFFFFFFu;
   if (fp.band_cull) {
     // the cheap band test first; a block of 256 Gaussians that it culls
     // entirely writes only its V (0): count and emit skip such blocks
@@ -742,7 +859,7 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
       store_rects(fp, b, i, kEmptyRect, kEmptyRect);
       b.depth_key[i] = 0xFFFFFFFFu;
     } else {
-      rendered = project_one<P2>(fp, b, i, rect, crect);
+      rendered = project_one<P2>(fp, b, i, rect, crect, nullptr, &dkey);
     }
   } else if constexpr (STAGE) {
     __shared__ float4 s_rec[4][128];
@@ -764,7 +881,12 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
   } else if (i < fp.n) {
     rendered = project_one<P2>(fp, b, i, rect, crect);
   }
-  if (fp.bin_agg && GS_X_BAND != 2) agg_count(fp, b, rect, crect, blk);
+  if (fp.bin_agg && GS_X_BAND != 2) {
+    if (fp.bin_direct)  // (uniform) the pairs go to the tiles' fixed segments now
+      agg_direct(fp, b, rect, crect, ((unsigned long long)dkey << 32) | (uint32_t)i);
+    else
+      agg_count(fp, b, rect, crect, blk);
+  }
   // V per workgroup (summed by the scan kernel): no single-address atomics
   const int v = __syncthreads_count(rendered);
   if (threadIdx.x == 0) b.block_rendered[blk] = (fp.band_cull && GS_X_BAND == 2) ? 0u : (uint32_t)v;
@@ -1742,6 +1864,12 @@ __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b)
 // --------------------------------------------------------------------- sort
 __device__ __forceinline__ void tile_segment(const FrameParams& fp, const Buffers& b, int t,
                                              uint32_t& s, uint32_t& L) {
+  if (fp.bin_direct) {  // the tile's fixed segment; its pairs past the segment were dropped (overflow)
+    const uint32_t c = (uint32_t)b.tile_cnt64[t];
+    s = (uint32_t)t * fp.tile_cap;
+    L = c < fp.tile_cap ? c : fp.tile_cap;
+    return;
+  }
   uint32_t st = b.tile_start[t], en = b.tile_start[t + 1];
   const unsigned long long cap = fp.pair_cap;
   if (en > cap) en = (uint32_t)cap;
@@ -3084,7 +3212,7 @@ __device__ __forceinline__ uint32_t blend_idx(const FrameParams& fp, const uint3
 // the tile of blend slot `slot`: the tile order, or (blend_lpt) the sort
 // queues' order -- big, medium (longest first), then small and empty lists
 __device__ __forceinline__ int blend_tile_of(const FrameParams& fp, const Buffers& b, int slot) {
-  if (!fp.blend_lpt) return slot;
+  if (!fp.blend_lpt || fp.bin_direct) return slot;
   const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
   return (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
 }
@@ -3623,6 +3751,112 @@ __device__ __forceinline__ void blend_sort_tile(const FrameParams& fp, const Buf
   }
 }
 
+// FrameParams::bin_direct: what the scan would have written, from the blend's
+// workgroups.  Each one, after its waves are done with the tile (blend_sort's
+// last reads of the tile's counter): the tile's reference list length to the
+// histogram (and the group's footer), its binned length for the totals, the
+// counter reset for the next frame's projection.  Then a ticket (agent-scope
+// release / acquire: the stores of every other workgroup are visible to the
+// one that takes the last ticket); the last workgroup sums the frame's
+// counters as gs_agg_scan_kernel lays them out, writes them to the device,
+// the mapped host mirror and the footer, and resets the ticket and the
+// overflow flag.
+__device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffers& b, uint32_t* lds) {
+  const int T = fp.n_tiles, nb = (fp.n + 255) / 256;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned long long sum = 0, rsum = 0;
+  uint32_t mx = 0, n_big = 0, n_med = 0, n_small = 0, vis = 0;
+  for (int t = tid; t < T; t += 256) {
+    const uint32_t L = b.tile_count[t];
+    sum += L;
+    rsum += b.tile_ref[t];
+    mx = max(mx, L);
+    n_big += L > (uint32_t)kSortLdsCap ? 1u : 0u;
+    n_med += (L > kSortRegCap && L <= (uint32_t)kSortLdsCap) ? 1u : 0u;
+    n_small += L <= kSortRegCap ? 1u : 0u;
+  }
+  for (int k = tid; k < nb; k += 256) vis += b.block_rendered[k];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    sum += (unsigned long long)__shfl_xor((long long)sum, d, 64);
+    rsum += (unsigned long long)__shfl_xor((long long)rsum, d, 64);
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+    n_big += (uint32_t)__shfl_xor((int)n_big, d, 64);
+    n_med += (uint32_t)__shfl_xor((int)n_med, d, 64);
+    n_small += (uint32_t)__shfl_xor((int)n_small, d, 64);
+    vis += (uint32_t)__shfl_xor((int)vis, d, 64);
+  }
+  unsigned long long* const w64 = reinterpret_cast<unsigned long long*>(lds);  // [4][2]
+  uint32_t* const w32 = lds + 16;                                              // [4][5]
+  __syncthreads();  // (the staging LDS is free: every wave is past its blend)
+  if (lane == 0) {
+    w64[2 * wave] = sum;
+    w64[2 * wave + 1] = rsum;
+    w32[5 * wave] = mx;
+    w32[5 * wave + 1] = n_big;
+    w32[5 * wave + 2] = n_med;
+    w32[5 * wave + 3] = n_small;
+    w32[5 * wave + 4] = vis;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long tot = 0, rtot = 0;
+    uint32_t m = 0, nbg = 0, nmd = 0, nsm = 0, v = 0;
+    for (int w = 0; w < 4; ++w) {
+      tot += w64[2 * w];
+      rtot += w64[2 * w + 1];
+      m = max(m, w32[5 * w]);
+      nbg += w32[5 * w + 1];
+      nmd += w32[5 * w + 2];
+      nsm += w32[5 * w + 3];
+      v += w32[5 * w + 4];
+    }
+    const bool ovf = b.dir_word[1] != 0u || m > fp.tile_cap || tot > fp.pair_cap;
+    const uint4 c0 = make_uint4(nbg, 0u, v, ovf ? 1u : 0u);
+    const uint4 c1 = make_uint4(m, (uint32_t)tot, (uint32_t)(tot >> 32), nmd);
+    const uint4 c2 = make_uint4(0u, nsm, (uint32_t)rtot, (uint32_t)(rtot >> 32));
+    const uint4 c3 = make_uint4(0u, 0u, 0u, 0u);
+    if (ovf) {  // sticky until the host's sync
+      *b.host_sticky = 1u;
+      if (b.group_sticky) *b.group_sticky = 1u;
+    }
+    uint4* const cv = reinterpret_cast<uint4*>(b.counters);
+    cv[0] = c0;
+    cv[1] = c1;
+    cv[2] = c2;
+    cv[3] = c3;
+    if (b.footer) {
+      uint4* const fv = reinterpret_cast<uint4*>(b.footer);
+      fv[0] = c0;
+      fv[1] = c1;
+      fv[2] = c2;
+      fv[3] = c3;
+    }
+    const uint32_t cc[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                             c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+    for (int k = 0; k < 16; ++k) b.host_counters[k] = cc[k];
+    b.dir_word[1] = 0u;
+    b.dir_word[0] = 0u;
+  }
+}
+
+__device__ __forceinline__ void direct_finish(const FrameParams& fp, const Buffers& b, int tile, uint32_t* lds) {
+  __shared__ uint32_t s_last;
+  __syncthreads();  // every wave is done with the tile's counter
+  if (threadIdx.x == 0) {
+    const unsigned long long c = b.tile_cnt64[tile];
+    const uint32_t ref = (uint32_t)(c >> 32);
+    b.tile_cnt64[tile] = 0ull;  // zero for the next frame's projection
+    b.tile_ref[tile] = ref;     // the histogram (reference list lengths)
+    if (b.footer) b.footer[16 + tile] = ref;
+    b.tile_count[tile] = (uint32_t)c;  // the binned length, for the totals
+    const uint32_t tk = __hip_atomic_fetch_add(&b.dir_word[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = tk == (uint32_t)fp.n_tiles - 1u ? 1u : 0u;
+  }
+  __syncthreads();
+  if (s_last) direct_totals(fp, b, lds);
+}
+
 // HWEXP: GS_FLAG_FAST_EXP (its own kernel: the default path's code is unchanged)
 template <int BQW, bool HWEXP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WPE, 8))) void gs_blend_kernel(FrameParams fp, Buffers b) {
@@ -3664,6 +3898,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
   if (GS_X_BSORT == 2) return;
 #endif
   blend_wave<4, HWEXP>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
+  if (fp.bin_direct) direct_finish(fp, b, slot, lds);
 }
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
@@ -3769,6 +4004,7 @@ hipError_t init_kernel_attributes() {
 }
 
 void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
+  if (fp.bin_agg && fp.bin_direct) return;  // (the blend's workgroups write the counters)
   if (fp.bin_agg) {
     // (1024 threads, 4 tiles each; 256 threads x 8 -- a workgroup easier to
     // place beside the other frames' waves -- ran the scan stage 10.5 ->
@@ -3788,6 +4024,7 @@ void launch_scan(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 
 void launch_emit(const FrameParams& fp, const Buffers& b, hipStream_t s) {
   if (fp.n == 0) return;
+  if (fp.bin_agg && fp.bin_direct) return;  // (the projection placed the pairs)
   if (fp.bin_agg) {
     const int nb = (fp.n + 255) / 256;
     gs_agg_emit_kernel<<<fp.emit_grid > 0 ? std::min(nb, fp.emit_grid) : nb, 256, 0, s>>>(fp, b);

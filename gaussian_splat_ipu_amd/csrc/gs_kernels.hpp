@@ -63,6 +63,12 @@ struct FrameParams {
   int bin_global;     // 1: fallback binning with global atomics
   int bin_agg;        // 1: aggregated binning (per-tile counters summed by the projection's
                       //   workgroups, gs_agg_scan_kernel, gs_agg_emit_kernel): no chunk matrix
+  int bin_direct;     // (bin_agg row bands with the sort in the blend) each tile owns the fixed
+                      //   pair segment [t * tile_cap, (t + 1) * tile_cap): the projection's
+                      //   workgroups place their pairs there at once (no scan, no emit
+                      //   launch); the blend's workgroups read the lengths from the tile
+                      //   counters, reset them, and the last one writes the frame counters
+  unsigned int tile_cap;  // (bin_direct) pairs per tile segment
   int chunk_size;     // Gaussians per binning chunk (<= 65535)
   int n_chunks;
   int emit_wide;      // emit with one u32 LDS cursor per tile (n_tiles * 4 <= kBinLdsMax)
@@ -157,6 +163,8 @@ struct Buffers {
                             //   small | medium << 8 | big << 16 counts, max length;
                             //   then the reference list-length sum (lo, hi), 0, 0
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
+  uint32_t* dir_word;       // (bin_direct) [2]: the blend workgroups' ticket, a tile segment's
+                            //   overflow flag (both reset by the frame's last blend workgroup)
   uint32_t* host_counters;  // mapped pinned mirror of counters[16] + tile_count[n_tiles],
                             //   written by the chunked scan (no D2H copy per frame)
   uint32_t* host_sticky;    // mapped pinned word: set by the scan of any frame that

@@ -37,6 +37,9 @@ size_t scene_bytes(size_t nn) { return cull_offset(nn) + nn * 32; }
 #ifndef GS_X_BAND
 #define GS_X_BAND 0
 #endif
+#ifndef GS_X_DIRECT_OFF
+#define GS_X_DIRECT_OFF 0
+#endif
 
 namespace gsr {
 
@@ -52,7 +55,8 @@ int select_device(gs_renderer* r) {
 }
 
 // gs_test_set (include/gsplat.h): the test hooks gs_create reads
-std::atomic<int64_t> g_test_chunk_size{0}, g_test_bin_agg{-1}, g_test_poison{0}, g_test_cov_cache{-1};
+std::atomic<int64_t> g_test_chunk_size{0}, g_test_bin_agg{-1}, g_test_poison{0}, g_test_cov_cache{-1},
+    g_test_bin_direct{-1};
 
 // gs_test_set("debug_poison", 1): every device buffer is filled with 0xA5
 // bytes when it is allocated (before any initialisation the renderer does
@@ -329,6 +333,34 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // ... and read their slot's tile and list segment in one load, written by
   // the sort launch (which sorts every list when big_separate is off)
   fp.blend_seg = (fp.blend_px2 && !fp.big_separate) ? 1 : 0;
+  // Direct band binning (round 6): a row band whose tiles the aggregated
+  // binning and the in-blend sort serve gives each tile a fixed segment of
+  // the pair buffer, pair_cap / n_tiles pairs, and its projection places the
+  // pairs there itself: the scan and emit launches leave the band's chain.
+  // Only when the last frame the device completed (the mapped counters: its
+  // longest binned list) fits twice over, so a frame rarely overflows; one
+  // that does reports GS_EOVERFLOW like a pair-buffer overflow, and its
+  // longest list (counted in full) sends the next frames back to the scan and
+  // emit.  The renderer's first frames take them too.  Test hook (gs_test_set
+  // "bin_direct"): 0 off, >= 64 forced on with that segment size.
+  fp.bin_direct = 0;
+  fp.tile_cap = 0;
+  {
+    const int64_t hook = GS_X_DIRECT_OFF ? 0 : g_test_bin_direct.load();  // (measurement builds: off)
+    if (hook != 0 && fp.bin_agg && fp.band_cull && fp.blend_sort && !fp.lazy && !r->bin_global && r->n_tiles > 0 &&
+        r->buf.dir_word) {
+      const uint64_t seg = hook > 0 ? (uint64_t)hook : ((r->pair_cap / (uint64_t)r->n_tiles) & ~63ull);
+      const uint32_t hint = r->h_counters ? ((volatile const uint32_t*)r->h_counters)[4] : 0u;
+      // (forced: any segment size, but a frame whose longest list overflowed
+      // it -- the hint counts every pair -- sends the next ones back)
+      const bool fits = hook > 0 ? (uint64_t)hint <= seg : (hint > 0 && 2ull * hint + 256 <= seg);
+      if (seg >= 64 && seg * (uint64_t)r->n_tiles <= r->pair_cap && seg <= 0xFFFFFFFFull && fits) {
+        fp.bin_direct = 1;
+        fp.tile_cap = (uint32_t)seg;
+        fp.big_separate = 0;  // (the blend's workgroups radix-sort a list > kSortLdsCap themselves)
+      }
+    }
+  }
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
@@ -580,7 +612,7 @@ uint32_t frame_paths(const gs_renderer* r) {
   return (r->last_fp.bin_agg ? GS_PATH_BIN_AGG : 0u) | (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u) |
          (r->last_fp.blend_px2 ? GS_PATH_BLEND_PX2 : 0u) | (r->last_fp.lazy ? GS_PATH_LAZY : 0u) |
          (r->last_fp.big_separate ? GS_PATH_BIG_LISTS : 0u) | (kind == 2 ? GS_PATH_PROJ_BAND : 0u) |
-         (kind == 0 ? GS_PATH_PROJ_ANY : 0u);
+         (kind == 0 ? GS_PATH_PROJ_ANY : 0u) | (r->last_fp.bin_agg && r->last_fp.bin_direct ? GS_PATH_BIN_DIRECT : 0u);
 }
 
 int finish_frame(gs_renderer* r) {
@@ -992,10 +1024,13 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       if (r->bin_agg) {  // per projection block: its tile box and its offsets in each tile
         const size_t nb = (nn + 255) / 256;
         const size_t agg_bytes = nb * 16 + nb * (size_t)gsk::kAggCap * 4;
-        if ((e = hipMalloc(&r->d_agg, agg_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(agg boxes)"));
+        // + the direct binning's ticket and overflow words (zero between frames)
+        if ((e = hipMalloc(&r->d_agg, agg_bytes + 16)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(agg boxes)"));
         poison(r->d_agg, agg_bytes, "agg");
         r->buf.agg_box = (uint4*)r->d_agg;
         r->buf.agg_off = (uint32_t*)((char*)r->d_agg + nb * 16);
+        r->buf.dir_word = (uint32_t*)((char*)r->d_agg + agg_bytes);
+        if ((e = hipMemset(r->buf.dir_word, 0, 16)) != hipSuccess) return fail(hip_fail(e, "hipMemset(direct words)"));
       }
       if ((e = hipMalloc(&r->d_chunk, r->chunk_entries * 4)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(chunk offsets)"));
@@ -1222,6 +1257,7 @@ int read_bins(gs_renderer* r, uint64_t* tile_start, size_t n_start, uint32_t* li
     fp.pair_cull = 0;
     fp.rect8 = 0;
     fp.blend_sort = 0;  // (no blend here: the sort launch sorts the lists)
+    fp.bin_direct = 0;  // (the scan and emit place the reference lists)
     gsk::Buffers bb = r->buf;
     bb.footer = nullptr;        // (a group's all-gather slot belongs to the frame)
     bb.group_sticky = nullptr;  // (this re-binning's overflow is handled here, not by the group)
@@ -1296,6 +1332,7 @@ int read_projected(gs_renderer* r, float* dst, size_t n_floats) {
     fp.band_cull = 0;
     fp.bin_global = 0;  // (no tile_count atomics)
     fp.bin_agg = 0;     // (nor the aggregated binning's: this pass has no scan to reset them)
+    fp.bin_direct = 0;
     fp.full_record = 1;
     fp.rect8 = 0;  // (the readback takes the 16-bit reference rectangle)
     fp.mean_w1 = 0;  // (and the 48-B record with the colour)
@@ -1346,6 +1383,8 @@ int gs_test_set(const char* key, int64_t value) {
     gsr::g_test_poison.store(value);
   } else if (k == "cov_cache" && (value == -1 || value == 0)) {
     gsr::g_test_cov_cache.store(value);
+  } else if (k == "bin_direct" && (value == -1 || value == 0 || value >= 64)) {
+    gsr::g_test_bin_direct.store(value);  // -1: default; 0: off; >= 64: on, with this segment size
   } else {
     gsh::set_error("gs_test_set: unknown key or value");
     return GS_EINVAL;

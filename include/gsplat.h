@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_ABI_VERSION 13
+#define GSPLAT_ABI_VERSION 14
 
 typedef enum gs_status {
   GS_OK = 0,
@@ -199,7 +199,7 @@ typedef struct gs_frame_stats {
                              continuation's windows                        */
 } gs_frame_stats;
 
-/* gs_frame_stats.paths bits (ABI 11; bits 2-4 ABI 12, 5-6 ABI 13): which kernels the
+/* gs_frame_stats.paths bits (ABI 11; bits 2-4 ABI 12, 5-6 ABI 13, 7 ABI 14): which kernels the
    last frame launched, so a profile's per-kernel counters can be matched to
    the frame path (bench.py's roofline) */
 enum {
@@ -209,9 +209,12 @@ enum {
   GS_PATH_LAZY = 8,        /* lazy big lists (prefix select / sort, continuation) */
   GS_PATH_BIG_LISTS = 16,  /* the big-list launches ran (lists > 2048 keys)       */
   GS_PATH_PROJ_BAND = 32,  /* ABI 13: the row band's projection (gs_project_band) */
-  GS_PATH_PROJ_ANY = 64    /* ABI 13: the every-path projection (gs_project_any:
+  GS_PATH_PROJ_ANY = 64,   /* ABI 13: the every-path projection (gs_project_any:
                               readback records, SH, global atomics, non-power-of-
                               two tiles); neither bit: gs_project (whole frames) */
+  GS_PATH_BIN_DIRECT = 128 /* ABI 14: a row band's direct binning: the projection
+                              placed the pairs in fixed per-tile segments, no
+                              gs_agg_scan / gs_agg_emit launch */
 };
 
 /* Kernel ids for gs_kernel_times (GS_FLAG_PROFILE). */

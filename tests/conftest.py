@@ -35,7 +35,7 @@ def pc12_scene(built):
 
 
 # gs_test_set keys (include/gsplat.h) and their automatic values
-TEST_HOOK_DEFAULTS = {"bin_chunk_size": 0, "bin_agg": -1, "debug_poison": 0, "cov_cache": -1}
+TEST_HOOK_DEFAULTS = {"bin_chunk_size": 0, "bin_agg": -1, "debug_poison": 0, "cov_cache": -1, "bin_direct": -1}
 
 
 @pytest.fixture

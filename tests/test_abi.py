@@ -47,7 +47,7 @@ def test_abi_version_and_config_defaults(built):
     from gaussian_splat_ipu_amd import _lib
 
     L = _lib.lib()
-    assert L.gs_abi_version() == 13
+    assert L.gs_abi_version() == 14
     cfg = _lib.Config()
     assert L.gs_config_init(ctypes.byref(cfg)) == 0
     # tile_config.hpp:5-15 and codelets.cpp:622
@@ -113,7 +113,7 @@ def test_cpp_wrapper_compiles_and_links(built, tmp_path):
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
                     "-L", libdir, "-lgsplat", f"-Wl,-rpath,{libdir}"], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    assert int(out[0]) == 13
+    assert int(out[0]) == 14
     # the ctypes mirrors have the C layouts
     assert int(out[2]) == ctypes.sizeof(_lib.Config)
     assert int(out[3]) == ctypes.sizeof(_lib.FrameStats)

@@ -707,6 +707,86 @@ def test_binning_paths_bit_exact(pc12, test_hook, agg, tile):
     s.close()
 
 
+PATH_BIN_DIRECT = 128  # (gs_frame_stats.paths, ABI 14)
+
+
+@pytest.mark.parametrize("band_count,band_index", [(8, 3), (3, 1), (8, 0)])
+def test_direct_binning_bit_exact(pc12, test_hook, band_count, band_index):
+    """A row band's direct binning (round 6): each tile owns a fixed segment
+    of the pair buffer and the projection places the pairs there itself (no
+    scan, no emit launch; the blend's workgroups write the histogram and the
+    frame counters).  The renderer's first frame bins with the scan and emit
+    (no completed frame to size the segments from); the next ones take the
+    direct path, and frames, histograms and stats stay the oracle's bit for
+    bit.  Forced off (hook 0), the same frames take the scan and emit."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+    from oracle import oracle as O
+
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    fb = TiledFramebuffer(W, H, 16, 16)
+    ty0, ty1, _, _ = fb.band_rows(band_count)[band_index]
+    f = O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
+    for hook, direct in ((-1, True), (0, False)):
+        test_hook("bin_direct", hook)
+        s = GpuSplatter(g, fb, device=0, band_index=band_index, band_count=band_count, pair_capacity=1 << 23)
+        s.set_view_wire(view)
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        s.execute()
+        assert not s.stats()["paths"] & PATH_BIN_DIRECT  # (the first frame: the scan and emit)
+        for _ in range(3):
+            s.execute()
+            assert bool(s.stats()["paths"] & PATH_BIN_DIRECT) == direct, s.stats()["paths"]
+            _assert_parity(s, f, g, check_proj=False)
+        s.close()
+
+
+def test_direct_binning_overflow_falls_back(pc12, test_hook):
+    """A direct frame whose tile segments are too small (forced 64 pairs):
+    the dropped pairs flag the frame, the blocking render reports the
+    overflow to itself and renders again, and the longest list the flagged
+    frame counted in full sends it to the scan and emit: the frame the caller
+    gets is the oracle's, and async frames that overflow report
+    GS_EOVERFLOW at sync."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd._lib import GsError
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+    from oracle import oracle as O
+
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    fb = TiledFramebuffer(W, H, 16, 16)
+    ty0, ty1, _, _ = fb.band_rows(8)[3]
+    f = O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
+    test_hook("bin_direct", 64)
+    s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23)
+    s.set_view_wire(view)
+    s.set_projection_wire(proj)
+    s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+    s.execute()  # (forced direct with 64-pair segments: overflows, then the scan and emit)
+    assert s.stats()["max_list"] > 64
+    assert not s.stats()["paths"] & PATH_BIN_DIRECT
+    _assert_parity(s, f, g, check_proj=False)
+    s.close()
+    # async: the first frame of a fresh renderer overflows its forced segments
+    s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23)
+    s.set_view_wire(view)
+    s.set_projection_wire(proj)
+    s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+    s.execute_async()
+    with pytest.raises(GsError):
+        s.sync()
+    s.execute()  # a blocking frame after it: the oracle's
+    _assert_parity(s, f, g, check_proj=False)
+    s.close()
+
+
 def test_aggregated_binning_4k_clustered(built):
     """The aggregated binning of the two bands of a 4K frame (16 200 tiles
     each: the scan runs two 8192-tile rounds) of a clustered scene
