@@ -121,6 +121,8 @@ def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
                                                             PATH_LAZY, PATH_BIG_LISTS))
     buckets = [("gs_big_count", 1), ("gs_big_bscan", 1), ("gs_big_scatter", 1), ("gs_big_bsort", 1)]
     if stage == "project":
+        if paths & PATH_BIN_DIRECT:
+            return [("gs_project_direct", 1)]
         if paths & PATH_PROJ_BAND:
             return [("gs_project_band", 1)]
         return [("gs_project_any" if paths & PATH_PROJ_ANY else "gs_project", 1)]
@@ -139,6 +141,8 @@ def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
             ks += [("gs_big_select", 1), ("gs_big_psort", 1)] if lazy else buckets
         return ks
     if stage == "blend":
+        if paths & PATH_BIN_DIRECT:
+            return [("gs_blend_direct", 1)]
         return [("gs_blend_px2" if px2 else ("gs_blend_sort" if bsort else "gs_blend"), 1)]
     if stage == "blend_cont":  # lazy big lists: window sort + continued blend, pass 2 (launch_blend_cont)
         return [("gs_big_cont", 1), ("gs_blend_cont", 2), ("gs_big_prefix", 1)] + buckets

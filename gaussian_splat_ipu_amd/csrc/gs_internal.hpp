@@ -75,6 +75,7 @@ struct gs_renderer {
   void* d_chunk = nullptr;      // chunk histogram / offset matrix (chunked binning)
   void* d_lazy = nullptr;       // lazy big lists (16x16 tiles): per-tile tables + saved blend waves
   void* d_agg = nullptr;        // aggregated binning: per projection block its tile box and offsets
+  void* d_dir = nullptr;        // direct band binning: the blend's ticket and the overflow word
   void* d_cov = nullptr;        // the scene's 3D covariances (Buffers::cov3): 9 float planes, 36 B per
                                 // Gaussian, an empty slot marked by Sigma[2][2] < 0; null: computed per frame
   float cov_sd = 0.0f;          // ... computed for this fxy[1]
@@ -125,6 +126,12 @@ struct gs_renderer {
   bool last_counted = false;   // the last enqueued frame counted its blend records
   uint64_t frame_seq = 0;
   uint64_t x_frames = 0;  // (GS_X_BAND measurement builds only: this renderer's frames)
+  // direct band binning's hint: frames are numbered (FrameParams::frame_seq,
+  // echoed in the host mirror's word 15); cam_first_seq = the first frame
+  // enqueued with the current camera, projection, focal lengths and band
+  uint32_t seq_next = 1, cam_first_seq = 0;
+  bool cam_key_set = false;
+  float cam_key[40] = {0};
   gsr::ProfileSlot ring[gsr::kProfileRing];
   int ring_head = 0;
   double k_ms[GS_K_COUNT] = {0};

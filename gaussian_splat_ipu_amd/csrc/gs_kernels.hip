@@ -829,7 +829,7 @@ __device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers&
 // stores of whole 128-B lines -- each wave's 64 records (2 KB, contiguous)
 // through LDS, written for every Gaussian of the wave (a record that no tile
 // binned is never read, so its contents do not matter)
-template <bool P2, bool STAGE = false>
+template <bool P2, bool STAGE = false, bool DIRECT = false>
 __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffers& b, int blk) {
   const int i = blk * 256 + threadIdx.x;
   bool rendered = false;
@@ -882,7 +882,7 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
     rendered = project_one<P2>(fp, b, i, rect, crect);
   }
   if (fp.bin_agg && GS_X_BAND != 2) {
-    if (fp.bin_direct)  // (uniform) the pairs go to the tiles' fixed segments now
+    if constexpr (DIRECT)  // the pairs go to the tiles' fixed segments now
       agg_direct(fp, b, rect, crect, ((unsigned long long)dkey << 32) | (uint32_t)i);
     else
       agg_count(fp, b, rect, crect, blk);
@@ -901,18 +901,20 @@ __device__ __forceinline__ void project_block(const FrameParams& fp, const Buffe
 // counting, no readback record, no SH, no global-atomic binning);
 // kProjBand: a row band's (band cull and aggregated counting, nothing else);
 // kProjAny: every path, chosen at run time.
-enum { kProjAny = 0, kProjLean = 1, kProjBand = 2 };
+// kProjDirect: a direct-binned band's (kProjBand with agg_direct instead of
+// agg_count: FrameParams::bin_direct).
+enum { kProjAny = 0, kProjLean = 1, kProjBand = 2, kProjDirect = 3 };
 template <bool P2, int MODE>
 __device__ __forceinline__ void project_entry(FrameParams fp, const Buffers& b) {
   GS_PROBE_SCOPE(kPrProject);
   if constexpr (MODE != kProjAny) {
-    fp.band_cull = MODE == kProjBand ? 1 : 0;
-    fp.bin_agg = MODE == kProjBand ? 1 : 0;
+    fp.band_cull = (MODE == kProjBand || MODE == kProjDirect) ? 1 : 0;
+    fp.bin_agg = (MODE == kProjBand || MODE == kProjDirect) ? 1 : 0;
     fp.full_record = 0;
     fp.sh_degree = -1;
     fp.bin_global = 0;
   }
-  project_block<P2, MODE == kProjLean>(fp, b, blockIdx.x);
+  project_block<P2, MODE == kProjLean, MODE == kProjDirect>(fp, b, blockIdx.x);
 }
 // one kernel name per kind, so a profile's per-kernel counters are the
 // kind's own (gs_frame_stats.paths bits GS_PATH_PROJ_BAND / _ANY)
@@ -927,6 +929,10 @@ __global__ __launch_bounds__(256) void gs_project_band_kernel(FrameParams fp, Bu
 template <bool P2>
 __global__ __launch_bounds__(256) void gs_project_any_kernel(FrameParams fp, Buffers b) {
   project_entry<P2, kProjAny>(fp, b);
+}
+template <bool P2>
+__global__ __launch_bounds__(256) void gs_project_direct_kernel(FrameParams fp, Buffers b) {
+  project_entry<P2, kProjDirect>(fp, b);
 }
 
 // --------------------------------------------------------------------- scan
@@ -1310,7 +1316,7 @@ __global__ __launch_bounds__(NT) void gs_agg_scan_kernel(FrameParams fp, Buffers
     // first workgroup copies it, off this single-workgroup kernel's path)
     if (fp.n == 0) {
       const uint32_t cc[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                               c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+                               c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, fp.frame_seq};
       for (int k = 0; k < 16; ++k) b.host_counters[k] = cc[k];
     }
   }
@@ -1420,7 +1426,9 @@ __global__ __launch_bounds__(256) void gs_agg_emit_kernel(FrameParams fp, Buffer
   __shared__ uint32_t s_wc[4][kAggBallot];
   // the scan's frame counters to the mapped host mirror (the next frames'
   // big-list hint, the host's counters at sync)
-  if (blockIdx.x == 0 && threadIdx.x < 16) b.host_counters[threadIdx.x] = b.counters[threadIdx.x];
+  // (word 15: the frame's number, for the host's direct-binning choice)
+  if (blockIdx.x == 0 && threadIdx.x < 16)
+    b.host_counters[threadIdx.x] = threadIdx.x == 15 ? fp.frame_seq : b.counters[threadIdx.x];
   const int nb = (fp.n + 255) / 256;
   for (int blk = blockIdx.x; blk < nb; blk += gridDim.x) {
     agg_emit_block(fp, b, blk, cnt, s_wc);
@@ -1862,9 +1870,12 @@ __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b)
 }
 
 // --------------------------------------------------------------------- sort
+// DIRECT (FrameParams::bin_direct frames, gs_blend_direct_kernel only): the
+// tile's fixed segment; its pairs past the segment were dropped (overflow)
+template <bool DIRECT = false>
 __device__ __forceinline__ void tile_segment(const FrameParams& fp, const Buffers& b, int t,
                                              uint32_t& s, uint32_t& L) {
-  if (fp.bin_direct) {  // the tile's fixed segment; its pairs past the segment were dropped (overflow)
+  if constexpr (DIRECT) {
     const uint32_t c = (uint32_t)b.tile_cnt64[t];
     s = (uint32_t)t * fp.tile_cap;
     L = c < fp.tile_cap ? c : fp.tile_cap;
@@ -2361,12 +2372,12 @@ __device__ __forceinline__ void radix_sort_seg(const Buffers& b, uint32_t s, uin
   for (uint32_t i = tid; i < L; i += NT) b.list[s + i] = b.inv_perm[(uint32_t)src[i]];
 }
 
-template <int NT, int KPL>
+template <int NT, int KPL, bool DIRECT = false>
 __device__ __forceinline__ void radix_sort_tile(const FrameParams& fp, const Buffers& b, int t,
                                                 uint32_t* hist, uint32_t* base,
                                                 uint32_t (*wcnt)[256]) {
   uint32_t s, L;
-  tile_segment(fp, b, t, s, L);
+  tile_segment<DIRECT>(fp, b, t, s, L);
   radix_sort_seg<NT, KPL, false>(b, s, L, hist, base, wcnt);
 }
 
@@ -3212,14 +3223,14 @@ __device__ __forceinline__ uint32_t blend_idx(const FrameParams& fp, const uint3
 // the tile of blend slot `slot`: the tile order, or (blend_lpt) the sort
 // queues' order -- big, medium (longest first), then small and empty lists
 __device__ __forceinline__ int blend_tile_of(const FrameParams& fp, const Buffers& b, int slot) {
-  if (!fp.blend_lpt || fp.bin_direct) return slot;
+  if (!fp.blend_lpt) return slot;
   const uint32_t nb = b.counters[0], nm = b.counters[7], u = (uint32_t)slot;
   return (int)(u < nb ? b.big_tiles[u] : (u < nb + nm ? b.medium_tiles[u - nb] : b.small_tiles[u - nb - nm]));
 }
 
 // wid = the wave's (tile slot, 8x8 block) item; st: the wave's LDS staging
 // of one batch (3 x 64 float4)
-template <int BQW, bool HWEXP>
+template <int BQW, bool HWEXP, bool DIRECT = false>
 __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers& b, int wid, float4 (*st)[64]) {
   const int slot = wid / fp.chunks_per_tile;
   const int chunk = wid - slot * fp.chunks_per_tile;
@@ -3242,7 +3253,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
   // where the tile order puts them (8 bands: blend 35.7 -> 29.3 us).  The
   // full frame keeps the tile order (neighbouring tiles share records in L2:
   // 75.1 against 76.1 us in queue order).
-  const int tile = fp.blend_cont ? (int)b.big_tiles[jb] : blend_tile_of(fp, b, slot);
+  const int tile = DIRECT ? slot : (fp.blend_cont ? (int)b.big_tiles[jb] : blend_tile_of(fp, b, slot));
   const int lane = threadIdx.x & 63;
   const int myq = lane >> 2;
   const int tx = tile % fp.tiles_x, tyb = tile / fp.tiles_x;
@@ -3288,7 +3299,7 @@ __device__ __forceinline__ void blend_wave(const FrameParams& fp, const Buffers&
 
   uint32_t s, L;
   uint32_t k0 = 0u, Lfull;
-  tile_segment(fp, b, tile, s, L);
+  tile_segment<DIRECT>(fp, b, tile, s, L);
   Lfull = L;
   // lazy big list: this pass composites the sorted prefix [0, big_len), the
   // continuation the rest [big_len, L) from the saved state
@@ -3726,16 +3737,17 @@ static_assert(GS_BLEND_WPG == 4, "blend_sort: one workgroup per 16x16 tile (the 
 static_assert(kBlendLdsWords * 4 >= GS_BLEND_WPG * 3 * 64 * 16, "the staging fits the sort's LDS");
 static_assert(kBlendLdsWords >= 8 * 256 + 256 + 4 * 256, "the radix histograms fit the sort's LDS");
 
+template <bool DIRECT = false>
 __device__ __forceinline__ void blend_sort_tile(const FrameParams& fp, const Buffers& b, int tile,
                                                 unsigned long long* keys) {
   uint32_t s, L;
-  tile_segment(fp, b, tile, s, L);
+  tile_segment<DIRECT>(fp, b, tile, s, L);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (L > (uint32_t)kSortLdsCap) {
     // a big list: sorted by the big-list launches (big_separate), else here
     if (!fp.big_separate) {
       uint32_t* const hist = (uint32_t*)keys;
-      radix_sort_tile<256, 1>(fp, b, tile, hist, hist + 8 * 256, (uint32_t(*)[256])(hist + 9 * 256));  // (1 key per lane and round: compact code for this rare path)
+      radix_sort_tile<256, 1, DIRECT>(fp, b, tile, hist, hist + 8 * 256, (uint32_t(*)[256])(hist + 9 * 256));  // (1 key per lane and round: compact code for this rare path)
     }
     return;
   }
@@ -3833,7 +3845,7 @@ __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffe
       fv[3] = c3;
     }
     const uint32_t cc[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                             c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+                             c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, fp.frame_seq};
     for (int k = 0; k < 16; ++k) b.host_counters[k] = cc[k];
     b.dir_word[1] = 0u;
     b.dir_word[0] = 0u;
@@ -3898,7 +3910,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
   if (GS_X_BSORT == 2) return;
 #endif
   blend_wave<4, HWEXP>(fp, b, slot * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
-  if (fp.bin_direct) direct_finish(fp, b, slot, lds);
+}
+
+// The blend with the sort inside for a direct-binned band (FrameParams::
+// bin_direct): the same workgroup per tile, the tile's pairs from its fixed
+// segment, then direct_finish.  Its own symbol (the other kernels keep their
+// code; profiles tell it apart).
+template <bool HWEXP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WPE, 8))) void gs_blend_direct_kernel(FrameParams fp, Buffers b) {
+  GS_PROBE_SCOPE(kPrBlend);
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile = (int)blockIdx.x;  // (chunks_per_tile == GS_BLEND_WPG, the grid is the band's tiles)
+  blend_sort_tile<true>(fp, b, tile, reinterpret_cast<unsigned long long*>(lds));
+  __syncthreads();
+  blend_wave<4, HWEXP, true>(fp, b, tile * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
+  direct_finish(fp, b, tile, lds);
 }
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
@@ -3967,7 +3994,7 @@ void launch_cov3d(const FrameParams& fp, const Buffers& b, hipStream_t s) {
 int project_kind(const FrameParams& fp, const Buffers& b) {
   const bool plain = !fp.full_record && !(fp.sh_degree >= 0 && b.sh) && !fp.bin_global;
   if (fp.pow2 && plain && !fp.band_cull && !fp.bin_agg) return kProjLean;
-  if (fp.pow2 && plain && fp.band_cull && fp.bin_agg) return kProjBand;
+  if (fp.pow2 && plain && fp.band_cull && fp.bin_agg) return fp.bin_direct ? kProjDirect : kProjBand;
   return kProjAny;
 }
 
@@ -3984,6 +4011,8 @@ void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s) {
       seen.push_back(b.rec);
     }
     gs_project_band_kernel<true><<<nb, 256, 0, s>>>(fp, b);
+  } else if (kind == kProjDirect) {
+    gs_project_direct_kernel<true><<<nb, 256, 0, s>>>(fp, b);
   } else if (fp.pow2) {
     gs_project_any_kernel<true><<<nb, 256, 0, s>>>(fp, b);
   } else {
@@ -4087,6 +4116,13 @@ void launch_blend(const FrameParams& fp, const Buffers& b, hipStream_t s) {
       gs_blend_px2_kernel<true><<<g2, 64 * GS_PX2_WPG, 0, s>>>(fp, b);
     else
       gs_blend_px2_kernel<false><<<g2, 64 * GS_PX2_WPG, 0, s>>>(fp, b);
+    return;
+  }
+  if (fp.blend_sort && fp.bin_direct) {  // (a direct-binned band: its own kernel)
+    if (fp.fast_exp)
+      gs_blend_direct_kernel<true><<<grid, block, 0, s>>>(fp, b);
+    else
+      gs_blend_direct_kernel<false><<<grid, block, 0, s>>>(fp, b);
     return;
   }
   if (fp.blend_sort) {  // (blend_bqw == 4, chunks_per_tile == GS_BLEND_WPG: one workgroup per tile)

@@ -63,12 +63,6 @@ struct FrameParams {
   int bin_global;     // 1: fallback binning with global atomics
   int bin_agg;        // 1: aggregated binning (per-tile counters summed by the projection's
                       //   workgroups, gs_agg_scan_kernel, gs_agg_emit_kernel): no chunk matrix
-  int bin_direct;     // (bin_agg row bands with the sort in the blend) each tile owns the fixed
-                      //   pair segment [t * tile_cap, (t + 1) * tile_cap): the projection's
-                      //   workgroups place their pairs there at once (no scan, no emit
-                      //   launch); the blend's workgroups read the lengths from the tile
-                      //   counters, reset them, and the last one writes the frame counters
-  unsigned int tile_cap;  // (bin_direct) pairs per tile segment
   int chunk_size;     // Gaussians per binning chunk (<= 65535)
   int n_chunks;
   int emit_wide;      // emit with one u32 LDS cursor per tile (n_tiles * 4 <= kBinLdsMax)
@@ -97,6 +91,15 @@ struct FrameParams {
                       // projection divides by them with exact multiplies / shifts
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)
   int sh_tw, sh_th, sh_stride;   // log2 tile_w, tile_h, band_stride (pow2 only)
+  // (appended last, so the other kernels' argument offsets stay as they were)
+  int bin_direct;     // (bin_agg row bands with the sort in the blend) each tile owns the fixed
+                      //   pair segment [t * tile_cap, (t + 1) * tile_cap): the projection's
+                      //   workgroups place their pairs there at once (no scan, no emit
+                      //   launch); the blend's workgroups read the lengths from the tile
+                      //   counters, reset them, and the last one writes the frame counters
+  unsigned int tile_cap;  // (bin_direct) pairs per tile segment
+  unsigned int frame_seq;  // the renderer's frame number (1, 2, ...): the aggregated binning's
+                           //   host mirror word 15, which frame its counters are from
 };
 
 // Device workspace of one renderer.
@@ -163,8 +166,6 @@ struct Buffers {
                             //   small | medium << 8 | big << 16 counts, max length;
                             //   then the reference list-length sum (lo, hi), 0, 0
   uint32_t* block_rendered; // [ceil(n / 256)] V per project workgroup
-  uint32_t* dir_word;       // (bin_direct) [2]: the blend workgroups' ticket, a tile segment's
-                            //   overflow flag (both reset by the frame's last blend workgroup)
   uint32_t* host_counters;  // mapped pinned mirror of counters[16] + tile_count[n_tiles],
                             //   written by the chunked scan (no D2H copy per frame)
   uint32_t* host_sticky;    // mapped pinned word: set by the scan of any frame that
@@ -206,6 +207,8 @@ struct Buffers {
   uint32_t* group_sticky;   // row-band group: one device word per GPU, set by the scan of any
                             //   frame of any of its band renderers that overflowed; copied into
                             //   footer word kFootSticky before each all-gather (nullptr = none)
+  uint32_t* dir_word;       // (bin_direct) [2]: the blend workgroups' ticket, a tile segment's
+                            //   overflow flag (both reset by the frame's last blend workgroup)
 };
 
 // footer word that carries the group's sticky overflow bit (counters[15] is unused)
@@ -222,7 +225,8 @@ bool bin_lds_fits(int n_tiles);
 hipError_t init_kernel_attributes();
 
 // the projection's instantiation for fp: 1 = a whole frame's lean one
-// (gs_project), 2 = a row band's (gs_project_band), 0 = every path (gs_project_any)
+// (gs_project), 2 = a row band's (gs_project_band), 3 = a direct-binned
+// band's (gs_project_direct), 0 = every path (gs_project_any)
 int project_kind(const FrameParams& fp, const Buffers& b);
 void launch_project(const FrameParams& fp, const Buffers& b, hipStream_t s);
 // the 3D covariances of the scene for fp's fxy[1] into Buffers::cov3

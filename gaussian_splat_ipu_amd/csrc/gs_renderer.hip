@@ -206,7 +206,7 @@ void release(gs_renderer* r) {
     (void)hipFree(r->buf.lanes);
   }
 #endif
-  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg, r->d_cov,
+  for (void* p : {r->d_gauss, r->d_zero, r->d_tiles, r->d_out, r->d_chunk, r->d_lazy, r->d_lat, r->d_bcount, r->d_agg, r->d_dir, r->d_cov,
                   r->d_probe})
     if (p) (void)hipFree(p);
   if (r->d_sh && r->owns_sh) (void)hipFree(r->d_sh);
@@ -333,34 +333,8 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // ... and read their slot's tile and list segment in one load, written by
   // the sort launch (which sorts every list when big_separate is off)
   fp.blend_seg = (fp.blend_px2 && !fp.big_separate) ? 1 : 0;
-  // Direct band binning (round 6): a row band whose tiles the aggregated
-  // binning and the in-blend sort serve gives each tile a fixed segment of
-  // the pair buffer, pair_cap / n_tiles pairs, and its projection places the
-  // pairs there itself: the scan and emit launches leave the band's chain.
-  // Only when the last frame the device completed (the mapped counters: its
-  // longest binned list) fits twice over, so a frame rarely overflows; one
-  // that does reports GS_EOVERFLOW like a pair-buffer overflow, and its
-  // longest list (counted in full) sends the next frames back to the scan and
-  // emit.  The renderer's first frames take them too.  Test hook (gs_test_set
-  // "bin_direct"): 0 off, >= 64 forced on with that segment size.
   fp.bin_direct = 0;
   fp.tile_cap = 0;
-  {
-    const int64_t hook = GS_X_DIRECT_OFF ? 0 : g_test_bin_direct.load();  // (measurement builds: off)
-    if (hook != 0 && fp.bin_agg && fp.band_cull && fp.blend_sort && !fp.lazy && !r->bin_global && r->n_tiles > 0 &&
-        r->buf.dir_word) {
-      const uint64_t seg = hook > 0 ? (uint64_t)hook : ((r->pair_cap / (uint64_t)r->n_tiles) & ~63ull);
-      const uint32_t hint = r->h_counters ? ((volatile const uint32_t*)r->h_counters)[4] : 0u;
-      // (forced: any segment size, but a frame whose longest list overflowed
-      // it -- the hint counts every pair -- sends the next ones back)
-      const bool fits = hook > 0 ? (uint64_t)hint <= seg : (hint > 0 && 2ull * hint + 256 <= seg);
-      if (seg >= 64 && seg * (uint64_t)r->n_tiles <= r->pair_cap && seg <= 0xFFFFFFFFull && fits) {
-        fp.bin_direct = 1;
-        fp.tile_cap = (uint32_t)seg;
-        fp.big_separate = 0;  // (the blend's workgroups radix-sort a list > kSortLdsCap themselves)
-      }
-    }
-  }
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
@@ -536,11 +510,60 @@ int ensure_cov(gs_renderer* r, const gsk::FrameParams& fp, hipStream_t s) {
   return GS_OK;
 }
 
+// Direct band binning (round 6): a row band whose tiles the aggregated
+// binning and the in-blend sort serve (gs_project_direct, gs_blend_direct)
+// gives each tile a fixed segment of the pair buffer, pair_cap / n_tiles
+// pairs, and its projection places the pairs there itself: the scan and emit
+// launches leave the band's chain.  Taken when the renderer has completed a
+// frame of the same camera, projection, focal lengths and band (the mapped
+// counters' word 15 names the frame they are from) whose longest binned list
+// fits a segment -- the same view bins the same lists, so such a frame cannot
+// overflow.  The first frame of a view takes the scan and emit.  A frame that
+// does overflow (only a forced segment size can) drops the pairs past the
+// segment, reports GS_EOVERFLOW like a pair-buffer overflow, and its longest
+// list, counted in full, sends the next frames back.  Test hook (gs_test_set
+// "bin_direct"): 0 off, >= 64 forced on with that segment size.
+void choose_direct(const gs_renderer* r, gsk::FrameParams& fp) {
+  fp.bin_direct = 0;
+  fp.tile_cap = 0;
+  const int64_t hook = GS_X_DIRECT_OFF ? 0 : g_test_bin_direct.load();  // (measurement builds: off)
+  if (hook == 0 || !fp.blend_sort || fp.lazy || r->bin_global || r->n_tiles <= 0 || !r->buf.dir_word ||
+      !r->h_counters || gsk::project_kind(fp, r->buf) != 2)  // (2: the row band's projection)
+    return;
+  const uint64_t seg = hook > 0 ? (uint64_t)hook : ((r->pair_cap / (uint64_t)r->n_tiles) & ~63ull);
+  const volatile uint32_t* h = (const volatile uint32_t*)r->h_counters;
+  const uint32_t hseq = h[15], hint = h[4];
+  const bool known = hseq != 0 && (int32_t)(hseq - r->cam_first_seq) >= 0;  // a completed frame of this view
+  const bool fits = hook > 0 ? (!known || (uint64_t)hint <= seg) : (known && (uint64_t)hint <= seg);
+  if (seg >= 64 && seg * (uint64_t)r->n_tiles <= r->pair_cap && seg <= 0xFFFFFFFFull && fits) {
+    fp.bin_direct = 1;
+    fp.tile_cap = (uint32_t)seg;
+    fp.big_separate = 0;  // (the blend's workgroups radix-sort a list > kSortLdsCap themselves)
+  }
+}
+
 int enqueue_frame(gs_renderer* r) {
   // several frames may be in flight on the stream; the host mirrors always
   // hold the last one's counters after gs_sync
   gsk::FrameParams fp = make_params(r);
   if (r->d_probe) fp.probe_frame = r->probe_n++;
+  {  // the frame's number, and the first of its view (choose_direct)
+    fp.frame_seq = r->seq_next++;
+    if (r->seq_next == 0) r->seq_next = 1;
+    float key[40] = {0};
+    std::memcpy(key, r->view_rm, 16 * sizeof(float));
+    std::memcpy(key + 16, r->proj_rm, 16 * sizeof(float));
+    key[32] = r->fov;
+    key[33] = r->scale_div;
+    const int32_t bk[4] = {r->band_ty0, r->band_nrows, r->band_stride, r->n_tiles};
+    std::memcpy(key + 34, bk, sizeof(bk));
+    if (!r->cam_key_set || std::memcmp(key, r->cam_key, sizeof(key)) != 0) {
+      std::memcpy(r->cam_key, key, sizeof(key));
+      r->cam_key_set = true;
+      r->cam_first_seq = fp.frame_seq;
+    }
+    choose_direct(r, fp);
+  }
   r->last_fp = fp;
   r->have_fp = true;
   r->band_moved = false;
@@ -612,7 +635,7 @@ uint32_t frame_paths(const gs_renderer* r) {
   return (r->last_fp.bin_agg ? GS_PATH_BIN_AGG : 0u) | (r->last_fp.blend_sort ? GS_PATH_BLEND_SORT : 0u) |
          (r->last_fp.blend_px2 ? GS_PATH_BLEND_PX2 : 0u) | (r->last_fp.lazy ? GS_PATH_LAZY : 0u) |
          (r->last_fp.big_separate ? GS_PATH_BIG_LISTS : 0u) | (kind == 2 ? GS_PATH_PROJ_BAND : 0u) |
-         (kind == 0 ? GS_PATH_PROJ_ANY : 0u) | (r->last_fp.bin_agg && r->last_fp.bin_direct ? GS_PATH_BIN_DIRECT : 0u);
+         (kind == 0 ? GS_PATH_PROJ_ANY : 0u) | (kind == 3 ? GS_PATH_BIN_DIRECT : 0u);
 }
 
 int finish_frame(gs_renderer* r) {
@@ -1024,13 +1047,14 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
       if (r->bin_agg) {  // per projection block: its tile box and its offsets in each tile
         const size_t nb = (nn + 255) / 256;
         const size_t agg_bytes = nb * 16 + nb * (size_t)gsk::kAggCap * 4;
-        // + the direct binning's ticket and overflow words (zero between frames)
-        if ((e = hipMalloc(&r->d_agg, agg_bytes + 16)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(agg boxes)"));
+        if ((e = hipMalloc(&r->d_agg, agg_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(agg boxes)"));
         poison(r->d_agg, agg_bytes, "agg");
         r->buf.agg_box = (uint4*)r->d_agg;
         r->buf.agg_off = (uint32_t*)((char*)r->d_agg + nb * 16);
-        r->buf.dir_word = (uint32_t*)((char*)r->d_agg + agg_bytes);
-        if ((e = hipMemset(r->buf.dir_word, 0, 16)) != hipSuccess) return fail(hip_fail(e, "hipMemset(direct words)"));
+        // the direct binning's ticket and overflow words (zero between frames)
+        if ((e = hipMalloc(&r->d_dir, 16)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(direct words)"));
+        if ((e = hipMemset(r->d_dir, 0, 16)) != hipSuccess) return fail(hip_fail(e, "hipMemset(direct words)"));
+        r->buf.dir_word = (uint32_t*)r->d_dir;
       }
       if ((e = hipMalloc(&r->d_chunk, r->chunk_entries * 4)) != hipSuccess)
         return fail(hip_fail(e, "hipMalloc(chunk offsets)"));

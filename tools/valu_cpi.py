@@ -44,6 +44,7 @@ KERNELS = {
     "gs_blend_px2": "_ZN3gsk12_GLOBAL__N_119gs_blend_px2_kernelILb0EEEvNS_11FrameParamsENS_7BuffersE",
     "gs_blend": "_ZN3gsk12_GLOBAL__N_115gs_blend_kernelILi4ELb0EEEvNS_11FrameParamsENS_7BuffersE",
     "gs_blend_sort": "_ZN3gsk12_GLOBAL__N_120gs_blend_sort_kernelILb0EEEvNS_11FrameParamsENS_7BuffersE",
+    "gs_blend_direct": "_ZN3gsk12_GLOBAL__N_122gs_blend_direct_kernelILb0EEEvNS_11FrameParamsENS_7BuffersE",
     "gs_blend_cont": "_ZN3gsk12_GLOBAL__N_120gs_blend_cont_kernelILb0EEEvNS_11FrameParamsENS_7BuffersE",
 }
 
