@@ -52,12 +52,15 @@ def _frame_pair(g, view, proj, W, H, TW, TH, scale_div, fov=None, guard_tile=Non
     return s, f
 
 
-def _assert_parity(s, f, g, check_proj=True):
+def _assert_parity(s, f, g, check_proj=True, band_culled=False):
     from oracle import oracle as O
 
     ref = O.render(g, f)
     st = s.stats()
-    assert st["n_rendered"] == ref["stats"]["n_rendered"]
+    if band_culled:  # (gsplat.h: a band-culled renderer's n_rendered counts only the Gaussians it projected)
+        assert 0 < st["n_rendered"] <= ref["stats"]["n_rendered"]
+    else:
+        assert st["n_rendered"] == ref["stats"]["n_rendered"]
     assert st["n_pairs"] == ref["stats"]["n_pairs"]
     assert st["max_list"] == ref["stats"]["max_list"]
     if check_proj and g.shape[0]:
@@ -712,7 +715,8 @@ PATH_BIN_DIRECT = 128  # (gs_frame_stats.paths, ABI 14)
 
 @pytest.mark.parametrize("band_count,band_index", [(8, 3), (3, 1), (8, 0)])
 def test_direct_binning_bit_exact(pc12, test_hook, band_count, band_index):
-    """A row band's direct binning (round 6): each tile owns a fixed segment
+    """A row band's direct binning (round 6; band-culled bands, the bench's and
+    the group's): each tile owns a fixed segment
     of the pair buffer and the projection places the pairs there itself (no
     scan, no emit launch; the blend's workgroups write the histogram and the
     frame counters).  The renderer's first frame bins with the scan and emit
@@ -730,9 +734,11 @@ def test_direct_binning_bit_exact(pc12, test_hook, band_count, band_index):
     fb = TiledFramebuffer(W, H, 16, 16)
     ty0, ty1, _, _ = fb.band_rows(band_count)[band_index]
     f = O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
+    seen = []
     for hook, direct in ((-1, True), (0, False)):
         test_hook("bin_direct", hook)
-        s = GpuSplatter(g, fb, device=0, band_index=band_index, band_count=band_count, pair_capacity=1 << 23)
+        s = GpuSplatter(g, fb, device=0, band_index=band_index, band_count=band_count, pair_capacity=1 << 23,
+                        band_cull=True)
         s.set_view_wire(view)
         s.set_projection_wire(proj)
         s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
@@ -741,8 +747,10 @@ def test_direct_binning_bit_exact(pc12, test_hook, band_count, band_index):
         for _ in range(3):
             s.execute()
             assert bool(s.stats()["paths"] & PATH_BIN_DIRECT) == direct, s.stats()["paths"]
-            _assert_parity(s, f, g, check_proj=False)
+            _assert_parity(s, f, g, check_proj=False, band_culled=True)
+            seen.append(s.stats()["n_rendered"])
         s.close()
+    assert len(set(seen)) == 1, seen  # (both paths count the same band-culled Gaussians)
 
 
 def test_direct_binning_overflow_falls_back(pc12, test_hook):
@@ -765,17 +773,17 @@ def test_direct_binning_overflow_falls_back(pc12, test_hook):
     ty0, ty1, _, _ = fb.band_rows(8)[3]
     f = O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
     test_hook("bin_direct", 64)
-    s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23)
+    s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23, band_cull=True)
     s.set_view_wire(view)
     s.set_projection_wire(proj)
     s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
     s.execute()  # (forced direct with 64-pair segments: overflows, then the scan and emit)
     assert s.stats()["max_list"] > 64
     assert not s.stats()["paths"] & PATH_BIN_DIRECT
-    _assert_parity(s, f, g, check_proj=False)
+    _assert_parity(s, f, g, check_proj=False, band_culled=True)
     s.close()
     # async: the first frame of a fresh renderer overflows its forced segments
-    s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23)
+    s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23, band_cull=True)
     s.set_view_wire(view)
     s.set_projection_wire(proj)
     s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
@@ -783,7 +791,7 @@ def test_direct_binning_overflow_falls_back(pc12, test_hook):
     with pytest.raises(GsError):
         s.sync()
     s.execute()  # a blocking frame after it: the oracle's
-    _assert_parity(s, f, g, check_proj=False)
+    _assert_parity(s, f, g, check_proj=False, band_culled=True)
     s.close()
 
 
