@@ -58,7 +58,7 @@ def _assert_parity(s, f, g, check_proj=True, band_culled=False):
     ref = O.render(g, f)
     st = s.stats()
     if band_culled:  # (gsplat.h: a band-culled renderer's n_rendered counts only the Gaussians it projected)
-        assert 0 < st["n_rendered"] <= ref["stats"]["n_rendered"]
+        assert st["n_rendered"] <= ref["stats"]["n_rendered"]
     else:
         assert st["n_rendered"] == ref["stats"]["n_rendered"]
     assert st["n_pairs"] == ref["stats"]["n_pairs"]
@@ -713,7 +713,7 @@ def test_binning_paths_bit_exact(pc12, test_hook, agg, tile):
 PATH_BIN_DIRECT = 128  # (gs_frame_stats.paths, ABI 14)
 
 
-@pytest.mark.parametrize("band_count,band_index", [(8, 3), (3, 1), (8, 0)])
+@pytest.mark.parametrize("band_count,band_index", [(8, 3), (3, 1), (8, 0)])  # (8, 0): no Gaussian reaches it
 def test_direct_binning_bit_exact(pc12, test_hook, band_count, band_index):
     """A row band's direct binning (round 6; band-culled bands, the bench's and
     the group's): each tile owns a fixed segment
