@@ -127,7 +127,7 @@ def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
             return [("gs_project_band", 1)]
         return [("gs_project_any" if paths & PATH_PROJ_ANY else "gs_project", 1)]
     if stage in ("scan", "emit") and paths & PATH_BIN_DIRECT:
-        return []  # (the projection placed the pairs; the blend's workgroups wrote the counters)
+        return []  # (the projection placed the pairs; the blend's last workgroup wrote the counters)
     if stage == "scan":
         if agg:
             return [("gs_agg_scan", 1)]

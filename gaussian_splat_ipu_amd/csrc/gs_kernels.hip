@@ -3763,31 +3763,52 @@ __device__ __forceinline__ void blend_sort_tile(const FrameParams& fp, const Buf
   }
 }
 
-// FrameParams::bin_direct: what the scan would have written, from the blend's
-// workgroups.  Each one, after its waves are done with the tile (blend_sort's
-// last reads of the tile's counter): the tile's reference list length to the
-// histogram (and the group's footer), its binned length for the totals, the
-// counter reset for the next frame's projection.  Then a ticket (agent-scope
-// release / acquire: the stores of every other workgroup are visible to the
-// one that takes the last ticket); the last workgroup sums the frame's
-// counters as gs_agg_scan_kernel lays them out, writes them to the device,
-// the mapped host mirror and the footer, and resets the ticket and the
-// overflow flag.
+// FrameParams::bin_direct: what the scan would have written.  Each of the
+// blend's workgroups leaves its tile's list lengths and takes a ticket; the
+// last one sums the frame's counters as gs_agg_scan_kernel lays them out,
+// writes them to the device, the mapped host mirror and the footer, and
+// resets the ticket and the overflow flag.
+// The per-tile values reach the totals write-through (system scope, past the
+// XCDs' L2s, sc0 sc1 loads and stores), so no workgroup releases its L2 with
+// a fence (MI355X_MICROARCH.md, the hand-off table's first row)
+__device__ __forceinline__ uint32_t direct_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int NT>
 __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffers& b, uint32_t* lds) {
+  constexpr int NW = NT / 64;
   const int T = fp.n_tiles, nb = (fp.n + 255) / 256;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long sum = 0, rsum = 0;
   uint32_t mx = 0, n_big = 0, n_med = 0, n_small = 0, vis = 0;
-  for (int t = tid; t < T; t += 256) {
-    const uint32_t L = b.tile_count[t];
-    sum += L;
-    rsum += b.tile_ref[t];
-    mx = max(mx, L);
-    n_big += L > (uint32_t)kSortLdsCap ? 1u : 0u;
-    n_med += (L > kSortRegCap && L <= (uint32_t)kSortLdsCap) ? 1u : 0u;
-    n_small += L <= kSortRegCap ? 1u : 0u;
+  // (four loads in flight per thread: one workgroup, latency-bound)
+  for (int t0 = tid; t0 < T; t0 += 4 * NT) {
+    uint32_t Lr[4], Rr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = t0 + j * NT;
+      Lr[j] = t < T ? direct_load(&b.tile_count[t]) : 0u;
+      Rr[j] = t < T ? direct_load(&b.tile_ref[t]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t L = Lr[j];
+      sum += L;
+      rsum += Rr[j];
+      mx = max(mx, L);
+      n_big += L > (uint32_t)kSortLdsCap ? 1u : 0u;
+      n_med += (L > kSortRegCap && L <= (uint32_t)kSortLdsCap) ? 1u : 0u;
+      n_small += (t0 + j * NT < T && L <= kSortRegCap) ? 1u : 0u;
+    }
   }
-  for (int k = tid; k < nb; k += 256) vis += b.block_rendered[k];
+  for (int k0 = tid; k0 < nb; k0 += 4 * NT) {
+    uint32_t vr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vr[j] = k0 + j * NT < nb ? b.block_rendered[k0 + j * NT] : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vis += vr[j];
+  }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) {
     sum += (unsigned long long)__shfl_xor((long long)sum, d, 64);
@@ -3798,9 +3819,9 @@ __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffe
     n_small += (uint32_t)__shfl_xor((int)n_small, d, 64);
     vis += (uint32_t)__shfl_xor((int)vis, d, 64);
   }
-  unsigned long long* const w64 = reinterpret_cast<unsigned long long*>(lds);  // [4][2]
-  uint32_t* const w32 = lds + 16;                                              // [4][5]
-  __syncthreads();  // (the staging LDS is free: every wave is past its blend)
+  unsigned long long* const w64 = reinterpret_cast<unsigned long long*>(lds);  // [NW][2]
+  uint32_t* const w32 = lds + 4 * NW;                                          // [NW][5]
+  __syncthreads();
   if (lane == 0) {
     w64[2 * wave] = sum;
     w64[2 * wave + 1] = rsum;
@@ -3814,7 +3835,7 @@ __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffe
   if (tid == 0) {
     unsigned long long tot = 0, rtot = 0;
     uint32_t m = 0, nbg = 0, nmd = 0, nsm = 0, v = 0;
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       tot += w64[2 * w];
       rtot += w64[2 * w + 1];
       m = max(m, w32[5 * w]);
@@ -3848,25 +3869,35 @@ __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffe
                              c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, fp.frame_seq};
     for (int k = 0; k < 16; ++k) b.host_counters[k] = cc[k];
     b.dir_word[1] = 0u;
-    b.dir_word[0] = 0u;
   }
 }
 
-__device__ __forceinline__ void direct_finish(const FrameParams& fp, const Buffers& b, int tile, uint32_t* lds) {
+// the tile's counter (c: read by thread 0 before the sort), zeroed for the
+// next frame's projection once every wave is past its reads of it; its
+// reference length (the histogram) and binned length (for the totals), stored
+// write-through and acknowledged before the ticket (a relaxed agent-scope
+// add).  An agent-scope release per workgroup instead (buffer_wbl2: the XCD's
+// L2 written back) made band 3's blend 44 -> 57 us; the totals in a
+// one-workgroup kernel after the blend cost 8.6 us more per frame than here.
+__device__ __forceinline__ void direct_finish(const FrameParams& fp, const Buffers& b, int tile, unsigned long long c,
+                                              uint32_t* lds) {
   __shared__ uint32_t s_last;
-  __syncthreads();  // every wave is done with the tile's counter
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned long long c = b.tile_cnt64[tile];
     const uint32_t ref = (uint32_t)(c >> 32);
-    b.tile_cnt64[tile] = 0ull;  // zero for the next frame's projection
-    b.tile_ref[tile] = ref;     // the histogram (reference list lengths)
+    b.tile_cnt64[tile] = 0ull;
     if (b.footer) b.footer[16 + tile] = ref;
-    b.tile_count[tile] = (uint32_t)c;  // the binned length, for the totals
-    const uint32_t tk = __hip_atomic_fetch_add(&b.dir_word[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&b.tile_ref[tile], ref, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&b.tile_count[tile], (uint32_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0);  // both acknowledged before the ticket
+    const uint32_t tk = __hip_atomic_fetch_add(&b.dir_word[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = tk == (uint32_t)fp.n_tiles - 1u ? 1u : 0u;
   }
   __syncthreads();
-  if (s_last) direct_totals(fp, b, lds);
+  if (s_last) {
+    direct_totals<256>(fp, b, lds);
+    if (threadIdx.x == 0) b.dir_word[0] = 0u;
+  }
 }
 
 // HWEXP: GS_FLAG_FAST_EXP (its own kernel: the default path's code is unchanged)
@@ -3922,11 +3953,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
   __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = (int)blockIdx.x;  // (chunks_per_tile == GS_BLEND_WPG, the grid is the band's tiles)
+  const unsigned long long c = threadIdx.x == 0 ? b.tile_cnt64[tile] : 0ull;
   blend_sort_tile<true>(fp, b, tile, reinterpret_cast<unsigned long long*>(lds));
   __syncthreads();
   blend_wave<4, HWEXP, true>(fp, b, tile * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
-  direct_finish(fp, b, tile, lds);
+  direct_finish(fp, b, tile, c, lds);
 }
+
 
 // the lazy big lists' continuation (its own symbol, so profiles tell it from
 // the prefix blend).  A grid-stride loop over the waves of the big lists

@@ -3,10 +3,10 @@
 # library), then band 3 of 8 (config 4) one and three frames in flight:
 # base (direct), classic (GS_X_DIRECT_OFF: the scan and emit), xb5 (classic
 # without the scan and emit launches after the first frames: wrong frames, the
-# bound); all 8 bands for base and classic; then the blend's magic-number
-# exponential (expm) against base on config 3.
+# bound); all 8 bands for base and classic.  (ab4: the totals in a kernel of
+# their own instead of the last blend workgroup's ticket.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
-O=gpurun_out/r6ab3
+O=gpurun_out/r6ab4
 mkdir -p $O
 set -e
 lib() { [ "$1" = base ] && echo "$PWD/gaussian_splat_ipu_amd/lib/libgsplat.so" || echo "$PWD/tmp_ab/$1/libgsplat.so"; }
@@ -24,16 +24,4 @@ done
 for v in base classic; do
   GSPLAT_LIB=$(lib $v) timeout -k 10 400 python3 tools/band_emulate.py --balanced --bands 1,8 --inflight 3 > $O/bands_${v}.jsonl 2> $O/bands_${v}.err
   echo "$v $(tail -n 1 $O/bands_${v}.jsonl | cut -c1-330)"
-done
-GSPLAT_LIB=$(lib expm) timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_expm.txt 2>&1
-tail -n 1 $O/pytest_expm.txt
-for rep in 1 2 3; do
-  for v in base expm; do
-    GSPLAT_LIB=$(lib $v) timeout -k 10 300 python3 bench.py --steps 600 --no-cpu-baseline > $O/bench_${v}_$rep.json 2> $O/bench_${v}_$rep.err
-    python3 - $v $O/bench_${v}_$rep.json <<'PY'
-import json, sys
-d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(sys.argv[1], d["value"], {k: round(1e3 * v["avg_ms"], 1) for k, v in d["kernels"].items()})
-PY
-  done
 done
