@@ -126,10 +126,14 @@ struct gs_renderer {
   bool last_counted = false;   // the last enqueued frame counted its blend records
   uint64_t frame_seq = 0;
   uint64_t x_frames = 0;  // (GS_X_BAND measurement builds only: this renderer's frames)
-  // direct band binning's hint: frames are numbered (FrameParams::frame_seq,
-  // echoed in the host mirror's word 15); cam_first_seq = the first frame
-  // enqueued with the current camera, projection, focal lengths and band
-  uint32_t seq_next = 1, cam_first_seq = 0;
+  // direct band binning: frames are numbered (FrameParams::frame_seq, echoed
+  // in the host mirror's word 15); cam_first_seq = the first frame enqueued
+  // with the current camera, projection, focal lengths and band; layout_seq =
+  // the last frame binned by a scan (its tile_start is the direct frames'
+  // layout; 0 after an overflow); direct_veto: an overflow since then (the
+  // test hook's forced direct frames wait for a scan too)
+  uint32_t seq_next = 1, cam_first_seq = 0, layout_seq = 0;
+  bool direct_veto = false;
   bool cam_key_set = false;
   float cam_key[40] = {0};
   gsr::ProfileSlot ring[gsr::kProfileRing];

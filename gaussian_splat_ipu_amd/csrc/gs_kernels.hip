@@ -699,32 +699,39 @@ __device__ __forceinline__ void agg_count(const FrameParams& fp, const Buffers& 
 }
 
 // FrameParams::bin_direct (row bands): the projection workgroup places its
-// own pairs.  Tile t owns the fixed pair segment [t * tile_cap, (t + 1) *
-// tile_cap); the workgroup's reservation -- the returning add on the tile's
-// counter that agg_count makes (binned | reference << 32) -- is its offset in
-// that segment, so no scan has to run before any pair can be placed and no
-// emit launch follows.  The same three box cases as agg_count (ballots for
-// <= kAggBallot tiles, LDS cursors for <= kAggCap, a returning add per pair
-// beyond), the emit's placement rules (agg_emit_block) inside each.  A pair
-// past its segment is not written and flags the frame (dir_word[1]): the
+// own pairs.  Tile t's pairs go to [tile_start[t], tile_start[t + 1]): the
+// layout the last scan of this view wrote (the same view bins the same
+// lists, so each tile's segment is exactly its list).  The workgroup's
+// reservation -- the returning add on the tile's counter that agg_count makes
+// (binned | reference << 32) -- is its offset in that segment, so no scan
+// has to run before any pair can be placed and no emit launch follows.  The
+// same three box cases as agg_count (ballots for <= kAggBallot tiles, LDS
+// cursors for <= kAggCap, a returning add per pair beyond), the emit's
+// placement rules (agg_emit_block) inside each.  A pair past its segment (or
+// the pair buffer) is not written and flags the frame (dir_word[1]): the
 // blend's last workgroup reports it as the pair-capacity overflow, and the
-// host then bins that renderer's next frames with the scan and emit again.
-// The order of a tile's pairs is set by the atomics, as with agg_emit: the
+// host bins that renderer's next frame with the scan and emit again.  The
+// order of a tile's pairs is set by the atomics, as with agg_emit: the
 // in-blend sort puts every list in its total (z, input index) order.
+__device__ __forceinline__ uint32_t direct_limit(const FrameParams& fp, const Buffers& b, uint32_t t) {
+  const uint32_t en = b.tile_start[t + 1];
+  return (unsigned long long)en < fp.pair_cap ? en : (uint32_t)min(fp.pair_cap, 0xFFFFFFFFull);
+}
+
 __device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers& b, uint2 r, uint2 q,
                                            unsigned long long key) {
   __shared__ uint32_t dcnt[kAggCap];
+  __shared__ uint32_t dlim[kAggCap];
   __shared__ uint32_t d_lo[4], d_hi[4];
   __shared__ uint32_t d_wc[4][kAggBallot];
   const AggBox bx = agg_box(r, d_lo, d_hi);
   if (bx.area == 0) return;  // (uniform)
-  const uint32_t cap = fp.tile_cap;
   const uint32_t x0 = r.x & 0xFFFFu, x1 = r.x >> 16, y0 = r.y & 0xFFFFu, y1 = r.y >> 16;
   const uint32_t u0 = q.x & 0xFFFFu, u1 = q.x >> 16, v0 = q.y & 0xFFFFu, v1 = q.y >> 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   bool ovf = false;
-  auto put = [&](uint32_t t, uint32_t off) {
-    if (off < cap) b.pairs[(size_t)t * cap + off] = key;
+  auto put = [&](uint32_t pos, uint32_t lim) {
+    if (pos < lim) b.pairs[pos] = key;
     else ovf = true;
   };
   if (bx.area <= kAggBallot) {  // (uniform) per tile: ballots of the rectangles covering it
@@ -736,21 +743,23 @@ __device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers&
       if (lane == 0) d_wc[wave][k] = (cr << 16) | cq;
     }
     __syncthreads();
-    if ((int)threadIdx.x < bx.area) {  // the workgroup's offset in the tile, split over its waves
+    if ((int)threadIdx.x < bx.area) {  // the workgroup's slots in the tile, split over its waves
       const int k = threadIdx.x;
       const uint32_t w0 = d_wc[0][k], w1 = d_wc[1][k], w2 = d_wc[2][k], w3 = d_wc[3][k];
       const uint32_t v = w0 + w1 + w2 + w3;
-      uint32_t base = 0u;
+      uint32_t base = 0u, lim = 0u;
       if (v) {
-        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
-        base = (uint32_t)atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x],
-                                   ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
+        const uint32_t t = (uint32_t)((bx.y0 + k / bx.w) * fp.tiles_x + bx.x0 + k % bx.w);
+        const uint32_t st = b.tile_start[t];
+        lim = direct_limit(fp, b, t);
+        base = st + (uint32_t)atomicAdd(&b.tile_cnt64[t], ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
       }
       const uint32_t c0 = w0 & 0xFFFFu, c1 = w1 & 0xFFFFu, c2 = w2 & 0xFFFFu;
       d_wc[0][k] = base;
       d_wc[1][k] = base + c0;
       d_wc[2][k] = base + c0 + c1;
       d_wc[3][k] = base + c0 + c1 + c2;
+      dlim[k] = lim;
     }
     __syncthreads();
     const unsigned long long lt = (1ull << lane) - 1ull;
@@ -758,7 +767,7 @@ __device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers&
       const uint32_t tx = (uint32_t)(bx.x0 + k % bx.w), ty = (uint32_t)(bx.y0 + k / bx.w);
       const bool in_q = u0 <= tx && tx <= u1 && v0 <= ty && ty <= v1;
       const unsigned long long m = ballot64(in_q);
-      if (in_q) put(ty * (uint32_t)fp.tiles_x + tx, d_wc[wave][k] + (uint32_t)__popcll(m & lt));
+      if (in_q) put(d_wc[wave][k] + (uint32_t)__popcll(m & lt), dlim[k]);
     }
   } else if (bx.area > kAggCap) {  // (uniform) spread-out workgroup: a returning add per pair
     if (x0 <= x1)
@@ -766,8 +775,10 @@ __device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers&
         const bool yin = v0 <= y && y <= v1;
         for (uint32_t x = x0; x <= x1; ++x) {
           const uint32_t t = y * fp.tiles_x + x;
-          if (yin && u0 <= x && x <= u1) put(t, (uint32_t)atomicAdd(&b.tile_cnt64[t], (1ull << 32) | 1ull));
-          else atomicAdd(&b.tile_cnt64[t], 1ull << 32);
+          if (yin && u0 <= x && x <= u1)
+            put(b.tile_start[t] + (uint32_t)atomicAdd(&b.tile_cnt64[t], (1ull << 32) | 1ull), direct_limit(fp, b, t));
+          else
+            atomicAdd(&b.tile_cnt64[t], 1ull << 32);
         }
       }
   } else {  // LDS histogram of the box, one returning add per (workgroup, tile), LDS cursors
@@ -785,13 +796,15 @@ __device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers&
     __syncthreads();
     for (int k = threadIdx.x; k < bx.area; k += 256) {
       const uint32_t v = dcnt[k];
-      uint32_t base = 0u;
+      uint32_t base = 0u, lim = 0u;
       if (v) {
-        const int y = bx.y0 + k / bx.w, x = bx.x0 + k % bx.w;
-        base = (uint32_t)atomicAdd(&b.tile_cnt64[y * fp.tiles_x + x],
-                                   ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
+        const uint32_t t = (uint32_t)((bx.y0 + k / bx.w) * fp.tiles_x + bx.x0 + k % bx.w);
+        const uint32_t st = b.tile_start[t];
+        lim = direct_limit(fp, b, t);
+        base = st + (uint32_t)atomicAdd(&b.tile_cnt64[t], ((unsigned long long)(v >> 16) << 32) | (v & 0xFFFFu));
       }
       dcnt[k] = base;  // the workgroup's cursor in the tile's segment
+      dlim[k] = lim;
     }
     __syncthreads();
     // a run of equal (reference, binned) rectangles takes its slots of each
@@ -806,7 +819,7 @@ __device__ __forceinline__ void agg_direct(const FrameParams& fp, const Buffers&
         for (uint32_t x = u0; x <= u1; ++x) {
           uint32_t base = 0u;
           if (start) base = atomicAdd(&dcnt[row + (int)x], len);
-          put(y * (uint32_t)fp.tiles_x + x, (uint32_t)__shfl((int)base, lead, 64) + rank);
+          put((uint32_t)__shfl((int)base, lead, 64) + rank, dlim[row + (int)x]);
         }
       }
   }
@@ -1875,10 +1888,13 @@ __global__ __launch_bounds__(256) void gs_emit_kernel(FrameParams fp, Buffers b)
 template <bool DIRECT = false>
 __device__ __forceinline__ void tile_segment(const FrameParams& fp, const Buffers& b, int t,
                                              uint32_t& s, uint32_t& L) {
-  if constexpr (DIRECT) {
+  if constexpr (DIRECT) {  // (the segment of the view's last scan; the list this frame placed in it)
     const uint32_t c = (uint32_t)b.tile_cnt64[t];
-    s = (uint32_t)t * fp.tile_cap;
-    L = c < fp.tile_cap ? c : fp.tile_cap;
+    const uint32_t en = direct_limit(fp, b, (uint32_t)t);
+    uint32_t st = b.tile_start[t];
+    if (st > en) st = en;
+    s = st;
+    L = c < en - st ? c : en - st;
     return;
   }
   uint32_t st = b.tile_start[t], en = b.tile_start[t + 1];
@@ -3844,7 +3860,7 @@ __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffe
       nsm += w32[5 * w + 3];
       v += w32[5 * w + 4];
     }
-    const bool ovf = b.dir_word[1] != 0u || m > fp.tile_cap || tot > fp.pair_cap;
+    const bool ovf = b.dir_word[1] != 0u || tot > fp.pair_cap;
     const uint4 c0 = make_uint4(nbg, 0u, v, ovf ? 1u : 0u);
     const uint4 c1 = make_uint4(m, (uint32_t)tot, (uint32_t)(tot >> 32), nmd);
     const uint4 c2 = make_uint4(0u, nsm, (uint32_t)rtot, (uint32_t)(rtot >> 32));
@@ -3881,6 +3897,18 @@ __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffe
 // one-workgroup kernel after the blend cost 8.6 us more per frame than here.
 __device__ __forceinline__ void direct_finish(const FrameParams& fp, const Buffers& b, int tile, unsigned long long c,
                                               uint32_t* lds) {
+#ifndef GS_X_DIRECT_FIN
+#define GS_X_DIRECT_FIN 0
+#endif
+#if GS_X_DIRECT_FIN  // (measurement builds, wrong stats: 1 no ticket or totals; 2 nor the barrier)
+  if (GS_X_DIRECT_FIN == 1) __syncthreads();
+  if (threadIdx.x == 0) {
+    b.tile_cnt64[tile] = 0ull;
+    b.tile_ref[tile] = (uint32_t)(c >> 32);
+    b.tile_count[tile] = (uint32_t)c;
+  }
+  return;
+#endif
   __shared__ uint32_t s_last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -3944,15 +3972,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
 }
 
 // The blend with the sort inside for a direct-binned band (FrameParams::
-// bin_direct): the same workgroup per tile, the tile's pairs from its fixed
-// segment, then direct_finish.  Its own symbol (the other kernels keep their
+// bin_direct): a workgroup per tile, the tile's pairs from its segment, then
+// direct_finish.  Its own symbol (the other kernels keep their
 // code; profiles tell it apart).
 template <bool HWEXP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WPE, 8))) void gs_blend_direct_kernel(FrameParams fp, Buffers b) {
   GS_PROBE_SCOPE(kPrBlend);
   __shared__ __attribute__((aligned(16))) uint32_t lds[kBlendLdsWords];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tile = (int)blockIdx.x;  // (chunks_per_tile == GS_BLEND_WPG, the grid is the band's tiles)
+  // (chunks_per_tile == GS_BLEND_WPG; tile order: the longest-lists-first
+  // order of the view's last scan took band 3's pipelined frame 28.7 -> 33.5 us)
+  const int tile = (int)blockIdx.x;
   const unsigned long long c = threadIdx.x == 0 ? b.tile_cnt64[tile] : 0ull;
   blend_sort_tile<true>(fp, b, tile, reinterpret_cast<unsigned long long*>(lds));
   __syncthreads();

@@ -92,12 +92,12 @@ struct FrameParams {
   float inv_tw, inv_th, inv_sd;  // 1 / tw, 1 / th, 1 / fxy[1]   (pow2 only)
   int sh_tw, sh_th, sh_stride;   // log2 tile_w, tile_h, band_stride (pow2 only)
   // (appended last, so the other kernels' argument offsets stay as they were)
-  int bin_direct;     // (bin_agg row bands with the sort in the blend) each tile owns the fixed
-                      //   pair segment [t * tile_cap, (t + 1) * tile_cap): the projection's
-                      //   workgroups place their pairs there at once (no scan, no emit
-                      //   launch); the blend's workgroups read the lengths from the tile
-                      //   counters, reset them, and the last one writes the frame counters
-  unsigned int tile_cap;  // (bin_direct) pairs per tile segment
+  int bin_direct;     // (bin_agg row bands with the sort in the blend) tile t's pairs go to
+                      //   [tile_start[t], tile_start[t + 1]) as the view's last scan laid
+                      //   them out: the projection's workgroups place them at once (no
+                      //   scan, no emit launch); the blend's workgroups read the lengths
+                      //   from the tile counters, reset them, and the last one writes the
+                      //   frame counters
   unsigned int frame_seq;  // the renderer's frame number (1, 2, ...): the aggregated binning's
                            //   host mirror word 15, which frame its counters are from
 };

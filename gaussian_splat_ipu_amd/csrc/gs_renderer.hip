@@ -334,7 +334,6 @@ gsk::FrameParams make_params(const gs_renderer* r) {
   // the sort launch (which sorts every list when big_separate is off)
   fp.blend_seg = (fp.blend_px2 && !fp.big_separate) ? 1 : 0;
   fp.bin_direct = 0;
-  fp.tile_cap = 0;
   fp.fast_exp = (r->cfg.flags & GS_FLAG_FAST_EXP) ? 1 : 0;
   fp.sh_degree = r->d_sh ? r->sh_degree : -1;
   camera_position(r->view_rm, fp.campos);
@@ -510,34 +509,30 @@ int ensure_cov(gs_renderer* r, const gsk::FrameParams& fp, hipStream_t s) {
   return GS_OK;
 }
 
-// Direct band binning (round 6): a row band whose tiles the aggregated
-// binning and the in-blend sort serve (gs_project_direct, gs_blend_direct)
-// gives each tile a fixed segment of the pair buffer, pair_cap / n_tiles
-// pairs, and its projection places the pairs there itself: the scan and emit
-// launches leave the band's chain.  Taken when the renderer has completed a
-// frame of the same camera, projection, focal lengths and band (the mapped
-// counters' word 15 names the frame they are from) whose longest binned list
-// fits a segment -- the same view bins the same lists, so such a frame cannot
-// overflow.  The first frame of a view takes the scan and emit.  A frame that
-// does overflow (only a forced segment size can) drops the pairs past the
-// segment, reports GS_EOVERFLOW like a pair-buffer overflow, and its longest
-// list, counted in full, sends the next frames back.  Test hook (gs_test_set
-// "bin_direct"): 0 off, >= 64 forced on with that segment size.
+// Direct band binning (FrameParams::bin_direct).  A row band whose camera,
+// projection, focal lengths and band have not changed since a frame binned
+// by the scan and emit has completed bins the same lists again: each tile's
+// pairs then go straight to that frame's segment of the pair buffer
+// (tile_start, left by the scan), placed by the projection itself, and the
+// scan and emit launches leave the band's chain.  The first frame of a view
+// (and any frame enqueued before one of its view has completed) takes the
+// scan and emit.  A direct frame whose pairs do not fit their segments (only
+// the test hook's forced frames can) drops the pairs past them and reports
+// GS_EOVERFLOW like a pair-buffer overflow; the next frame takes the scan.
+// Test hook (gs_test_set "bin_direct"): 0 off, > 0 forced on (the first
+// frame too, into whatever layout tile_start holds) until an overflow.
 void choose_direct(const gs_renderer* r, gsk::FrameParams& fp) {
   fp.bin_direct = 0;
-  fp.tile_cap = 0;
   const int64_t hook = GS_X_DIRECT_OFF ? 0 : g_test_bin_direct.load();  // (measurement builds: off)
   if (hook == 0 || !fp.blend_sort || fp.lazy || r->bin_global || r->n_tiles <= 0 || !r->buf.dir_word ||
       !r->h_counters || gsk::project_kind(fp, r->buf) != 2)  // (2: the row band's projection)
     return;
-  const uint64_t seg = hook > 0 ? (uint64_t)hook : ((r->pair_cap / (uint64_t)r->n_tiles) & ~63ull);
   const volatile uint32_t* h = (const volatile uint32_t*)r->h_counters;
-  const uint32_t hseq = h[15], hint = h[4];
-  const bool known = hseq != 0 && (int32_t)(hseq - r->cam_first_seq) >= 0;  // a completed frame of this view
-  const bool fits = hook > 0 ? (!known || (uint64_t)hint <= seg) : (known && (uint64_t)hint <= seg);
-  if (seg >= 64 && seg * (uint64_t)r->n_tiles <= r->pair_cap && seg <= 0xFFFFFFFFull && fits) {
+  const uint32_t hseq = h[15];  // the last completed frame
+  const bool known = r->layout_seq != 0 && (int32_t)(r->layout_seq - r->cam_first_seq) >= 0 && hseq != 0 &&
+                     (int32_t)(hseq - r->layout_seq) >= 0;
+  if (hook > 0 ? !r->direct_veto : known) {
     fp.bin_direct = 1;
-    fp.tile_cap = (uint32_t)seg;
     fp.big_separate = 0;  // (the blend's workgroups radix-sort a list > kSortLdsCap themselves)
   }
 }
@@ -563,6 +558,10 @@ int enqueue_frame(gs_renderer* r) {
       r->cam_first_seq = fp.frame_seq;
     }
     choose_direct(r, fp);
+    if (!fp.bin_direct) {  // (this frame's scan lays out the pair buffer)
+      r->layout_seq = fp.frame_seq;
+      r->direct_veto = false;
+    }
   }
   r->last_fp = fp;
   r->have_fp = true;
@@ -727,6 +726,8 @@ int finish_frame(gs_renderer* r) {
   const bool ovf = c[3] != 0 || *sticky != 0;
   *sticky = 0;
   if (ovf) {
+    r->layout_seq = 0;  // (the next frame takes the scan: choose_direct)
+    r->direct_veto = true;
     set_error("pair list overflow: a frame since the last sync binned more pairs than the capacity " +
               std::to_string(r->pair_cap) + " (last frame: " + std::to_string(P) + " pairs)");
     return GS_EOVERFLOW;
@@ -999,6 +1000,9 @@ int create(const gs_gaussian3d* g, size_t n, const gs_config* cfg, const gs_rend
   if ((e = hipMalloc(&r->d_tiles, tiles_bytes)) != hipSuccess) return fail(hip_fail(e, "hipMalloc(tiles)"));
   poison(r->d_tiles, tiles_bytes, "tiles");
   r->buf.tile_start = (uint32_t*)r->d_tiles;
+  // (an empty layout until a scan writes one: a forced direct frame before
+  // any scan drops every pair and reports the overflow)
+  if ((e = hipMemset(r->buf.tile_start, 0, (T + 1) * 4)) != hipSuccess) return fail(hip_fail(e, "hipMemset(tiles)"));
   r->buf.tile_cursor = r->buf.tile_start + T + 1;
   r->buf.big_tiles = r->buf.tile_cursor + T;
   r->buf.medium_tiles = r->buf.big_tiles + T;
@@ -1407,8 +1411,8 @@ int gs_test_set(const char* key, int64_t value) {
     gsr::g_test_poison.store(value);
   } else if (k == "cov_cache" && (value == -1 || value == 0)) {
     gsr::g_test_cov_cache.store(value);
-  } else if (k == "bin_direct" && (value == -1 || value == 0 || value >= 64)) {
-    gsr::g_test_bin_direct.store(value);  // -1: default; 0: off; >= 64: on, with this segment size
+  } else if (k == "bin_direct" && (value == -1 || value == 0 || value == 1)) {
+    gsr::g_test_bin_direct.store(value);  // -1: default; 0: off; 1: forced on until an overflow
   } else {
     gsh::set_error("gs_test_set: unknown key or value");
     return GS_EINVAL;

@@ -233,6 +233,10 @@ def test_committed_lines_use_the_survey_terms():
     (8, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_PROJ_BAND),
     (4, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_PROJ_BAND),
     (2, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_PROJ_BAND),
+    # a band renderer's frames after its first (direct binning: no scan or emit launch)
+    (8, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_BIN_DIRECT),
+    (4, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_BIN_DIRECT),
+    (2, bench.PATH_BIN_AGG | bench.PATH_BLEND_SORT | bench.PATH_BIN_DIRECT),
     (1, bench.PATH_BLEND_PX2),  # bench.py --gather: the one-GPU group renders the whole frame as band 0 of 1
 ])
 def test_group_line_shapes_resolve_traffic_and_valu(bands, paths):

@@ -716,13 +716,13 @@ PATH_BIN_DIRECT = 128  # (gs_frame_stats.paths, ABI 14)
 @pytest.mark.parametrize("band_count,band_index", [(8, 3), (3, 1), (8, 0)])  # (8, 0): no Gaussian reaches it
 def test_direct_binning_bit_exact(pc12, test_hook, band_count, band_index):
     """A row band's direct binning (round 6; band-culled bands, the bench's and
-    the group's): each tile owns a fixed segment
-    of the pair buffer and the projection places the pairs there itself (no
-    scan, no emit launch; the blend's workgroups write the histogram and the
-    frame counters).  The renderer's first frame bins with the scan and emit
-    (no completed frame to size the segments from); the next ones take the
-    direct path, and frames, histograms and stats stay the oracle's bit for
-    bit.  Forced off (hook 0), the same frames take the scan and emit."""
+    the group's): a view's frames after its first completed one place their
+    pairs straight into the segments that frame's scan laid out (no scan, no
+    emit launch; the blend's workgroups write the histogram and the frame
+    counters).  The renderer's first frame bins with the scan and emit; the
+    next ones take the direct path, and frames, histograms and stats stay the
+    oracle's bit for bit.  Forced off (hook 0), the same frames take the scan
+    and emit."""
     from gaussian_splat_ipu_amd import camera
     from gaussian_splat_ipu_amd.splatter import GpuSplatter
     from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
@@ -754,12 +754,12 @@ def test_direct_binning_bit_exact(pc12, test_hook, band_count, band_index):
 
 
 def test_direct_binning_overflow_falls_back(pc12, test_hook):
-    """A direct frame whose tile segments are too small (forced 64 pairs):
-    the dropped pairs flag the frame, the blocking render reports the
-    overflow to itself and renders again, and the longest list the flagged
-    frame counted in full sends it to the scan and emit: the frame the caller
-    gets is the oracle's, and async frames that overflow report
-    GS_EOVERFLOW at sync."""
+    """A direct frame whose tile segments do not hold its lists (forced on
+    before any scan has laid out the pair buffer: every segment empty): the
+    dropped pairs flag the frame, the blocking render reports the overflow to
+    itself and renders again with the scan and emit: the frame the caller
+    gets is the oracle's, and async frames that overflow report GS_EOVERFLOW
+    at sync."""
     from gaussian_splat_ipu_amd import camera
     from gaussian_splat_ipu_amd._lib import GsError
     from gaussian_splat_ipu_amd.splatter import GpuSplatter
@@ -772,17 +772,16 @@ def test_direct_binning_overflow_falls_back(pc12, test_hook):
     fb = TiledFramebuffer(W, H, 16, 16)
     ty0, ty1, _, _ = fb.band_rows(8)[3]
     f = O.make_frame(view, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0, band=(ty0, ty1))
-    test_hook("bin_direct", 64)
+    test_hook("bin_direct", 1)
     s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23, band_cull=True)
     s.set_view_wire(view)
     s.set_projection_wire(proj)
     s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
-    s.execute()  # (forced direct with 64-pair segments: overflows, then the scan and emit)
-    assert s.stats()["max_list"] > 64
+    s.execute()  # (forced direct into the empty layout: overflows, then the scan and emit)
     assert not s.stats()["paths"] & PATH_BIN_DIRECT
     _assert_parity(s, f, g, check_proj=False, band_culled=True)
     s.close()
-    # async: the first frame of a fresh renderer overflows its forced segments
+    # async: the first frame of a fresh renderer overflows the empty layout
     s = GpuSplatter(g, fb, device=0, band_index=3, band_count=8, pair_capacity=1 << 23, band_cull=True)
     s.set_view_wire(view)
     s.set_projection_wire(proj)
@@ -793,6 +792,49 @@ def test_direct_binning_overflow_falls_back(pc12, test_hook):
     s.execute()  # a blocking frame after it: the oracle's
     _assert_parity(s, f, g, check_proj=False, band_culled=True)
     s.close()
+
+
+def test_direct_binning_follows_the_view(pc12):
+    """Direct frames reuse the layout of their view's last scan: a view
+    change (and a band move) sends the next frames to the scan and emit until
+    one of the new view's frames has completed, with frames of the old view
+    still in flight; every frame is the oracle's."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+    from oracle import oracle as O
+
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    view2 = view.copy()
+    view2[3] += np.float32(0.05)
+    fb = TiledFramebuffer(W, H, 16, 16)
+    ref = {}
+    for k, v in (("a", view), ("b", view2)):
+        for rows in ((27, 36), (20, 30)):
+            f = O.make_frame(v, proj, W, H, 16, 16, camera.FOV_DEFAULT, 1.0, band=rows)
+            r = O.render(g, f)
+            ref[k, rows] = (r["bgr"], r["hist"])
+    with GpuSplatter(g, fb, device=0, band_rows=(0, fb.tiles_down), band_cull=True, pair_capacity=1 << 23) as s:
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        rows = (27, 36)
+        s.set_band_rows(*rows)
+        for k in "aabba" + "M" + "ab":
+            if k == "M":  # the band moves
+                rows = (20, 30)
+                s.set_band_rows(*rows)
+                continue
+            s.set_view_wire(view if k == "a" else view2)
+            s.execute_async()
+            s.execute_async()
+            s.execute()
+            np.testing.assert_array_equal(s.get_frame_buffer(), ref[k, rows][0])
+            s.execute()  # (a frame of this view has completed: direct)
+            assert s.stats()["paths"] & PATH_BIN_DIRECT, (k, rows)
+            np.testing.assert_array_equal(s.get_frame_buffer(), ref[k, rows][0])
+            np.testing.assert_array_equal(s.get_histogram(), ref[k, rows][1])
 
 
 def test_aggregated_binning_4k_clustered(built):

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--contiguous", action="store_true")
     ap.add_argument("--balanced", action="store_true", help="work-balanced contiguous bands (bench.py's N > 1 default)")
+    ap.add_argument("--tile-cost", type=float, default=64.0,
+                    help="--balanced: the fixed work per tile of a row, in pairs (dist.row_work)")
     ap.add_argument("--no-cull", action="store_true")
     ap.add_argument("--bin-global", action="store_true", help="the bands bin with global atomics")
     ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
@@ -77,13 +79,13 @@ def main():
         cal.close()
     for N in [int(v) for v in a.bands.split(",")]:
         per_band, stages, host = [], [], []
-        bands = gdist.balanced_bands(gdist.row_work(hist, fb), N) if hist is not None and N > 1 else None
+        bands = gdist.balanced_bands(gdist.row_work(hist, fb, a.tile_cost), N) if hist is not None and N > 1 else None
         pad = max(t1 - t0 for t0, t1 in bands) if bands else 0
         # the group's policy: frame k renders with the split cut at frame
         # 8 (k // 8) from the footers of 4 frames before it
         view_bands = None
         if view_hist is not None and N > 1:
-            view_bands = [gdist.balanced_bands(gdist.row_work(h, fb), N) for h in view_hist]
+            view_bands = [gdist.balanced_bands(gdist.row_work(h, fb, a.tile_cost), N) for h in view_hist]
             pad = fb.tiles_down
         for r in range(N):
             if a.only_band >= 0 and r != a.only_band:

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round 6: the measurement set for direct band binning (the in-tree library)
+# Round 6 (ab7): direct band binning into the layout of the view's last scan
 # against classic (tmp_ab/classic: GS_X_DIRECT_OFF, the scan and emit):
 # GPU suite + smoke, band 3 of 8 (config 4) one and three frames in flight,
 # 1- and 8-band splits, a kernel trace of band 3, PMC summaries of the band
 # shapes (pmc_bands.sh), and the bench's default and --gather lines.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
-O=gpurun_out/r6direct
+O=gpurun_out/r6ab7
 mkdir -p $O
 set -e
 export TMPDIR=/tmp
@@ -26,10 +26,6 @@ for v in base classic; do
   GSPLAT_LIB=$(lib $v) timeout -k 10 400 python3 tools/band_emulate.py --balanced --bands 1,8 --inflight 3 > $O/bands_${v}.jsonl 2> $O/bands_${v}.err
   echo "$v $(tail -n 1 $O/bands_${v}.jsonl | cut -c1-400)"
 done
-for tc in 128 192 256; do
-  timeout -k 10 300 python3 tools/band_emulate.py --balanced --bands 8 --inflight 3 --tile-cost $tc > $O/bands_tc$tc.jsonl 2> $O/bands_tc$tc.err
-  echo "tile cost $tc $(tail -n 1 $O/bands_tc$tc.jsonl | cut -c1-330)"
-done
 for v in base classic; do
   GSPLAT_LIB=$(lib $v) timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$v -o band3 -- python3 $EMU --inflight 3 > $O/prof_$v.log 2>&1
   f=$(find $O/prof_$v -name '*kernel_stats.csv' | head -n 1)
@@ -37,17 +33,5 @@ for v in base classic; do
 import csv, sys
 for r in list(csv.DictReader(open(sys.argv[1])))[:8]:
     print(f'{r["Name"][:70]:70s} {int(r["Calls"]):6d} {float(r["AverageNs"])/1e3:8.2f} us')
-PY
-done
-SHAPES="bands1 bands2 bands4 bands8" timeout -k 10 900 bash tools/r6/pmc_bands.sh > $O/pmc_bands.txt 2>&1 || { tail -n 20 $O/pmc_bands.txt; exit 1; }
-tail -n 1 $O/pmc_bands.txt
-cp gpurun_out/pmcb/pmc_bands.json $O/pmc_bands.json
-timeout -k 10 300 python3 bench.py --pmc-json $O/pmc_bands.json > $O/bench_default.json 2> $O/bench_default.err
-timeout -k 10 300 python3 bench.py --gather --no-cpu-baseline --pmc-json $O/pmc_bands.json > $O/bench_gather.json 2> $O/bench_gather.err
-for f in default gather; do python3 - $O/bench_$f.json $f <<'PY'
-import json, sys
-d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-r = d["roofline"]
-print(sys.argv[2], d["value"], d["ms_per_step"], r.get("kernel"), r.get("frac"), "traffic", r.get("traffic"), "valu", r.get("valu_issue_frac"))
 PY
 done
