@@ -59,7 +59,7 @@ namespace gsg {
 
 namespace {
 
-constexpr double kTileCost = 64.0;   // fixed work per tile of a row (dist.row_work)
+constexpr double kTileCost = 128.0;  // fixed work per tile of a row, in pairs (dist.row_work)
 constexpr double kRebalanceGain = 0.97;  // switch splits only if the slowest band gains > 3 %
 constexpr uint64_t kRebalanceEvery = 8;  // frames between re-balancing decisions
 constexpr int kMaxInFlight = 8;

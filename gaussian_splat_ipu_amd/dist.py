@@ -62,10 +62,12 @@ def extract_band(frame: np.ndarray, fb: TiledFramebuffer, world: int, rank: int,
     return out
 
 
-def row_work(hist: np.ndarray, fb: TiledFramebuffer, tile_cost: float = 64.0) -> np.ndarray:
+def row_work(hist: np.ndarray, fb: TiledFramebuffer, tile_cost: float = 128.0) -> np.ndarray:
     """Work per tile row from a frame's tile histogram (list lengths): the
     pairs of the row (sort + blend work) plus a fixed cost per tile (its blend
-    waves and queue slots)."""
+    workgroup; gs_group.hip kTileCost).  128 pairs per tile since round 6: 8
+    balanced bands of config 4, three frames in flight, slowest band 34.9 µs
+    at 64, 31.8 at 128, 32.1 at 192, 32.2 at 256 (profiles/r06_direct/)."""
     h = np.asarray(hist, np.float64).reshape(fb.tiles_down, fb.tiles_across)
     return h.sum(1) + tile_cost * fb.tiles_across
 

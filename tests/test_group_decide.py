@@ -79,7 +79,7 @@ def test_identical_footers_identical_decisions(built):
     from gaussian_splat_ipu_amd import dist
 
     hist = np.concatenate([foot[r, 16:16 + (bounds[r + 1] - bounds[r]) * tx] for r in range(world)]).astype(np.float64)
-    w = hist.reshape(ty, tx).sum(1) + 64.0 * tx
+    w = hist.reshape(ty, tx).sum(1) + 128.0 * tx
     want = dist.balanced_bands(w, world)
     assert [b0 for b0, _ in want] + [ty] == nb
 
