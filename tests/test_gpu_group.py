@@ -138,6 +138,29 @@ def test_emulated_bands_orbit_rebalance(clustered, G, F):
         assert len(splits) > 1  # the split followed the camera
 
 
+def test_emulated_bands_direct_binning(clustered):
+    """A group's band renderers bin a repeated view directly (round 6: the
+    pairs go into the layout of the view's last scan; no scan or emit launch;
+    the blend's last workgroup writes the footer's counters): the gathered
+    frames, histograms and counts stay the oracle's."""
+    from gaussian_splat_ipu_amd import camera
+
+    g, bb = clustered
+    W, H, T = 960, 540, 16
+    view, proj = camera.headless(bb, W, H)
+    f, ref = _oracle(g, view, proj, W, H, T)
+    with _group(g, W, H, T, num_gpus=4, device_ids=[0] * 4, frames_in_flight=2, rebalance=False) as s:
+        s.set_projection_wire(proj)
+        s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+        s.set_view_wire(view)
+        paths = []
+        for _ in range(6):
+            s.execute()
+            paths.append(s.stats()["paths"])
+            _check(s, g, f, ref, lists=False)
+        assert not paths[0] & 128 and paths[-1] & 128, paths  # (GS_PATH_BIN_DIRECT)
+
+
 def test_emulated_bands_async_pipeline(synth):
     """gs_render_async of several views, one sync: the last frame is the last
     view's frame (the pipeline keeps F frames in flight)."""
