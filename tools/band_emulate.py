@@ -28,8 +28,8 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--contiguous", action="store_true")
     ap.add_argument("--balanced", action="store_true", help="work-balanced contiguous bands (bench.py's N > 1 default)")
-    ap.add_argument("--tile-cost", type=float, default=64.0,
-                    help="--balanced: the fixed work per tile of a row, in pairs (dist.row_work)")
+    ap.add_argument("--tile-cost", type=float, default=128.0,
+                    help="--balanced: the fixed work per tile of a row, in pairs (dist.row_work's default)")
     ap.add_argument("--no-cull", action="store_true")
     ap.add_argument("--bin-global", action="store_true", help="the bands bin with global atomics")
     ap.add_argument("--only-band", type=int, default=-1, help="time just this band (profiling)")
