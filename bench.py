@@ -111,6 +111,15 @@ PATH_PROJ_BAND, PATH_PROJ_ANY = 32, 64  # (ABI 13: which projection instantiatio
 PATH_BIN_DIRECT = 128  # (ABI 14: a row band's direct binning -- no scan, no emit launch)
 
 
+def binning_of(paths: int, bin_global: bool = False) -> str:
+    """A frame's binning path, in words (gs_frame_stats.paths)."""
+    if paths & PATH_BIN_DIRECT:
+        return "direct: pairs placed by the projection into the layout of this view's last scan (no scan, no emit)"
+    if paths & PATH_BIN_AGG:
+        return "aggregated: counted in the projection, one-workgroup scan, emit"
+    return "global atomics" if bin_global else "chunked: count, column scan, multi scan, emit"
+
+
 def stage_kernels(stage: str, paths: int, bin_global: bool = False) -> list:
     """[(rocprof short name, launches per frame)] of the kernels a timed stage
     launched, from the frame's gs_frame_stats.paths (gs_kernels.hip launch_*):
@@ -837,6 +846,9 @@ def main():
                 "parallelism": par,
                 "bands": bands,
                 "pmc_key": pmc_key,
+                # (the last timed frame's binning; a fixed camera's band frames after the first
+                # place their pairs into the layout of that view's last scan: DESIGN.md section 4)
+                "binning": binning_of(int(st["paths"]), bool(st.get("bin_global"))),
             },
             "frame": {k: st[k] for k in ("n_rendered", "n_pairs", "n_pairs_binned", "max_list", "n_tiles",
                                          "n_big_tiles", "paths", "bin_global")},
