@@ -3984,9 +3984,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_BLEND_WP
   // order of the view's last scan took band 3's pipelined frame 28.7 -> 33.5 us)
   const int tile = (int)blockIdx.x;
   const unsigned long long c = threadIdx.x == 0 ? b.tile_cnt64[tile] : 0ull;
-  blend_sort_tile<true>(fp, b, tile, reinterpret_cast<unsigned long long*>(lds));
+#ifndef GS_X_DSPLIT
+#define GS_X_DSPLIT 0
+#endif
+  // (GS_X_DSPLIT measurement builds, wrong frames: 1 no sort, 2 no blend walk)
+  if (GS_X_DSPLIT != 1) blend_sort_tile<true>(fp, b, tile, reinterpret_cast<unsigned long long*>(lds));
   __syncthreads();
-  blend_wave<4, HWEXP, true>(fp, b, tile * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
+  if (GS_X_DSPLIT != 2)
+    blend_wave<4, HWEXP, true>(fp, b, tile * GS_BLEND_WPG + wave, reinterpret_cast<float4(*)[64]>(lds) + 3 * wave);
   direct_finish(fp, b, tile, c, lds);
 }
 
