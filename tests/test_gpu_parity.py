@@ -794,6 +794,34 @@ def test_direct_binning_overflow_falls_back(pc12, test_hook):
     s.close()
 
 
+def test_direct_binning_fast_exp_same_frame(pc12, test_hook):
+    """GS_FLAG_FAST_EXP band renderers take the direct binning too (its own
+    blend instantiation): the direct frames are bit-identical to the same
+    renderer's frames binned by the scan and emit."""
+    from gaussian_splat_ipu_amd import camera
+    from gaussian_splat_ipu_amd.splatter import GpuSplatter
+    from gaussian_splat_ipu_amd.tiles import TiledFramebuffer
+
+    g, bb = pc12
+    W, H = 1920, 1080
+    view, proj = camera.headless(bb, W, H)
+    fb = TiledFramebuffer(W, H, 16, 16)
+    out = {}
+    for hook in (-1, 0):
+        test_hook("bin_direct", hook)
+        with GpuSplatter(g, fb, device=0, band_index=3, band_count=8, band_cull=True, fast_exp=True) as s:
+            s.set_view_wire(view)
+            s.set_projection_wire(proj)
+            s.update_focal_lengths(camera.FOV_DEFAULT, 1.0)
+            s.execute()
+            s.execute()
+            assert bool(s.stats()["paths"] & PATH_BIN_DIRECT) == (hook != 0)
+            out[hook] = (s.get_rgba(), s.get_frame_buffer(), s.get_histogram())
+    assert_same_bits(out[-1][0], out[0][0], "fast-exp RGBA, direct against scan")
+    np.testing.assert_array_equal(out[-1][1], out[0][1])
+    np.testing.assert_array_equal(out[-1][2], out[0][2])
+
+
 def test_direct_binning_follows_the_view(pc12):
     """Direct frames reuse the layout of their view's last scan: a view
     change (and a band move) sends the next frames to the scan and emit until
