@@ -3818,12 +3818,13 @@ __device__ __forceinline__ void direct_totals(const FrameParams& fp, const Buffe
       n_small += (t0 + j * NT < T && L <= kSortRegCap) ? 1u : 0u;
     }
   }
-  for (int k0 = tid; k0 < nb; k0 += 4 * NT) {
-    uint32_t vr[4];
+  // (16 loads in flight per thread: 1M Gaussians' 3 907 block counts in one round)
+  for (int k0 = tid; k0 < nb; k0 += 16 * NT) {
+    uint32_t vr[16];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vr[j] = k0 + j * NT < nb ? b.block_rendered[k0 + j * NT] : 0u;
+    for (int j = 0; j < 16; ++j) vr[j] = k0 + j * NT < nb ? b.block_rendered[k0 + j * NT] : 0u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vis += vr[j];
+    for (int j = 0; j < 16; ++j) vis += vr[j];
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) {
