@@ -256,3 +256,12 @@ def test_group_line_shapes_resolve_traffic_and_valu(bands, paths):
     cpi = json.load(open(os.path.join(ROOT, "profiles", "valu_cpi.json")))
     cyc, used = bench.stage_valu_cycles("blend", paths, kernels, cpi)
     assert cyc is not None and cyc > 0, (key, used)
+
+
+def test_binning_named_from_the_frame_paths():
+    """The line's config.binning follows gs_frame_stats.paths (a fixed view's
+    band frames after the first take the direct binning)."""
+    assert bench.binning_of(bench.PATH_BIN_AGG | bench.PATH_BIN_DIRECT).startswith("direct")
+    assert bench.binning_of(bench.PATH_BIN_AGG).startswith("aggregated")
+    assert bench.binning_of(bench.PATH_BLEND_PX2).startswith("chunked")
+    assert bench.binning_of(0, bin_global=True) == "global atomics"
